@@ -1,0 +1,60 @@
+"""Pin the oracle restatement against fixtures produced by running the reference module itself
+(oracle/gen_golden.py).  CPU only."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+
+
+def _load(name):
+    return dict(np.load(os.path.join(GOLDEN, name + ".npz")))
+
+
+def test_fixture_weights_unchanged(state_dict, text_table):
+    from athd.weights import weights_checksum
+    meta = _load("meta")
+    assert np.allclose(meta["weights_checksum"], weights_checksum(state_dict), rtol=1e-12)
+    assert np.array_equal(meta["text_table"], text_table)
+
+
+@pytest.mark.parametrize("name", ["b1_t44100_vocals", "b2_t30000_drums_bass", "b1_t1500_other"])
+def test_oracle_matches_reference_fixture(oracle_model, text_table, name):
+    g = _load(name)
+    wav = torch.as_tensor(g["wav"])
+    te = torch.as_tensor(text_table[g["prompt_idx"]])
+    if te.shape[0] != wav.shape[0]:
+        te = te.expand(wav.shape[0], -1)
+    cap = {}
+    out = oracle_model.forward(wav, te, capture=cap).numpy()
+    ref = g["out"]
+    assert out.shape == ref.shape
+    err = np.abs(out - ref).max()
+    rms = np.sqrt(np.mean(ref ** 2))
+    assert err <= 1e-5 * max(rms, 1e-3), (err, rms)
+    if "x_cond" in g:
+        for k in ("x_enc", "xt_enc", "x_cond", "xt_cond"):
+            a, b = cap[k].numpy(), g[k]
+            assert np.abs(a - b).max() <= 1e-5 * max(1.0, np.abs(b).max()), k
+
+
+def test_oracle_full_length_stats(oracle_model, text_table):
+    g = _load("b1_t264600_vocals")
+    wav = torch.as_tensor(g["wav"])
+    te = torch.as_tensor(text_table[g["prompt_idx"]])
+    out = oracle_model.forward(wav, te).numpy()
+    assert tuple(out.shape) == tuple(g["out_shape"])
+    sub = out[..., ::97]
+    assert np.abs(sub - g["out_stride97"]).max() <= 1e-5 * max(1e-3, np.sqrt(np.mean(sub ** 2)))
+
+
+def test_forward_prompts_equals_per_prompt_forward(oracle_model, text_table):
+    from athd.synth import synthetic_batch
+    wav = torch.as_tensor(synthetic_batch(2, 9000))
+    tt = torch.as_tensor(text_table)
+    multi = oracle_model.forward_prompts(wav, tt)
+    for p in range(4):
+        single = oracle_model.forward(wav, tt[p:p + 1].expand(2, -1))
+        assert torch.allclose(multi[:, p], single, atol=1e-6)
