@@ -1,0 +1,161 @@
+"""`AudioTextHTDemucs` - drop-in for the reference model class (`ATHTDemucs_v2.py:141-326`) on MI355X.
+
+Same construction and call surface that `test_inference.load_model` / `benchmark.OurModel` use
+(`test_inference.py:21-40`, `benchmark.py:125-153,175`):
+
+    model = AudioTextHTDemucs(htdemucs, clap, tokenizer)      # htdemucs: nn.Module with demucs key names, or None
+    model.load_state_dict(checkpoint["model_state_dict"], strict=False)
+    model = model.to("cuda").eval()
+    out = model(wav, "vocals")  /  model(wav, ["drums", "bass"])  # (B,2,T) f32 cuda -> (B,2,T) f32 cuda
+
+`forward` runs entirely in libathd.so (HIP kernels on the current torch stream).  PyTorch only provides device
+memory and the stream.  Additionally `forward_prompts(wav, prompts)` encodes once and decodes once per prompt.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Union
+
+import numpy as np
+import torch
+
+from .text import PromptEmbedder
+from .weights import hot_path_spec
+
+
+def _to_numpy(v) -> np.ndarray:
+    if isinstance(v, torch.Tensor):
+        return v.detach().to("cpu", torch.float32).numpy()
+    return np.asarray(v, dtype=np.float32)
+
+
+class AudioTextHTDemucs:
+    def __init__(self, htdemucs_model=None, clap_encoder=None, clap_tokenizer=None, model_dim: int = 384,
+                 text_dim: int = 512, num_heads: int = 8, sample_rate: int = 44100, segment: float = 7.8,
+                 dtype: str = "bf16", text_table: Optional[Dict[str, np.ndarray]] = None):
+        if (model_dim, text_dim, num_heads) != (384, 512, 8):
+            raise ValueError("the native path is built for model_dim=384, text_dim=512, num_heads=8 "
+                             "(config.yaml:15-17)")
+        if dtype not in ("bf16", "f32"):
+            raise ValueError("dtype must be 'bf16' or 'f32'")
+        self.sample_rate = sample_rate
+        self.segment = segment
+        self.dtype = dtype
+        self.embedder = PromptEmbedder(clap_encoder, clap_tokenizer, text_table)
+        self._weights: Dict[str, np.ndarray] = {}
+        if htdemucs_model is not None:
+            for k, v in htdemucs_model.state_dict().items():
+                self._weights["htdemucs." + k] = _to_numpy(v)
+        self.device: Optional[torch.device] = None
+        self._ctx = None
+        self._ws: Optional[torch.Tensor] = None
+        self.training = False
+
+    # ------------------------------------------------------------------ nn.Module-like surface
+    def load_state_dict(self, state_dict, strict: bool = False):
+        """Reference key names; like `load_state_dict(strict=False)` unknown keys (clap.*, htdemucs.decoder.*)
+        are ignored.  Returns (missing_keys, unexpected_keys) restricted to the hot-path contract."""
+        needed = {k for k, _, _ in hot_path_spec()}
+        unexpected = []
+        for k, v in state_dict.items():
+            if k.startswith("module."):
+                k = k[len("module."):]        # DataParallel prefix (benchmark.py:398-404)
+            if k in needed:
+                self._weights[k] = _to_numpy(v)
+            else:
+                unexpected.append(k)
+        missing = sorted(needed - set(self._weights))
+        if strict and (missing or unexpected):
+            raise RuntimeError(f"missing {missing[:5]}..., unexpected {unexpected[:5]}...")
+        self._ctx = None
+        return missing, unexpected
+
+    def to(self, device):
+        device = torch.device(device)
+        if device.type != "cuda":
+            raise RuntimeError("athd runs on a HIP device only (there is no CPU path)")
+        if device.index is None:
+            device = torch.device("cuda", torch.cuda.current_device())
+        if self.device != device:
+            self._ctx = None
+        self.device = device
+        return self
+
+    def cuda(self, index: int = 0):
+        return self.to(torch.device("cuda", index))
+
+    def eval(self):
+        self.training = False
+        return self
+
+    def train(self, mode: bool = True):
+        if mode:
+            raise RuntimeError("athd is inference-only")
+        return self
+
+    def parameters(self):
+        return iter(())
+
+    # ------------------------------------------------------------------ native context
+    def _ensure_ctx(self):
+        if self._ctx is not None:
+            return self._ctx
+        from . import native   # raises if libathd.so is missing
+        if self.device is None:
+            self.to("cuda")
+        ctx = native.Context(self.device.index, native.BF16 if self.dtype == "bf16" else native.F32)
+        missing = [k for k in native.required_keys() if k not in self._weights]
+        if missing:
+            raise RuntimeError(f"{len(missing)} hot-path weights missing, e.g. {missing[:3]}")
+        for k in native.required_keys():
+            ctx.set_weight(k, self._weights[k])
+        ctx.finalize()
+        self._ctx = ctx
+        return ctx
+
+    def _workspace(self, nbytes: int) -> torch.Tensor:
+        if self._ws is None or self._ws.numel() < nbytes or self._ws.device != self.device:
+            self._ws = None
+            self._ws = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
+        return self._ws
+
+    def _check_wav(self, wav: torch.Tensor):
+        if wav.dim() != 3 or wav.shape[1] != 2:
+            raise ValueError(f"expected (B, 2, T) stereo, got {tuple(wav.shape)}")
+        if self.device is None:
+            self.to(wav.device)
+        if wav.device != self.device:
+            raise ValueError(f"wav on {wav.device}, model on {self.device}")
+        return wav.contiguous().float()
+
+    # ------------------------------------------------------------------ forward
+    @torch.no_grad()
+    def forward(self, wav: torch.Tensor, text: Union[str, List[str]]) -> torch.Tensor:
+        """`ATHTDemucs_v2.py:250-326`: (B,2,T) mixture + prompt(s) -> (B,2,T) separated stem."""
+        wav = self._check_wav(wav)
+        B, _, T = wav.shape
+        ctx = self._ensure_ctx()
+        emb = self.embedder.rows(text, B).to(self.device).contiguous()
+        out = torch.empty_like(wav)
+        nbytes = ctx.workspace_bytes(B, T, 1)
+        ws = self._workspace(nbytes)
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        ctx.forward(wav.data_ptr(), B, T, emb.data_ptr(), out.data_ptr(), ws.data_ptr(), ws.numel(), stream)
+        return out
+
+    __call__ = forward
+
+    @torch.no_grad()
+    def forward_prompts(self, wav: torch.Tensor, prompts: List[str]) -> torch.Tensor:
+        """Encode once, decode once per prompt: (B,2,T) -> (B,P,2,T)."""
+        wav = self._check_wav(wav)
+        B, _, T = wav.shape
+        ctx = self._ensure_ctx()
+        table = self.embedder.rows(list(prompts), len(prompts)).to(self.device).contiguous()
+        P = table.shape[0]
+        out = torch.empty((B, P, 2, T), dtype=torch.float32, device=self.device)
+        nbytes = ctx.workspace_bytes(B, T, P)
+        ws = self._workspace(nbytes)
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        ctx.forward_prompts(wav.data_ptr(), B, T, table.data_ptr(), P, out.data_ptr(), ws.data_ptr(), ws.numel(),
+                            stream)
+        return out

@@ -1,0 +1,337 @@
+// athd C-ABI: weight staging/packing and the per-segment forward orchestration.
+//
+// Data layout in HBM (all channels-last, fp32 unless noted; bf16 mode keeps GEMM-operand intermediates in bf16):
+//   spec      [B][2048][Tspec][4]       CaC spectrogram {Re L, Im L, Re R, Im R} (also the complex z for masking)
+//   saved[i]  [B][F_i][Tspec][C_i]      freq encoder outputs, F = 512/128/32/8, C = 48/96/192/384
+//   saved_t[i][B][L_i][C_i]             time encoder outputs, L = ceil(T/4), ...
+//   X / XT    [B][Nf][512] / [B][Nt][512]  transformer tokens; freq tokens kept in (f, t) order (the reference
+//                                      uses (t f); attention and GroupNorm are order-free, positions are indexed
+//                                      explicitly, so only the summation order differs)
+//   decoder   [items][rows][W][C]       items = segments x prompts
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/athd.h"
+#include "attn.h"
+#include "gemm.h"
+#include "kernels.h"
+#include "ctx.h"
+
+namespace {
+
+
+std::vector<std::pair<std::string, std::vector<int64_t>>> required_keys() {
+    std::vector<std::pair<std::string, std::vector<int64_t>>> r;
+    auto dconv = [&](const std::string& p, int64_t c) {
+        int64_t h = c / 8;
+        for (int d = 0; d < 2; ++d) {
+            std::string q = p + ".dconv.layers." + std::to_string(d);
+            r.push_back({q + ".0.weight", {h, c, 3}});
+            r.push_back({q + ".0.bias", {h}});
+            r.push_back({q + ".1.weight", {h}});
+            r.push_back({q + ".1.bias", {h}});
+            r.push_back({q + ".3.weight", {2 * c, h, 1}});
+            r.push_back({q + ".3.bias", {2 * c}});
+            r.push_back({q + ".4.weight", {2 * c}});
+            r.push_back({q + ".4.bias", {2 * c}});
+            r.push_back({q + ".6.scale", {c}});
+        }
+    };
+    int64_t cf = 4, ct = 2;
+    for (int i = 0; i < 4; ++i) {
+        int64_t c = ENC_CH[i];
+        std::string p = "htdemucs.encoder." + std::to_string(i);
+        r.push_back({p + ".conv.weight", {c, cf, 8, 1}});
+        r.push_back({p + ".conv.bias", {c}});
+        dconv(p, c);
+        r.push_back({p + ".rewrite.weight", {2 * c, c, 1, 1}});
+        r.push_back({p + ".rewrite.bias", {2 * c}});
+        p = "htdemucs.tencoder." + std::to_string(i);
+        r.push_back({p + ".conv.weight", {c, ct, 8}});
+        r.push_back({p + ".conv.bias", {c}});
+        dconv(p, c);
+        r.push_back({p + ".rewrite.weight", {2 * c, c, 1}});
+        r.push_back({p + ".rewrite.bias", {2 * c}});
+        cf = ct = c;
+    }
+    r.push_back({"htdemucs.freq_emb.embedding.weight", {512, 48}});
+    for (const char* s : {"", "_t"}) {
+        std::string u = std::string("htdemucs.channel_upsampler") + s, d = std::string("htdemucs.channel_downsampler") + s;
+        r.push_back({u + ".weight", {512, 384, 1}});
+        r.push_back({u + ".bias", {512}});
+        r.push_back({d + ".weight", {384, 512, 1}});
+        r.push_back({d + ".bias", {384}});
+    }
+    const std::string ct_ = "htdemucs.crosstransformer";
+    for (const char* s : {".norm_in", ".norm_in_t"}) {
+        r.push_back({ct_ + s + ".weight", {512}});
+        r.push_back({ct_ + s + ".bias", {512}});
+    }
+    for (int idx = 0; idx < 5; ++idx) {
+        bool cross = idx % 2 == 1;
+        for (const char* br : {".layers.", ".layers_t."}) {
+            std::string p = ct_ + br + std::to_string(idx);
+            std::string a = p + (cross ? ".cross_attn" : ".self_attn");
+            r.push_back({a + ".in_proj_weight", {1536, 512}});
+            r.push_back({a + ".in_proj_bias", {1536}});
+            r.push_back({a + ".out_proj.weight", {512, 512}});
+            r.push_back({a + ".out_proj.bias", {512}});
+            r.push_back({p + ".linear1.weight", {2048, 512}});
+            r.push_back({p + ".linear1.bias", {2048}});
+            r.push_back({p + ".linear2.weight", {512, 2048}});
+            r.push_back({p + ".linear2.bias", {512}});
+            for (const char* n : {".norm1", ".norm2", ".norm3", ".norm_out"}) {
+                if (!cross && std::string(n) == ".norm3") continue;
+                r.push_back({p + n + ".weight", {512}});
+                r.push_back({p + n + ".bias", {512}});
+            }
+            r.push_back({p + ".gamma_1.scale", {512}});
+            r.push_back({p + ".gamma_2.scale", {512}});
+        }
+    }
+    const std::string ta = "text_attn";
+    r.push_back({ta + ".v_proj.weight", {384, 512}});
+    r.push_back({ta + ".v_proj.bias", {384}});
+    r.push_back({ta + ".attn.in_proj_weight", {1152, 384}});
+    r.push_back({ta + ".attn.in_proj_bias", {1152}});
+    r.push_back({ta + ".attn.out_proj.weight", {384, 384}});
+    r.push_back({ta + ".attn.out_proj.bias", {384}});
+    r.push_back({ta + ".out_mlp.0.weight", {384, 384}});
+    r.push_back({ta + ".out_mlp.0.bias", {384}});
+    r.push_back({ta + ".out_mlp.2.weight", {384, 384}});
+    r.push_back({ta + ".out_mlp.2.bias", {384}});
+    r.push_back({ta + ".norm_out.weight", {384}});
+    r.push_back({ta + ".norm_out.bias", {384}});
+    for (const char* name : {"freq_decoder", "time_decoder"}) {
+        bool fr = std::string(name) == "freq_decoder";
+        for (int i = 0; i < 4; ++i) {
+            std::string p = std::string(name) + ".layers." + std::to_string(i);
+            std::vector<int64_t> ws = {DEC_CH[i], DEC_CH[i + 1], 8};
+            if (fr) ws.push_back(1);
+            r.push_back({p + ".0.weight", ws});
+            r.push_back({p + ".0.bias", {DEC_CH[i + 1]}});
+            if (i < 3) {
+                r.push_back({p + ".1.weight", {DEC_CH[i + 1]}});
+                r.push_back({p + ".1.bias", {DEC_CH[i + 1]}});
+            }
+        }
+    }
+    r.push_back({"freq_out.weight", {2, 4, 1, 1}});
+    r.push_back({"freq_out.bias", {2}});
+    r.push_back({"time_out.weight", {2, 4, 1}});
+    r.push_back({"time_out.bias", {2}});
+    return r;
+}
+
+const std::vector<std::pair<std::string, std::vector<int64_t>>>& keys() {
+    static const auto k = required_keys();
+    return k;
+}
+
+
+}  // namespace
+
+// =============================================================================================== ABI
+extern "C" {
+
+int athd_version(void) { return 100; }
+
+int athd_num_required_keys(void) { return (int)keys().size(); }
+
+const char* athd_required_key(int i) {
+    if (i < 0 || i >= (int)keys().size()) return nullptr;
+    return keys()[i].first.c_str();
+}
+
+int athd_create(athd_ctx** out, int device, int dtype) {
+    if (!out || (dtype != ATHD_F32 && dtype != ATHD_BF16)) return ATHD_EINVAL;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return ATHD_EHIP;
+    athd_ctx* c = new athd_ctx();
+    c->device = device;
+    c->mode = dtype;
+    *out = c;
+    return ATHD_OK;
+}
+
+int athd_set_weight(athd_ctx* c, const char* key, const void* host, const int64_t* shape, int ndim, int src_dtype) {
+    if (!c || !key || !host || (ndim > 0 && !shape)) return ATHD_EINVAL;
+    if (c->finalized) return c->fail(ATHD_ESTATE, "athd_set_weight after finalize");
+    if (src_dtype != 0) return c->fail(ATHD_EINVAL, std::string("only fp32 host weights are accepted: ") + key);
+    bool needed = false;
+    for (const auto& k : keys())
+        if (k.first == key) { needed = true; break; }
+    if (!needed) return ATHD_OK;   // strict=False: ignore keys outside the hot path
+    HostT t;
+    int64_t n = 1;
+    for (int i = 0; i < ndim; ++i) { t.shape.push_back(shape[i]); n *= shape[i]; }
+    t.v.assign((const float*)host, (const float*)host + n);
+    c->host[key] = std::move(t);
+    return ATHD_OK;
+}
+
+int athd_finalize(athd_ctx* c) {
+    if (!c) return ATHD_EINVAL;
+    if (c->finalized) return c->fail(ATHD_ESTATE, "already finalized");
+    for (const auto& k : keys()) {
+        auto it = c->host.find(k.first);
+        if (it == c->host.end()) return c->fail(ATHD_EKEY, "missing weight: " + k.first);
+        if (it->second.shape != k.second) return c->fail(ATHD_EKEY, "shape mismatch for " + k.first);
+    }
+    if (hipSetDevice(c->device) != hipSuccess) return c->fail(ATHD_EHIP, "hipSetDevice failed");
+    // ---- encoders ----
+    int cf = 4, ct = 2;
+    for (int i = 0; i < 4; ++i) {
+        for (int br = 0; br < 2; ++br) {
+            EncW& e = br == 0 ? c->fenc[i] : c->tenc[i];
+            const int C = ENC_CH[i];
+            const std::string p = std::string(br == 0 ? "htdemucs.encoder." : "htdemucs.tencoder.") + std::to_string(i);
+            e.cin = br == 0 ? cf : ct;
+            e.cout = C;
+            e.conv = c->conv_gemm(p + ".conv.weight", p + ".conv.bias", C, e.cin, 8);
+            e.rewrite = c->conv_gemm(p + ".rewrite.weight", p + ".rewrite.bias", 2 * C, C, 1, true);
+            for (int d = 0; d < 2; ++d) {
+                const std::string q = p + ".dconv.layers." + std::to_string(d);
+                e.dc.c3[d] = c->conv_gemm(q + ".0.weight", q + ".0.bias", C / 8, C, 3);
+                e.dc.c1[d] = c->conv_gemm(q + ".3.weight", q + ".3.bias", 2 * C, C / 8, 1);
+                e.dc.g1w[d] = c->up_key(q + ".1.weight");
+                e.dc.g1b[d] = c->up_key(q + ".1.bias");
+                e.dc.g2w[d] = c->up_key(q + ".4.weight");
+                e.dc.g2b[d] = c->up_key(q + ".4.bias");
+                e.dc.scale[d] = c->up_key(q + ".6.scale");
+            }
+        }
+        cf = ct = ENC_CH[i];
+    }
+    {
+        const auto& w = c->W("htdemucs.freq_emb.embedding.weight").v;
+        std::vector<float> t(w.size());
+        for (size_t i = 0; i < w.size(); ++i) t[i] = (w[i] * 10.0f) * 0.2f;   // ScaledEmbedding * freq_emb_scale
+        c->femb = c->up_f32(t);
+    }
+    {
+        auto one = [&](const std::string& s, int N, int K) {
+            const auto& w = c->W(s + ".weight").v;
+            return c->up_gemm(w, N, K, c->W(s + ".bias").v);
+        };
+        c->up = one("htdemucs.channel_upsampler", 512, 384);
+        c->down = one("htdemucs.channel_downsampler", 384, 512);
+        c->up_t = one("htdemucs.channel_upsampler_t", 512, 384);
+        c->down_t = one("htdemucs.channel_downsampler_t", 384, 512);
+    }
+    const std::string ctp = "htdemucs.crosstransformer";
+    c->nin_w = c->up_key(ctp + ".norm_in.weight");
+    c->nin_b = c->up_key(ctp + ".norm_in.bias");
+    c->nint_w = c->up_key(ctp + ".norm_in_t.weight");
+    c->nint_b = c->up_key(ctp + ".norm_in_t.bias");
+    for (int idx = 0; idx < 5; ++idx) {
+        for (int br = 0; br < 2; ++br) {
+            TLayerW& l = br == 0 ? c->L[idx] : c->Lt[idx];
+            l.cross = idx % 2 == 1;
+            const std::string p = ctp + (br == 0 ? ".layers." : ".layers_t.") + std::to_string(idx);
+            const std::string a = p + (l.cross ? ".cross_attn" : ".self_attn");
+            if (l.cross) {
+                l.q = c->lin_gemm(a + ".in_proj_weight", a + ".in_proj_bias", 0, 512);
+                l.kv = c->lin_gemm(a + ".in_proj_weight", a + ".in_proj_bias", 512, 1024);
+            } else {
+                l.qkv = c->lin_gemm(a + ".in_proj_weight", a + ".in_proj_bias");
+            }
+            l.out = c->lin_gemm(a + ".out_proj.weight", a + ".out_proj.bias");
+            l.l1 = c->lin_gemm(p + ".linear1.weight", p + ".linear1.bias");
+            l.l2 = c->lin_gemm(p + ".linear2.weight", p + ".linear2.bias");
+            l.n1w = c->up_key(p + ".norm1.weight");
+            l.n1b = c->up_key(p + ".norm1.bias");
+            l.n2w = c->up_key(p + ".norm2.weight");
+            l.n2b = c->up_key(p + ".norm2.bias");
+            if (l.cross) {
+                l.n3w = c->up_key(p + ".norm3.weight");
+                l.n3b = c->up_key(p + ".norm3.bias");
+            }
+            l.now = c->up_key(p + ".norm_out.weight");
+            l.nob = c->up_key(p + ".norm_out.bias");
+            l.g1 = c->up_key(p + ".gamma_1.scale");
+            l.g2 = c->up_key(p + ".gamma_2.scale");
+        }
+    }
+    // ---- text cross-attention (closed form: single key => softmax == 1) ----
+    c->ta_vw = c->up_key("text_attn.v_proj.weight");
+    c->ta_vb = c->up_key("text_attn.v_proj.bias");
+    {
+        const auto& w = c->W("text_attn.attn.in_proj_weight").v;
+        const auto& b = c->W("text_attn.attn.in_proj_bias").v;
+        c->ta_ivw = c->up_f32(std::vector<float>(w.begin() + 768 * 384, w.end()));
+        c->ta_ivb = c->up_f32(std::vector<float>(b.begin() + 768, b.end()));
+    }
+    c->ta_ow = c->up_key("text_attn.attn.out_proj.weight");
+    c->ta_ob = c->up_key("text_attn.attn.out_proj.bias");
+    c->mlp0 = c->lin_gemm("text_attn.out_mlp.0.weight", "text_attn.out_mlp.0.bias");
+    c->mlp2 = c->lin_gemm("text_attn.out_mlp.2.weight", "text_attn.out_mlp.2.bias");
+    c->ta_nw = c->up_key("text_attn.norm_out.weight");
+    c->ta_nb = c->up_key("text_attn.norm_out.bias");
+    // ---- decoders: ConvTranspose weight [Cin][Cout][8] -> per residue [Cout][tap*Cin + ci] ----
+    for (int br = 0; br < 2; ++br) {
+        for (int i = 0; i < 4; ++i) {
+            DecW& dw = br == 0 ? c->fdec[i] : c->tdec[i];
+            const std::string p = std::string(br == 0 ? "freq_decoder" : "time_decoder") + ".layers." + std::to_string(i);
+            dw.cin = DEC_CH[i];
+            dw.cout = DEC_CH[i + 1];
+            const auto& w = c->W(p + ".0.weight").v;
+            const auto& b = c->W(p + ".0.bias").v;
+            for (int r = 0; r < 4; ++r) {
+                std::vector<float> pk((size_t)dw.cout * 2 * dw.cin);
+                for (int co = 0; co < dw.cout; ++co)
+                    for (int ci = 0; ci < dw.cin; ++ci) {
+                        pk[(size_t)co * 2 * dw.cin + ci] = w[((size_t)ci * dw.cout + co) * 8 + RES_K0[r]];
+                        pk[(size_t)co * 2 * dw.cin + dw.cin + ci] = w[((size_t)ci * dw.cout + co) * 8 + RES_K1[r]];
+                    }
+                dw.res[r] = c->up_gemm(pk, dw.cout, 2 * dw.cin, b);
+            }
+            if (i < 3) {
+                dw.gnw = c->up_key(p + ".1.weight");
+                dw.gnb = c->up_key(p + ".1.bias");
+            }
+        }
+    }
+    c->fout_w = c->up_key("freq_out.weight");
+    c->fout_b = c->up_key("freq_out.bias");
+    c->tout_w = c->up_key("time_out.weight");
+    c->tout_b = c->up_key("time_out.bias");
+    // ---- FFT twiddles and the periodic Hann window (torch.hann_window(4096)) ----
+    {
+        std::vector<float2> tw(4096);
+        std::vector<float> win(4096), win2(4096);
+        for (int k = 0; k < 4096; ++k) {
+            const double a = -2.0 * M_PI * (double)k / 4096.0;
+            tw[k] = make_float2((float)cos(a), (float)sin(a));
+            const float w = (float)(0.5 - 0.5 * cos(2.0 * M_PI * (double)k / 4096.0));
+            win[k] = w;
+            win2[k] = w * w;
+        }
+        c->tw = c->dalloc<float2>(4096);
+        hipMemcpy(c->tw, tw.data(), 4096 * sizeof(float2), hipMemcpyHostToDevice);
+        c->win = c->up_f32(win);
+        c->win2 = c->up_f32(win2);
+    }
+    for (void* p : c->allocs)
+        if (!p) return c->fail(ATHD_EHIP, "device allocation failed");
+    if (hipDeviceSynchronize() != hipSuccess) return c->fail(ATHD_EHIP, "upload failed");
+    c->host.clear();
+    c->finalized = true;
+    return ATHD_OK;
+}
+
+const char* athd_last_error(athd_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+void athd_destroy(athd_ctx* c) {
+    if (!c) return;
+    for (void* p : c->allocs) hipFree(p);
+    delete c;
+}
+
+}  // extern "C"

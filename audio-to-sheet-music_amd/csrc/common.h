@@ -1,0 +1,64 @@
+// Shared device helpers for the athd HIP kernels (gfx950 / CDNA4 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define ATHD_DEV __device__ __forceinline__
+
+typedef __attribute__((ext_vector_type(8))) short bf16x8_t;   // 8 bf16 = one MFMA 16x16x32 operand fragment
+typedef __attribute__((ext_vector_type(4))) float f32x4_t;    // 16x16 accumulator fragment
+typedef uint16_t bf16_t;                                      // raw bf16 storage
+
+// Round-to-nearest-even f32 -> bf16 (NaN stays NaN through the plain cast path in hipcc; we only feed finite
+// activations here, and the explicit form keeps the rounding identical across host and device).
+ATHD_DEV bf16_t f2bf(float f) {
+    uint32_t u = __float_as_uint(f);
+    u += 0x7FFFu + ((u >> 16) & 1u);
+    return (bf16_t)(u >> 16);
+}
+ATHD_DEV float bf2f(bf16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
+
+ATHD_DEV float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752440f)); }
+ATHD_DEV float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+ATHD_DEV float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+ATHD_DEV double wave_sum_d(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+ATHD_DEV float wave_max(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+// PyTorch-faithful fp32 source index for linear/bilinear resize with align_corners=False and no explicit scale
+// (ATen UpSample.h area_pixel_compute_scale / area_pixel_compute_source_index / guard_index_and_lambda).
+struct LinIdx { int i0, i1; float l0, l1; };
+ATHD_DEV LinIdx lin_index(int dst, int in_size, int out_size) {
+    LinIdx r;
+    if (in_size == out_size) { r.i0 = r.i1 = dst; r.l0 = 1.f; r.l1 = 0.f; return r; }
+    float scale = (float)in_size / (float)out_size;
+    float src = scale * ((float)dst + 0.5f) - 0.5f;
+    if (src < 0.f) src = 0.f;
+    int i0 = (int)floorf(src);
+    if (i0 > in_size - 1) i0 = in_size - 1;
+    float lam = src - (float)i0;
+    lam = fminf(fmaxf(lam, 0.f), 1.f);
+    r.i0 = i0;
+    r.i1 = i0 + ((i0 < in_size - 1) ? 1 : 0);
+    r.l1 = lam;
+    r.l0 = 1.f - lam;
+    return r;
+}
+
+#define HIP_CHECK_RET(x)                                                       \
+    do {                                                                       \
+        hipError_t e_ = (x);                                                   \
+        if (e_ != hipSuccess) return (int)e_;                                  \
+    } while (0)

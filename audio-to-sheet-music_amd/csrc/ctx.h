@@ -1,0 +1,175 @@
+// Private: athd context (packed device weights) shared by athd_api.cpp and forward.cpp.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+namespace athd {
+
+struct HostT {
+    std::vector<float> v;
+    std::vector<int64_t> shape;
+};
+
+struct GemmW {
+    void* w = nullptr;
+    float* bias = nullptr;
+    int N = 0, K = 0, Kp = 0;
+};
+
+struct DConvW {
+    GemmW c3[2], c1[2];
+    float *g1w[2], *g1b[2], *g2w[2], *g2b[2], *scale[2];
+};
+
+struct EncW {
+    int cin = 0, cout = 0;
+    GemmW conv, rewrite;
+    DConvW dc;
+};
+
+struct TLayerW {
+    bool cross = false;
+    GemmW qkv, q, kv, out, l1, l2;
+    float *n1w, *n1b, *n2w, *n2b, *n3w = nullptr, *n3b = nullptr, *now, *nob, *g1, *g2;
+};
+
+struct DecW {
+    int cin = 0, cout = 0;
+    GemmW res[4];
+    float *gnw = nullptr, *gnb = nullptr;
+};
+
+}  // namespace athd
+
+namespace athd {
+inline uint16_t host_f2bf(float f) {
+    uint32_t u;
+    std::memcpy(&u, &f, 4);
+    u += 0x7FFFu + ((u >> 16) & 1u);
+    return (uint16_t)(u >> 16);
+}
+inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+inline int64_t rup(int64_t a, int64_t b) { return cdiv(a, b) * b; }
+constexpr int ENC_CH[4] = {48, 96, 192, 384};
+constexpr int DEC_CH[5] = {384, 192, 96, 48, 4};
+// ConvTranspose (k8 s4 p2) residue classes: output row 4u+rho = taps in rows u+in_off, u+in_off+1 with kernel
+// indices {k0, k1}
+constexpr int RES_OFF[4] = {-1, -1, 0, 0};
+constexpr int RES_K0[4] = {6, 7, 4, 5};
+constexpr int RES_K1[4] = {2, 3, 0, 1};
+
+// Bump allocator over the caller's workspace (or sizing pass when base == nullptr).
+struct Arena {
+    char* base = nullptr;
+    size_t off = 0;
+    template <typename T>
+    T* take(int64_t n) {
+        size_t bytes = (size_t)rup((int64_t)(n * (int64_t)sizeof(T)), 256);
+        T* p = base ? reinterpret_cast<T*>(base + off) : nullptr;
+        off += bytes;
+        return p;
+    }
+};
+}  // namespace athd
+
+using namespace athd;
+
+struct athd_ctx {
+    int device = 0;
+    int mode = 1;
+    bool finalized = false;
+    std::string err;
+    std::map<std::string, HostT> host;
+    std::vector<void*> allocs;
+
+    EncW fenc[4], tenc[4];
+    float* femb = nullptr;           // [512][48] = (w * 10) * 0.2
+    GemmW up, down, up_t, down_t;
+    float *nin_w, *nin_b, *nint_w, *nint_b;
+    TLayerW L[5], Lt[5];
+    float *ta_vw, *ta_vb, *ta_ivw, *ta_ivb, *ta_ow, *ta_ob, *ta_nw, *ta_nb;
+    GemmW mlp0, mlp2;
+    DecW fdec[4], tdec[4];
+    float *fout_w, *fout_b, *tout_w, *tout_b;
+    float2* tw = nullptr;
+    float* win = nullptr;
+    float* win2 = nullptr;
+
+    int fail(int code, const std::string& m) {
+        err = m;
+        return code;
+    }
+    template <typename T>
+    T* dalloc(size_t n) {
+        void* p = nullptr;
+        if (hipMalloc(&p, n * sizeof(T)) != hipSuccess) return nullptr;
+        allocs.push_back(p);
+        return (T*)p;
+    }
+    const HostT& W(const std::string& k) { return host.at(k); }
+    float* up_f32(const std::vector<float>& v) {
+        float* p = dalloc<float>(v.size());
+        if (p) hipMemcpy(p, v.data(), v.size() * 4, hipMemcpyHostToDevice);
+        return p;
+    }
+    float* up_key(const std::string& k) { return up_f32(W(k).v); }
+    // Pack a [N][K] fp32 host matrix (row-major, k contiguous) into the compute dtype, Kp = roundup(K, 32).
+    GemmW up_gemm(const std::vector<float>& w, int N, int K, const std::vector<float>& bias) {
+        GemmW g;
+        g.N = N;
+        g.K = K;
+        g.Kp = (int)rup(K, 32);
+        if (mode == 1) {
+            std::vector<uint16_t> p((size_t)N * g.Kp, 0);
+            for (int n = 0; n < N; ++n)
+                for (int k = 0; k < K; ++k) p[(size_t)n * g.Kp + k] = host_f2bf(w[(size_t)n * K + k]);
+            void* d = dalloc<uint16_t>(p.size());
+            hipMemcpy(d, p.data(), p.size() * 2, hipMemcpyHostToDevice);
+            g.w = d;
+        } else {
+            std::vector<float> p((size_t)N * g.Kp, 0.f);
+            for (int n = 0; n < N; ++n)
+                for (int k = 0; k < K; ++k) p[(size_t)n * g.Kp + k] = w[(size_t)n * K + k];
+            g.w = up_f32(p);
+        }
+        g.bias = bias.empty() ? nullptr : up_f32(bias);
+        return g;
+    }
+    // conv weight [Cout][Cin][taps] -> [Cout][tap*Cin + ci]
+    GemmW conv_gemm(const std::string& wk, const std::string& bk, int cout, int cin, int taps, bool glu = false) {
+        const auto& w = W(wk).v;
+        std::vector<float> p((size_t)cout * taps * cin);
+        for (int co = 0; co < cout; ++co)
+            for (int ci = 0; ci < cin; ++ci)
+                for (int t = 0; t < taps; ++t) p[((size_t)co * taps + t) * cin + ci] = w[((size_t)co * cin + ci) * taps + t];
+        std::vector<float> b = W(bk).v;
+        if (glu) {   // pair order: per 32 packed rows [a(16q..16q+15) | gate(C+16q..)]
+            const int C = cout / 2;
+            std::vector<float> q(p.size()), qb(b.size());
+            const int K = taps * cin;
+            for (int pr = 0; pr < cout; ++pr) {
+                int qq = pr / 32, s = pr % 32;
+                int src = s < 16 ? 16 * qq + s : C + 16 * qq + (s - 16);
+                std::memcpy(&q[(size_t)pr * K], &p[(size_t)src * K], K * 4);
+                qb[pr] = b[src];
+            }
+            p.swap(q);
+            b.swap(qb);
+        }
+        return up_gemm(p, cout, taps * cin, b);
+    }
+    GemmW lin_gemm(const std::string& wk, const std::string& bk, int row0 = 0, int rows = -1) {
+        const HostT& w = W(wk);
+        int N = (int)w.shape[0], K = (int)w.shape[1];
+        if (rows < 0) rows = N - row0;
+        std::vector<float> p(w.v.begin() + (size_t)row0 * K, w.v.begin() + (size_t)(row0 + rows) * K);
+        const auto& bb = W(bk).v;
+        std::vector<float> b(bb.begin() + row0, bb.begin() + row0 + rows);
+        return up_gemm(p, rows, K, b);
+    }
+};
+

@@ -1,0 +1,564 @@
+// athd forward orchestration: AudioTextHTDemucs.forward (ATHTDemucs_v2.py:250-326) as a sequence of HIP
+// kernels on the caller's stream.  Workspace layout is computed by the same code path in a sizing pass.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <vector>
+
+#include "../../include/athd.h"
+#include "attn.h"
+#include "ctx.h"
+#include "gemm.h"
+#include "kernels.h"
+
+namespace {
+
+struct Dims {
+    int64_t B = 0, T = 0;
+    int P = 1;
+    int Tspec = 0;
+    int F[5] = {2048, 512, 128, 32, 8};
+    int64_t L[5] = {0, 0, 0, 0, 0};   // L[0] = T, L[i+1] = ceil(L[i]/4)
+    int64_t Nf = 0, Nt = 0, Nmax = 0;
+    int64_t Bc = 0;                   // samples per decode chunk
+    int64_t chunks = 0;
+};
+
+Dims make_dims(int64_t B, int64_t T, int P) {
+    Dims d;
+    d.B = B;
+    d.T = T;
+    d.P = P;
+    d.Tspec = (int)cdiv(T, 1024);
+    d.L[0] = T;
+    for (int i = 0; i < 4; ++i) d.L[i + 1] = cdiv(d.L[i], 4);
+    d.Nf = 8LL * d.Tspec;
+    d.Nt = d.L[4];
+    d.Nmax = std::max(d.Nf, d.Nt);
+    int64_t items_per_chunk = 64;
+    d.Bc = std::max<int64_t>(1, std::min<int64_t>(B, items_per_chunk / P));
+    d.chunks = cdiv(B, d.Bc);
+    return d;
+}
+
+struct Bufs {
+    float* spec;
+    double* stats;
+    int64_t nstats;     // number of double pairs
+    float *snorm, *tnorm_div, *tnorm_std;
+    float* saved[4];
+    float* saved_t[4];
+    float *ybuf, *hbuf, *y2buf;
+    float *X, *XT;
+    void *H[4], *QKV, *O, *F1;
+    float *pos2d, *pos1d, *x_enc, *xt_enc;
+    // decode (per chunk)
+    float* avec;
+    float *U, *Yb, *x_cond, *xt_cond;
+    void* Hm;
+    float *G, *D, *FO, *frames;
+};
+
+size_t plan(Arena& ar, const Dims& d, Bufs& b, bool actbf) {
+    const int64_t B = d.B, Ts = d.Tspec;
+    const size_t ab = actbf ? 2 : 4;
+    auto act = [&](int64_t n) -> void* { return (void*)ar.take<char>(n * (int64_t)ab); };
+    // stats pool
+    int64_t ns = 0;
+    for (int i = 0; i < 4; ++i) ns += 4 * (B * d.F[i + 1]) + 4 * B;
+    ns += 10 * B + 4 * B;
+    ns += d.chunks * 6 * d.Bc * d.P;
+    b.nstats = ns;
+    b.stats = ar.take<double>(2 * ns);
+    b.spec = ar.take<float>(B * 2048 * Ts * 4);
+    b.snorm = ar.take<float>(2 * B);
+    b.tnorm_div = ar.take<float>(2 * B);
+    b.tnorm_std = ar.take<float>(2 * B);
+    int64_t ymax = 0, hmax = 0;
+    for (int i = 0; i < 4; ++i) {
+        const int64_t C = ENC_CH[i];
+        b.saved[i] = ar.take<float>(B * d.F[i + 1] * Ts * C);
+        b.saved_t[i] = ar.take<float>(B * d.L[i + 1] * C);
+        const int64_t rows = std::max(B * d.F[i + 1] * Ts, B * d.L[i + 1]);
+        ymax = std::max(ymax, rows * C);
+        hmax = std::max(hmax, rows * (C / 8));
+    }
+    b.ybuf = ar.take<float>(ymax);
+    b.hbuf = ar.take<float>(hmax);
+    b.y2buf = ar.take<float>(2 * ymax);
+    b.X = ar.take<float>(B * d.Nf * 512);
+    b.XT = ar.take<float>(B * d.Nt * 512);
+    for (int i = 0; i < 4; ++i) b.H[i] = act(B * d.Nmax * 512);
+    b.QKV = act(B * d.Nmax * 1536);
+    b.O = act(B * d.Nmax * 512);
+    b.F1 = act(B * d.Nmax * 2048);
+    b.pos2d = ar.take<float>(d.Nf * 512);
+    b.pos1d = ar.take<float>(d.Nt * 512);
+    b.x_enc = ar.take<float>(B * d.Nf * 384);
+    b.xt_enc = ar.take<float>(B * d.Nt * 384);
+    // decode chunk
+    const int64_t NI = d.Bc * d.P;
+    b.avec = ar.take<float>(NI * 384);
+    b.U = ar.take<float>(NI * d.Nmax * 384);
+    b.Hm = act(NI * d.Nmax * 384);
+    b.Yb = ar.take<float>(NI * d.Nmax * 384);
+    b.x_cond = ar.take<float>(NI * d.Nf * 384);
+    b.xt_cond = ar.take<float>(NI * d.Nt * 384);
+    int64_t g = std::max<int64_t>(32 * Ts * 192, 2 * Ts * Ts * 96);
+    g = std::max(g, 4 * d.Nt * 192);
+    g = std::max(g, 4 * d.L[3] * 96);
+    g = std::max(g, 4 * d.L[2] * 48);
+    g = std::max(g, 4 * d.L[1] * 4);
+    b.G = ar.take<float>(NI * g);
+    int64_t dm = Ts * Ts * 192;
+    dm = std::max(dm, d.L[3] * 192);
+    dm = std::max(dm, d.L[2] * 96);
+    dm = std::max(dm, d.L[1] * 48);
+    dm = std::max(dm, d.T * 4);
+    b.D = ar.take<float>(NI * dm);
+    b.FO = ar.take<float>(NI * Ts * Ts * 2);
+    b.frames = ar.take<float>(NI * Ts * 2 * 4096);
+    return ar.off;
+}
+
+struct Run {
+    athd_ctx* c;
+    hipStream_t s;
+    int mode;
+    bool actbf;
+    double* st_next;
+    int err = 0;
+    std::string what;
+
+    double* stats(int64_t pairs) {
+        double* p = st_next;
+        st_next += 2 * pairs;
+        return p;
+    }
+    void check(int rc, const char* w) {
+        if (rc != 0 && err == 0) {
+            err = rc;
+            what = w;
+        }
+    }
+    // Linear layer on token rows: out[nb][N][n] = A[nb][N][:] @ W^T (+ epilogue)
+    GemmDesc lin(const GemmW& w, const void* A, int a_bf16, int nb, int64_t ntok, int ldA) {
+        GemmDesc g;
+        g.A = A;
+        g.a_bf16 = a_bf16;
+        g.nb = nb;
+        g.H_in = (int)ntok;
+        g.W = 1;
+        g.C_in = w.K;
+        g.a_ld = ldA;
+        g.H_out = (int)ntok;
+        g.Wp = w.w;
+        g.N = w.N;
+        g.K = w.K;
+        g.Kp = w.Kp;
+        g.bias = w.bias;
+        g.H_out_total = (int)ntok;
+        g.ldo = w.N;
+        return g;
+    }
+    void gemm(const GemmDesc& g, const char* w) { check(gemm_launch(g, mode, s), w); }
+};
+
+// One encoder level's DConv (2 residual layers) on x viewed as [nb][L][C] (freq: nb = B*F rows along time).
+void dconv(Run& r, const EncW& e, const Bufs& b, float* x, int64_t nb, int64_t L) {
+    const int C = e.cout, Hh = C / 8;
+    for (int dd = 0; dd < 2; ++dd) {
+        const int dil = 1 << dd;
+        double* st_h = r.stats(nb);
+        double* st_y = r.stats(nb);
+        GemmDesc g;
+        g.A = x; g.nb = (int)nb; g.H_in = (int)L; g.W = 1; g.C_in = C; g.a_ld = C;
+        g.ntaps = 3; g.in_stride = 1; g.in_off = -dil; g.dil = dil; g.H_out = (int)L;
+        g.Wp = e.dc.c3[dd].w; g.N = Hh; g.K = e.dc.c3[dd].K; g.Kp = e.dc.c3[dd].Kp; g.bias = e.dc.c3[dd].bias;
+        g.C = b.hbuf; g.H_out_total = (int)L; g.ldo = Hh; g.stats = st_h;
+        r.gemm(g, "dconv.conv3");
+        gn_gelu_launch(b.hbuf, (int)nb, L * Hh, Hh, st_h, e.dc.g1w[dd], e.dc.g1b[dd], r.s);
+        GemmDesc g2;
+        g2.A = b.hbuf; g2.nb = (int)nb; g2.H_in = (int)L; g2.W = 1; g2.C_in = Hh; g2.a_ld = Hh; g2.H_out = (int)L;
+        g2.Wp = e.dc.c1[dd].w; g2.N = 2 * C; g2.K = Hh; g2.Kp = e.dc.c1[dd].Kp; g2.bias = e.dc.c1[dd].bias;
+        g2.C = b.y2buf; g2.H_out_total = (int)L; g2.ldo = 2 * C; g2.stats = st_y;
+        r.gemm(g2, "dconv.conv1x1");
+        dconv_out_launch(x, b.y2buf, (int)nb, L, C, st_y, e.dc.g2w[dd], e.dc.g2b[dd], e.dc.scale[dd], r.s);
+    }
+}
+
+void encode(Run& r, const Dims& d, const Bufs& b, const float* wav) {
+    athd_ctx* c = r.c;
+    const int64_t B = d.B, Ts = d.Tspec;
+    // ---- STFT + CaC, input normalisation statistics (ATHTDemucs_v2.py:261-275) ----
+    PadPlan pp;
+    {
+        const int64_t le = d.Tspec, pad = 1536;
+        const int64_t pl = pad, pr = pad + le * 1024 - d.T;
+        int64_t epl = 0, epr = 0;
+        const int64_t maxpad = std::max(pl, pr);
+        if (d.T <= maxpad) {
+            const int64_t extra = maxpad - d.T + 1;
+            epr = std::min(pr, extra);
+            epl = extra - epr;
+        }
+        pp.L = d.T;
+        pp.left = pl - epl;
+        pp.ext_left = epl;
+        pp.Lx = d.T + epl + epr;
+    }
+    stft_launch(wav, (int)B, d.T, pp, (int)Ts, c->tw, c->win, b.spec, r.s);
+    double* st_spec = r.stats(B);
+    double* st_wav = r.stats(B);
+    stats_launch(b.spec, (int)B, 2048LL * Ts * 4, st_spec, r.s);
+    stats_launch(wav, (int)B, 2 * d.T, st_wav, r.s);
+    input_norm_params_launch(st_spec, (int)B, 2048LL * Ts * 4, b.snorm, nullptr, r.s);
+    input_norm_params_launch(st_wav, (int)B, 2 * d.T, b.tnorm_div, b.tnorm_std, r.s);
+
+    // ---- encoders (ATHTDemucs_v2.py:197-217; HEncLayer + DConv) ----
+    for (int i = 0; i < 4; ++i) {
+        // freq branch: conv (8,1)/(4,1) along freq rows
+        const EncW& e = c->fenc[i];
+        const int C = e.cout;
+        const int Fi = d.F[i], Fo = d.F[i + 1];
+        GemmDesc g;
+        g.A = i == 0 ? (const void*)b.spec : (const void*)b.saved[i - 1];
+        g.nb = (int)B; g.H_in = Fi; g.W = (int)Ts; g.C_in = e.cin; g.a_ld = e.cin;
+        g.ntaps = 8; g.in_stride = 4; g.in_off = -2; g.dil = 1; g.H_out = Fo;
+        g.a_norm = i == 0 ? b.snorm : nullptr;
+        g.Wp = e.conv.w; g.N = C; g.K = e.conv.K; g.Kp = e.conv.Kp; g.bias = e.conv.bias;
+        g.C = b.ybuf; g.H_out_total = Fo; g.ldo = C; g.act = ACT_GELU;
+        r.gemm(g, "fenc.conv");
+        dconv(r, e, b, b.ybuf, B * Fo, Ts);
+        GemmDesc gr;
+        gr.A = b.ybuf; gr.nb = (int)B; gr.H_in = Fo; gr.W = (int)Ts; gr.C_in = C; gr.a_ld = C; gr.H_out = Fo;
+        gr.Wp = e.rewrite.w; gr.N = 2 * C; gr.K = C; gr.Kp = e.rewrite.Kp; gr.bias = e.rewrite.bias;
+        gr.C = b.saved[i]; gr.H_out_total = Fo; gr.ldo = C; gr.act = ACT_GLU;
+        gr.row_add = i == 0 ? c->femb : nullptr;    // + freq_emb_scale * freq_emb(frs) (ATHTDemucs_v2.py:212-215)
+        r.gemm(gr, "fenc.rewrite");
+
+        // time branch: right zero-pad to a multiple of 4 is implicit (rows >= L read as 0)
+        const EncW& et = c->tenc[i];
+        const int64_t Li = d.L[i], Lo = d.L[i + 1];
+        GemmDesc gt;
+        if (i == 0) {
+            gt.A = wav; gt.a_ld = 1; gt.a_cs = d.T; gt.a_bs = 2 * d.T; gt.a_norm = b.tnorm_div;
+        } else {
+            gt.A = b.saved_t[i - 1]; gt.a_ld = et.cin;
+        }
+        gt.nb = (int)B; gt.H_in = (int)Li; gt.W = 1; gt.C_in = et.cin;
+        gt.ntaps = 8; gt.in_stride = 4; gt.in_off = -2; gt.dil = 1; gt.H_out = (int)Lo;
+        gt.Wp = et.conv.w; gt.N = C; gt.K = et.conv.K; gt.Kp = et.conv.Kp; gt.bias = et.conv.bias;
+        gt.C = b.ybuf; gt.H_out_total = (int)Lo; gt.ldo = C; gt.act = ACT_GELU;
+        r.gemm(gt, "tenc.conv");
+        dconv(r, et, b, b.ybuf, B, Lo);
+        GemmDesc grt;
+        grt.A = b.ybuf; grt.nb = (int)B; grt.H_in = (int)Lo; grt.W = 1; grt.C_in = C; grt.a_ld = C; grt.H_out = (int)Lo;
+        grt.Wp = et.rewrite.w; grt.N = 2 * C; grt.K = C; grt.Kp = et.rewrite.Kp; grt.bias = et.rewrite.bias;
+        grt.C = b.saved_t[i]; grt.H_out_total = (int)Lo; grt.ldo = C; grt.act = ACT_GLU;
+        r.gemm(grt, "tenc.rewrite");
+    }
+
+    // ---- cross-transformer (ATHTDemucs_v2.py:219-234) ----
+    const int ab = r.actbf ? 1 : 0;
+    {
+        GemmDesc g = r.lin(c->up, b.saved[3], 0, (int)B, d.Nf, 384);
+        g.C = b.X;
+        r.gemm(g, "upsampler");
+        GemmDesc gt = r.lin(c->up_t, b.saved_t[3], 0, (int)B, d.Nt, 384);
+        gt.C = b.XT;
+        r.gemm(gt, "upsampler_t");
+    }
+    pos2d_launch(b.pos2d, 8, (int)Ts, 512, r.s);
+    pos1d_launch(b.pos1d, (int)d.Nt, 512, r.s);
+    {
+        LnDesc l;
+        l.x = b.X; l.nb = (int)B; l.N = d.Nf; l.C = 512; l.w = c->nin_w; l.b = c->nin_b; l.pos = b.pos2d; l.out = b.X;
+        layernorm_launch(l, r.s);
+        LnDesc lt;
+        lt.x = b.XT; lt.nb = (int)B; lt.N = d.Nt; lt.C = 512; lt.w = c->nint_w; lt.b = c->nint_b; lt.pos = b.pos1d; lt.out = b.XT;
+        layernorm_launch(lt, r.s);
+    }
+    struct Pending { const double* st = nullptr; const float* w = nullptr; const float* b = nullptr; };
+    Pending pf, pt;
+    auto ln = [&](float* x, int64_t N, const float* w, const float* bb, Pending* pend, void* out) {
+        LnDesc l;
+        l.x = x; l.nb = (int)B; l.N = N; l.C = 512; l.w = w; l.b = bb; l.out = out; l.out_bf16 = ab;
+        if (pend && pend->st) { l.gn_stats = pend->st; l.gn_w = pend->w; l.gn_b = pend->b; *pend = Pending(); }
+        layernorm_launch(l, r.s);
+    };
+    // attention + FFN of one branch given LN'ed query rows Hq and key/value source (projected inside)
+    auto block = [&](const TLayerW& L, float* X, int64_t N, void* Hq, void* Hkv, int64_t Nk, Pending* pend) {
+        AttnDesc a;
+        a.nb = (int)B; a.Nq = (int)N; a.Nk = (int)Nk; a.heads = 8; a.scale = 0.125f;
+        if (!L.cross) {
+            GemmDesc g = r.lin(L.qkv, Hq, ab, (int)B, N, 512);
+            g.C = b.QKV; g.c_bf16 = ab;
+            r.gemm(g, "qkv");
+            a.Q = b.QKV; a.q_bf16 = ab; a.q_bs = N * 1536; a.q_ld = 1536; a.q_off = 0;
+            a.K = b.QKV; a.k_bf16 = ab; a.k_bs = N * 1536; a.k_ld = 1536; a.k_off = 512;
+            a.V = b.QKV; a.v_bf16 = ab; a.v_bs = N * 1536; a.v_ld = 1536; a.v_off = 1024;
+        } else {
+            char* Qb = (char*)b.QKV;
+            char* KVb = Qb + (size_t)B * d.Nmax * 512 * (ab ? 2 : 4);
+            GemmDesc gq = r.lin(L.q, Hq, ab, (int)B, N, 512);
+            gq.C = Qb; gq.c_bf16 = ab;
+            r.gemm(gq, "q");
+            GemmDesc gk = r.lin(L.kv, Hkv, ab, (int)B, Nk, 512);
+            gk.C = KVb; gk.c_bf16 = ab;
+            r.gemm(gk, "kv");
+            a.Q = Qb; a.q_bf16 = ab; a.q_bs = N * 512; a.q_ld = 512; a.q_off = 0;
+            a.K = KVb; a.k_bf16 = ab; a.k_bs = Nk * 1024; a.k_ld = 1024; a.k_off = 0;
+            a.V = KVb; a.v_bf16 = ab; a.v_bs = Nk * 1024; a.v_ld = 1024; a.v_off = 512;
+        }
+        a.O = b.O; a.o_bf16 = ab; a.o_bs = N * 512; a.o_ld = 512;
+        r.check(attn_launch(a, r.mode, r.s), "attention");
+        GemmDesc go = r.lin(L.out, b.O, ab, (int)B, N, 512);
+        go.C = X; go.res = X; go.res_scale = L.g1;
+        r.gemm(go, "out_proj");
+        ln(X, N, L.cross ? L.n3w : L.n2w, L.cross ? L.n3b : L.n2b, nullptr, Hq);
+        GemmDesc g1 = r.lin(L.l1, Hq, ab, (int)B, N, 512);
+        g1.C = b.F1; g1.c_bf16 = ab; g1.act = ACT_GELU;
+        r.gemm(g1, "linear1");
+        double* st = r.stats(B);
+        GemmDesc g2 = r.lin(L.l2, b.F1, ab, (int)B, N, 2048);
+        g2.C = X; g2.res = X; g2.res_scale = L.g2; g2.stats = st;
+        r.gemm(g2, "linear2");
+        pend->st = st; pend->w = L.now; pend->b = L.nob;
+    };
+    for (int idx = 0; idx < 5; ++idx) {
+        const TLayerW& Lf = c->L[idx];
+        const TLayerW& Lt = c->Lt[idx];
+        if (!Lf.cross) {
+            ln(b.X, d.Nf, Lf.n1w, Lf.n1b, &pf, b.H[0]);
+            block(Lf, b.X, d.Nf, b.H[0], nullptr, d.Nf, &pf);
+            ln(b.XT, d.Nt, Lt.n1w, Lt.n1b, &pt, b.H[1]);
+            block(Lt, b.XT, d.Nt, b.H[1], nullptr, d.Nt, &pt);
+        } else {
+            // all four norms read the pre-layer X / XT (time branch attends to old_x, demucs transformer.py)
+            ln(b.X, d.Nf, Lf.n1w, Lf.n1b, &pf, b.H[0]);      // applies pending GroupNorm to X
+            ln(b.X, d.Nf, Lt.n2w, Lt.n2b, nullptr, b.H[1]);  // kv of the time branch = norm2_t(old_x)
+            ln(b.XT, d.Nt, Lt.n1w, Lt.n1b, &pt, b.H[2]);     // applies pending GroupNorm to XT
+            ln(b.XT, d.Nt, Lf.n2w, Lf.n2b, nullptr, b.H[3]); // kv of the freq branch = norm2(xt)
+            block(Lf, b.X, d.Nf, b.H[0], b.H[3], d.Nt, &pf);
+            block(Lt, b.XT, d.Nt, b.H[2], b.H[1], d.Nf, &pt);
+        }
+    }
+    gn_apply_launch(b.X, (int)B, d.Nf, 512, pf.st, pf.w, pf.b, r.s);
+    gn_apply_launch(b.XT, (int)B, d.Nt, 512, pt.st, pt.w, pt.b, r.s);
+    {
+        GemmDesc g = r.lin(c->down, b.X, 0, (int)B, d.Nf, 512);
+        g.C = b.x_enc;
+        r.gemm(g, "downsampler");
+        GemmDesc gt = r.lin(c->down_t, b.XT, 0, (int)B, d.Nt, 512);
+        gt.C = b.xt_enc;
+        r.gemm(gt, "downsampler_t");
+    }
+}
+
+// ConvTranspose (k8, s4, p2) along H as 4 residue GEMMs; rows 4u+rho.  keep: -1 = store all rows (4*H_in rows),
+// 1 = store only rho 1, 2 as slots 2u, 2u+1 (stats of all 4 if st != null), 2 = only rho 1, 2 (no stats).
+void conv_t(Run& r, const DecW& w, const void* A, int nb, int H_in, int W, float* out, double* st, int keep) {
+    for (int rho = 0; rho < 4; ++rho) {
+        const bool kept_row = (rho == 1 || rho == 2);
+        if (keep == 2 && !kept_row) continue;
+        GemmDesc g;
+        g.A = A; g.nb = nb; g.H_in = H_in; g.W = W; g.C_in = w.cin; g.a_ld = w.cin;
+        g.ntaps = 2; g.in_stride = 1; g.in_off = RES_OFF[rho]; g.dil = 1; g.H_out = H_in;
+        g.Wp = w.res[rho].w; g.N = w.cout; g.K = w.res[rho].K; g.Kp = w.res[rho].Kp; g.bias = w.res[rho].bias;
+        g.C = out; g.ldo = w.cout; g.stats = st;
+        if (keep < 0) {
+            g.H_out_total = 4 * H_in; g.o_stride = 4; g.o_off = rho;
+        } else {
+            g.H_out_total = 2 * H_in; g.o_stride = 2; g.o_off = rho == 2 ? 1 : 0; g.store = kept_row ? 1 : 0;
+        }
+        r.gemm(g, "conv_transpose");
+    }
+}
+
+void decode_chunk(Run& r, const Dims& d, const Bufs& b, int64_t s0, int64_t Bc, const float* text, bool text_per_item,
+                  float* out) {
+    athd_ctx* c = r.c;
+    const int P = d.P;
+    const int NI = (int)(Bc * P);
+    const int64_t Ts = d.Tspec;
+    const int ab = r.actbf ? 1 : 0;
+    // ---- text cross-attention, closed form (ATHTDemucs_v2.py:38-58) ----
+    text_vec_launch(text_per_item ? text + s0 * 512 : text, NI, P, text_per_item ? 1 : 0, c->ta_vw, c->ta_vb, c->ta_ivw,
+                    c->ta_ivb, c->ta_ow, c->ta_ob, b.avec, r.s);
+    auto text_attn = [&](const float* enc, int64_t ntok, float* cond) {
+        add_rowvec_launch(enc, b.avec, NI, P, ntok, 384, b.U, r.s);
+        GemmDesc g = r.lin(c->mlp0, b.U, 0, NI, ntok, 384);
+        g.C = b.Hm; g.c_bf16 = ab; g.act = ACT_GELU;
+        r.gemm(g, "text.mlp0");
+        GemmDesc g2 = r.lin(c->mlp2, b.Hm, ab, NI, ntok, 384);
+        g2.C = b.Yb; g2.res = b.U;
+        r.gemm(g2, "text.mlp2");
+        LnDesc l;
+        l.x = b.Yb; l.nb = NI; l.N = ntok; l.C = 384; l.w = c->ta_nw; l.b = c->ta_nb; l.out = cond;
+        layernorm_launch(l, r.s);
+    };
+    text_attn(b.x_enc + s0 * d.Nf * 384, d.Nf, b.x_cond);
+    text_attn(b.xt_enc + s0 * d.Nt * 384, d.Nt, b.xt_cond);
+
+    // ---- frequency decoder (ATHTDemucs_v2.py:82-104, 293-297) ----
+    float* const sv[4] = {b.saved[0] + s0 * 512 * Ts * 48, b.saved[1] + s0 * 128 * Ts * 96,
+                          b.saved[2] + s0 * 32 * Ts * 192, b.saved[3] + s0 * 8 * Ts * 384};
+    {
+        // level 0: 8 -> 32 rows, GN+GELU, resize to Tspec rows, + 0.1 * resize(saved[3][:, :192])
+        double* st = r.stats(NI);
+        conv_t(r, c->fdec[0], b.x_cond, NI, 8, (int)Ts, b.G, st, -1);
+        MergeDesc m;
+        m.src = b.G; m.H_src = 32; m.kept = 0; m.C = 192; m.stats = st; m.gn_count = 32 * Ts * 192;
+        m.gn_w = c->fdec[0].gnw; m.gn_b = c->fdec[0].gnb;
+        m.skip = sv[3]; m.H_skip = 8; m.C_skip = 384; m.P = P;
+        m.out = b.D; m.H_out = (int)Ts; m.W = (int)Ts; m.NI = NI;
+        dec_merge_launch(m, r.s);
+        // levels 1..3: Tspec -> 4 Tspec rows; the /4 bilinear resize reads only rows 4d+1, 4d+2
+        const int skH[3] = {32, 128, 512};
+        const int skC[3] = {192, 96, 48};
+        for (int i = 1; i < 4; ++i) {
+            const DecW& w = c->fdec[i];
+            const bool last = i == 3;
+            double* sti = last ? nullptr : r.stats(NI);
+            conv_t(r, w, b.D, NI, (int)Ts, (int)Ts, b.G, sti, last ? 2 : 1);
+            MergeDesc mm;
+            mm.src = b.G; mm.H_src = 4 * (int)Ts; mm.kept = 1; mm.C = w.cout;
+            mm.stats = sti; mm.gn_count = 4 * Ts * Ts * w.cout; mm.gn_w = w.gnw; mm.gn_b = w.gnb;
+            mm.skip = sv[3 - i]; mm.H_skip = skH[i - 1]; mm.C_skip = skC[i - 1]; mm.P = P;
+            mm.H_out = (int)Ts; mm.W = (int)Ts; mm.NI = NI;
+            if (last) {
+                mm.out = b.FO; mm.proj_w = c->fout_w; mm.proj_b = c->fout_b;     // freq_out 1x1 (4 -> 2)
+            } else {
+                mm.out = b.D;
+            }
+            dec_merge_launch(mm, r.s);
+        }
+    }
+    // ---- mask + iSTFT frames (ATHTDemucs_v2.py:297-310) ----
+    istft_frames_launch(b.FO, NI, (int)Ts, P, b.spec + s0 * 2048 * Ts * 4, c->tw, c->win, b.frames, r.s);
+
+    // ---- time decoder (ATHTDemucs_v2.py:125-139, 313-321) ----
+    {
+        const float* svt[4] = {b.saved_t[0] + s0 * d.L[1] * 48, b.saved_t[1] + s0 * d.L[2] * 96,
+                               b.saved_t[2] + s0 * d.L[3] * 192, b.saved_t[3] + s0 * d.L[4] * 384};
+        const void* A = b.xt_cond;
+        int64_t Lin = d.Nt;
+        for (int i = 0; i < 4; ++i) {
+            const DecW& w = c->tdec[i];
+            const bool last = i == 3;
+            double* st = last ? nullptr : r.stats(NI);
+            conv_t(r, w, A, NI, (int)Lin, 1, b.G, st, -1);
+            const int64_t target = d.L[3 - i];       // lengths_t reversed
+            MergeDesc m;
+            m.src = b.G; m.H_src = (int)(4 * Lin); m.kept = 0; m.C = w.cout;
+            m.stats = st; m.gn_count = 4 * Lin * w.cout; m.gn_w = w.gnw; m.gn_b = w.gnb;
+            m.skip = svt[3 - i]; m.H_skip = (int)d.L[4 - i]; m.C_skip = ENC_CH[3 - i]; m.P = P;
+            m.out = b.D; m.H_out = (int)target; m.W = 1; m.NI = NI;
+            dec_merge_launch(m, r.s);
+            A = b.D;
+            Lin = target;
+        }
+    }
+    // ---- iSTFT overlap-add + time_out + denorm + branch sum (ATHTDemucs_v2.py:310-324) ----
+    combine_launch(b.frames, NI, (int)Ts, d.T, c->win2, b.D, c->tout_w, c->tout_b, b.tnorm_std + 2 * s0, P,
+                   out + s0 * P * 2 * d.T, r.s);
+}
+
+// Debug aid: ATHD_DUMP=<dir> makes the forward synchronise at the end and write the main intermediates of the
+// first decode chunk as raw little-endian arrays (<dir>/<name>.f32 / .f64) plus <dir>/index.txt with shapes.
+void dump_all(const Dims& d, const Bufs& b, hipStream_t s) {
+    const char* dir = std::getenv("ATHD_DUMP");
+    if (!dir || !*dir) return;
+    if (hipStreamSynchronize(s) != hipSuccess) return;
+    const int64_t B = d.B, Ts = d.Tspec, NI = std::min(d.B, d.Bc) * d.P;
+    struct E { std::string name; const void* p; int64_t n; std::string shape; };
+    std::vector<E> es = {
+        {"spec", b.spec, B * 2048 * Ts * 4, "B,2048,Ts,4"},
+        {"snorm", b.snorm, 2 * B, "B,2"},
+        {"tnorm_std", b.tnorm_std, 2 * B, "B,2"},
+        {"x_enc", b.x_enc, B * d.Nf * 384, "B,Nf,384"},
+        {"xt_enc", b.xt_enc, B * d.Nt * 384, "B,Nt,384"},
+        {"x_cond", b.x_cond, NI * d.Nf * 384, "NI,Nf,384"},
+        {"xt_cond", b.xt_cond, NI * d.Nt * 384, "NI,Nt,384"},
+        {"FO", b.FO, NI * Ts * Ts * 2, "NI,Ts,Ts,2"},
+        {"E3", b.D, NI * d.T * 4, "NI,T,4"},
+    };
+    for (int i = 0; i < 4; ++i) {
+        es.push_back({"saved" + std::to_string(i), b.saved[i], B * d.F[i + 1] * Ts * ENC_CH[i], "B,F,Ts,C"});
+        es.push_back({"saved_t" + std::to_string(i), b.saved_t[i], B * d.L[i + 1] * ENC_CH[i], "B,L,C"});
+    }
+    std::string idx = std::string(dir) + "/index.txt";
+    FILE* fi = std::fopen(idx.c_str(), "w");
+    for (const auto& e : es) {
+        std::vector<float> h((size_t)e.n);
+        if (hipMemcpy(h.data(), e.p, (size_t)e.n * 4, hipMemcpyDeviceToHost) != hipSuccess) continue;
+        std::string fn = std::string(dir) + "/" + e.name + ".f32";
+        FILE* f = std::fopen(fn.c_str(), "wb");
+        if (f) { std::fwrite(h.data(), 4, h.size(), f); std::fclose(f); }
+        if (fi) std::fprintf(fi, "%s %lld %s\n", e.name.c_str(), (long long)e.n, e.shape.c_str());
+    }
+    if (fi) std::fclose(fi);
+}
+
+int forward_impl(athd_ctx* c, const float* wav, int64_t B, int64_t T, const float* text, bool per_item, int P,
+                 float* out, void* ws, size_t ws_bytes, void* stream) {
+    if (!c) return ATHD_EINVAL;
+    if (!c->finalized) return c->fail(ATHD_ESTATE, "athd_forward before athd_finalize");
+    if (!wav || !text || !out || B <= 0 || T <= 0 || P <= 0) return c->fail(ATHD_EINVAL, "bad forward arguments");
+    if (T > (int64_t)1 << 26) return c->fail(ATHD_EINVAL, "segment too long");
+    const Dims d = make_dims(B, T, P);
+    Bufs b;
+    Arena sz;
+    const size_t need = plan(sz, d, b, c->mode == 1);
+    if (!ws || ws_bytes < need) return c->fail(ATHD_EWORKSPACE, "workspace too small: need " + std::to_string(need));
+    Arena ar;
+    ar.base = (char*)ws;
+    plan(ar, d, b, c->mode == 1);
+    if (hipSetDevice(c->device) != hipSuccess) return c->fail(ATHD_EHIP, "hipSetDevice failed");
+    Run r;
+    r.c = c;
+    r.s = (hipStream_t)stream;
+    r.mode = c->mode;
+    r.actbf = c->mode == 1;
+    r.st_next = b.stats;
+    if (hipMemsetAsync(b.stats, 0, (size_t)b.nstats * 2 * sizeof(double), r.s) != hipSuccess)
+        return c->fail(ATHD_EHIP, "memset failed");
+    encode(r, d, b, wav);
+    for (int64_t ch = 0; ch < d.chunks && r.err == 0; ++ch) {
+        const int64_t s0 = ch * d.Bc;
+        const int64_t bc = std::min(d.Bc, B - s0);
+        decode_chunk(r, d, b, s0, bc, text, per_item, out);
+    }
+    if (d.chunks == 1) dump_all(d, b, r.s);
+    if (r.err) return c->fail(ATHD_EHIP, "launch failed in " + r.what + " (code " + std::to_string(r.err) + ")");
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return c->fail(ATHD_EHIP, std::string("HIP error: ") + hipGetErrorString(e));
+    return ATHD_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t athd_workspace_bytes(athd_ctx* c, int64_t B, int64_t T, int P) {
+    if (!c || B <= 0 || T <= 0 || P <= 0) return 0;
+    Bufs b;
+    Arena a;
+    return plan(a, make_dims(B, T, P), b, c->mode == 1);
+}
+
+int athd_forward(athd_ctx* c, const float* wav, int64_t B, int64_t T, const float* text_emb, float* out, void* ws,
+                 size_t ws_bytes, void* stream) {
+    return forward_impl(c, wav, B, T, text_emb, true, 1, out, ws, ws_bytes, stream);
+}
+
+int athd_forward_prompts(athd_ctx* c, const float* wav, int64_t B, int64_t T, const float* text_table, int P,
+                         float* out, void* ws, size_t ws_bytes, void* stream) {
+    return forward_impl(c, wav, B, T, text_table, false, P, out, ws, ws_bytes, stream);
+}
+
+}  // extern "C"

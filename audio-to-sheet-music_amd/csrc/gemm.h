@@ -1,0 +1,52 @@
+// Implicit-GEMM convolution / linear layer on MFMA (gfx950).
+//
+// One descriptor covers every contraction on the hot path:
+//   Conv2d (k,1) / Conv1d along the "H" axis of a channels-last tensor [nb][H][W][C] with `ntaps` taps,
+//   1x1 convs and Linear layers (ntaps = 1), and one residue class of a stride-4 ConvTranspose (2 taps).
+//   out[b][ho*os+oo][w][n] = epi( sum_{tap,ci} A[b][ho*s+off+tap*dil][w][ci] * Wp[n][tap*C_in+ci] + bias[n] )
+// Weights are pre-packed [N][Kp] (k contiguous, zero padded to Kp % 32 == 0) in the compute dtype.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace athd {
+
+enum Act { ACT_NONE = 0, ACT_GELU = 1, ACT_GLU = 2 };
+
+struct GemmDesc {
+    // A operand (activations), channels-last
+    const void* A = nullptr;
+    int a_bf16 = 0;           // A stored as bf16 (else f32)
+    int nb = 1;               // batch count (GEMM M = nb * H_out * W)
+    int H_in = 1, W = 1, C_in = 0;
+    int a_ld = 0;             // elements between consecutive positions (>= C_in)
+    int64_t a_cs = 1;         // elements between channels (1 = channels-last; the raw (B,2,T) waveform uses T)
+    int64_t a_bs = -1;        // elements between batches (-1: H_in*W*a_ld)
+    int ntaps = 1, in_stride = 1, in_off = 0, dil = 1;
+    int H_out = 1;            // output rows computed per batch
+    const float* a_norm = nullptr;    // optional per-batch {sub, div} on in-bounds A: (a - sub[b]) / div[b]
+    // B operand (packed weights [N][Kp]) and bias
+    const void* Wp = nullptr;
+    int N = 0, K = 0, Kp = 0;
+    const float* bias = nullptr;
+    // C output
+    void* C = nullptr;
+    int c_bf16 = 0;
+    int H_out_total = 1;      // rows in the output tensor per batch
+    int o_stride = 1, o_off = 0;
+    int ldo = 0;              // elements between output positions
+    int col_off = 0;
+    int64_t c_bs = -1;        // elements between output batches (-1: H_out_total*W*ldo)
+    int store = 1;            // 0: compute statistics only
+    // epilogue
+    int act = ACT_NONE;       // ACT_GLU: packed pairs [a(16) | gate(16)] per 32 columns, output N/2 channels
+    const float* res = nullptr;       // residual (same layout as C, f32); out = res + rs[n]*v
+    const float* res_scale = nullptr;
+    const float* row_add = nullptr;   // out += row_add[ho][n]   (freq embedding after encoder level 0)
+    double* stats = nullptr;          // per-batch {sum, sumsq} of the final output value
+};
+
+// mode: 0 = exact fp32 (v_mfma_f32_16x16x4_f32), 1 = bf16 (v_mfma_f32_16x16x32_bf16, fp32 accumulate)
+int gemm_launch(const GemmDesc& d, int mode, hipStream_t s);
+
+}  // namespace athd

@@ -1,0 +1,69 @@
+// Launchers for the non-GEMM kernels of the hot path.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace athd {
+
+// demucs pad1d(reflect) plan for HTDemucs._spec: padded index p -> original sample (or 0)
+struct PadPlan {
+    int64_t L;          // original length
+    int64_t left;       // reflect pad applied to the zero-extended signal
+    int64_t ext_left;   // zero extension on the left (only when L <= max pad)
+    int64_t Lx;         // zero-extended length
+};
+
+// spectral.hip
+void stft_launch(const float* wav, int nb, int64_t T, const PadPlan& pp, int Tspec, const float2* tw,
+                 const float* win, float* spec, hipStream_t s);
+void istft_frames_launch(const float* fo, int NI, int Tspec, int P, const float* spec, const float2* tw,
+                         const float* win, float* frames, hipStream_t s);
+void combine_launch(const float* frames, int NI, int Tspec, int64_t T, const float* win2, const float* xt3,
+                    const float* tw_out, const float* tb_out, const float* tnorm, int P, float* out, hipStream_t s);
+
+// norm.hip
+// per-batch {sum, sumsq} (double) of x[b][0..n)
+void stats_launch(const float* x, int nb, int64_t n, double* stats, hipStream_t s);
+// input normalisation: per batch (mean, 1/(1e-5 + unbiased std)) as floats {mean, inv} and (mean, std)
+void input_norm_params_launch(const double* stats, int nb, int64_t n, float* mean_inv, float* mean_std,
+                              hipStream_t s);
+// h[nb][L*H] = GELU(GN(h)) in place (GroupNorm(1,H), stats over L*H per nb)
+void gn_gelu_launch(float* h, int nb, int64_t per_batch, int H, const double* stats, const float* w,
+                    const float* b, hipStream_t s);
+// x[nb][L][C] += scale[c] * GLU(GN(y))  with y[nb][L][2C]
+void dconv_out_launch(float* x, const float* y, int nb, int64_t L, int C, const double* stats, const float* w,
+                      const float* b, const float* scale, hipStream_t s);
+// x[nb][N][C] = GN(x) in place
+void gn_apply_launch(float* x, int nb, int64_t N, int C, const double* stats, const float* w, const float* b,
+                     hipStream_t s);
+// LayerNorm over C (384 or 512) of rows x[nb*N][C]; optional pending GroupNorm applied first (and written back
+// to x), optional positional table pos[N][C] added after the norm, output f32 or bf16 (may alias x if f32).
+struct LnDesc {
+    float* x = nullptr; int nb = 1; int64_t N = 0; int C = 512;
+    const float* w = nullptr; const float* b = nullptr;
+    const double* gn_stats = nullptr; const float* gn_w = nullptr; const float* gn_b = nullptr;
+    const float* pos = nullptr;
+    void* out = nullptr; int out_bf16 = 0;
+};
+void layernorm_launch(const LnDesc& d, hipStream_t s);
+// U[item][tok][c] = X[item / P][tok][c] + a[item][c]
+void add_rowvec_launch(const float* X, const float* a, int NI, int P, int64_t ntok, int C, float* U, hipStream_t s);
+// a[item] = out_proj(in_v(v_proj(text[item])))   (TextCrossAttention closed form, 384 <- 512)
+void text_vec_launch(const float* text, int NI, int P, int text_per_item, const float* wv, const float* bv,
+                     const float* wiv, const float* biv, const float* wo, const float* bo, float* a, hipStream_t s);
+// decoder merge: out[item][ho][w][c] = resize_H(act(GN(src)))[ho][w][c] + 0.1 * resize_H(skip[item/P][..][c])
+struct MergeDesc {
+    const float* src = nullptr; int H_src = 0;   // logical ConvT output rows
+    int kept = 0;                                // src holds only rows 4d+1, 4d+2 as slots 2d, 2d+1
+    int C = 0;                                   // channels of src and out
+    const double* stats = nullptr; int64_t gn_count = 0; const float* gn_w = nullptr; const float* gn_b = nullptr;
+    const float* skip = nullptr; int H_skip = 0; int C_skip = 0; int P = 1;
+    float* out = nullptr; int H_out = 0; int W = 1; int NI = 1;
+    const float* proj_w = nullptr; const float* proj_b = nullptr;   // optional 1x1 C(=4) -> 2 projection
+};
+void dec_merge_launch(const MergeDesc& d, hipStream_t s);
+// positional tables of the cross-transformer (computed on device with the fp32 op order of demucs)
+void pos2d_launch(float* out, int Fr, int T1, int C, hipStream_t s);   // out[(f*T1+t)][C]
+void pos1d_launch(float* out, int T2, int C, hipStream_t s);           // out[t][C]
+
+}  // namespace athd

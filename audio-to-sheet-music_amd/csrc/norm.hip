@@ -1,0 +1,349 @@
+// Normalisation, elementwise, resize/merge and table kernels of the hot path (gfx950).
+// GroupNorm/LayerNorm statistics are accumulated in fp64 (sum, sum of squares) so that the one-pass
+// variance matches PyTorch's fp32 two-pass/Welford results to rounding.
+#include "common.h"
+#include "kernels.h"
+
+namespace athd {
+
+// --------------------------------------------------------------------------------------------- statistics
+__global__ __launch_bounds__(256) void stats_kernel(const float* __restrict__ x, int64_t n, double* __restrict__ st) {
+    const int64_t b = blockIdx.y;
+    const float* p = x + b * n;
+    double s1 = 0.0, s2 = 0.0;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+        const double v = p[i];
+        s1 += v;
+        s2 += v * v;
+    }
+    s1 = wave_sum_d(s1);
+    s2 = wave_sum_d(s2);
+    __shared__ double sh[2][4];
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) { sh[0][w] = s1; sh[1][w] = s2; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        atomicAdd(&st[2 * b], sh[0][0] + sh[0][1] + sh[0][2] + sh[0][3]);
+        atomicAdd(&st[2 * b + 1], sh[1][0] + sh[1][1] + sh[1][2] + sh[1][3]);
+    }
+}
+
+void stats_launch(const float* x, int nb, int64_t n, double* stats, hipStream_t s) {
+    int blocks = (int)((n + 256 * 16 - 1) / (256 * 16));
+    if (blocks > 512) blocks = 512;
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL(stats_kernel, dim3(blocks, nb), dim3(256), 0, s, x, n, stats);
+}
+
+__global__ void input_norm_params_kernel(const double* st, int nb, int64_t n, float* mean_div, float* mean_std) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= nb) return;
+    const double mean = st[2 * b] / (double)n;
+    double var = (st[2 * b + 1] - st[2 * b] * mean) / (double)(n - 1);     // unbiased (torch.std default)
+    if (var < 0) var = 0;
+    const float stdv = (float)sqrt(var);
+    mean_div[2 * b] = (float)mean;
+    mean_div[2 * b + 1] = 1e-5f + stdv;
+    if (mean_std) { mean_std[2 * b] = (float)mean; mean_std[2 * b + 1] = stdv; }
+}
+
+void input_norm_params_launch(const double* stats, int nb, int64_t n, float* mean_div, float* mean_std, hipStream_t s) {
+    hipLaunchKernelGGL(input_norm_params_kernel, dim3((nb + 63) / 64), dim3(64), 0, s, stats, nb, n, mean_div, mean_std);
+}
+
+ATHD_DEV void gn_params(const double* st, int64_t b, int64_t count, float& mean, float& rstd) {
+    const double m = st[2 * b] / (double)count;
+    double var = st[2 * b + 1] / (double)count - m * m;
+    if (var < 0) var = 0;
+    mean = (float)m;
+    rstd = (float)(1.0 / sqrt(var + 1e-5));
+}
+
+// --------------------------------------------------------------------------------------------- GroupNorm users
+__global__ __launch_bounds__(256) void gn_gelu_kernel(float* __restrict__ h, int64_t per_batch, int H,
+                                                      const double* __restrict__ st, const float* __restrict__ w,
+                                                      const float* __restrict__ bb) {
+    const int64_t b = blockIdx.y;
+    float mean, rstd;
+    gn_params(st, b, per_batch, mean, rstd);
+    float* p = h + b * per_batch;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < per_batch; i += (int64_t)gridDim.x * 256) {
+        const int c = (int)(i % H);
+        p[i] = gelu_erf((p[i] - mean) * rstd * w[c] + bb[c]);
+    }
+}
+
+void gn_gelu_launch(float* h, int nb, int64_t per_batch, int H, const double* stats, const float* w, const float* b,
+                    hipStream_t s) {
+    int blocks = (int)((per_batch + 255) / 256);
+    if (blocks > 1024) blocks = 1024;
+    hipLaunchKernelGGL(gn_gelu_kernel, dim3(blocks, nb), dim3(256), 0, s, h, per_batch, H, stats, w, b);
+}
+
+__global__ __launch_bounds__(256) void dconv_out_kernel(float* __restrict__ x, const float* __restrict__ y, int64_t L,
+                                                        int C, const double* __restrict__ st,
+                                                        const float* __restrict__ w, const float* __restrict__ bb,
+                                                        const float* __restrict__ sc) {
+    const int64_t b = blockIdx.y;
+    float mean, rstd;
+    gn_params(st, b, L * 2 * C, mean, rstd);
+    const int64_t n = L * C;
+    float* xp = x + b * n;
+    const float* yp = y + b * n * 2;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+        const int c = (int)(i % C);
+        const int64_t l = i / C;
+        const float a = (yp[l * 2 * C + c] - mean) * rstd * w[c] + bb[c];
+        const float g = (yp[l * 2 * C + C + c] - mean) * rstd * w[C + c] + bb[C + c];
+        xp[i] = xp[i] + sc[c] * (a * sigmoidf_(g));
+    }
+}
+
+void dconv_out_launch(float* x, const float* y, int nb, int64_t L, int C, const double* stats, const float* w,
+                      const float* b, const float* scale, hipStream_t s) {
+    int blocks = (int)((L * C + 255) / 256);
+    if (blocks > 1024) blocks = 1024;
+    hipLaunchKernelGGL(dconv_out_kernel, dim3(blocks, nb), dim3(256), 0, s, x, y, L, C, stats, w, b, scale);
+}
+
+__global__ __launch_bounds__(256) void gn_apply_kernel(float* __restrict__ x, int64_t per_batch, int C,
+                                                       const double* __restrict__ st, const float* __restrict__ w,
+                                                       const float* __restrict__ bb) {
+    const int64_t b = blockIdx.y;
+    float mean, rstd;
+    gn_params(st, b, per_batch, mean, rstd);
+    float* p = x + b * per_batch;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < per_batch; i += (int64_t)gridDim.x * 256) {
+        const int c = (int)(i % C);
+        p[i] = (p[i] - mean) * rstd * w[c] + bb[c];
+    }
+}
+
+void gn_apply_launch(float* x, int nb, int64_t N, int C, const double* stats, const float* w, const float* b,
+                     hipStream_t s) {
+    int64_t per = N * C;
+    int blocks = (int)((per + 255) / 256);
+    if (blocks > 1024) blocks = 1024;
+    hipLaunchKernelGGL(gn_apply_kernel, dim3(blocks, nb), dim3(256), 0, s, x, per, C, stats, w, b);
+}
+
+// --------------------------------------------------------------------------------------------- LayerNorm
+template <int PER>
+__global__ __launch_bounds__(256) void layernorm_kernel(const LnDesc d) {
+    constexpr int C = PER * 64;
+    const int lane = threadIdx.x & 63;
+    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int64_t rows = (int64_t)d.nb * d.N;
+    if (row >= rows) return;
+    const int64_t b = row / d.N;
+    const int64_t tok = row % d.N;
+    float* xr = d.x + row * C;
+    float v[PER];
+#pragma unroll
+    for (int j = 0; j < PER; ++j) v[j] = xr[lane + 64 * j];
+    if (d.gn_stats) {
+        float gm, gr;
+        gn_params(d.gn_stats, b, d.N * (int64_t)C, gm, gr);
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            const int c = lane + 64 * j;
+            v[j] = (v[j] - gm) * gr * d.gn_w[c] + d.gn_b[c];
+            xr[c] = v[j];
+        }
+    }
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) s += v[j];
+    const float mean = wave_sum(s) * (1.f / C);
+    float q = 0.f;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) { const float t = v[j] - mean; q += t * t; }
+    const float rstd = 1.f / sqrtf(wave_sum(q) * (1.f / C) + 1e-5f);
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        const int c = lane + 64 * j;
+        float y = (v[j] - mean) * rstd * d.w[c] + d.b[c];
+        if (d.pos) y += d.pos[tok * C + c];
+        if (d.out_bf16) ((bf16_t*)d.out)[row * C + c] = f2bf(y);
+        else ((float*)d.out)[row * C + c] = y;
+    }
+}
+
+void layernorm_launch(const LnDesc& d, hipStream_t s) {
+    const int64_t rows = (int64_t)d.nb * d.N;
+    dim3 grid((unsigned)((rows + 3) / 4));
+    if (d.C == 512) hipLaunchKernelGGL(layernorm_kernel<8>, grid, dim3(256), 0, s, d);
+    else hipLaunchKernelGGL(layernorm_kernel<6>, grid, dim3(256), 0, s, d);
+}
+
+// --------------------------------------------------------------------------------------------- text conditioning
+__global__ __launch_bounds__(256) void add_rowvec_kernel(const float* __restrict__ X, const float* __restrict__ a,
+                                                         int P, int64_t ntok, int C, float* __restrict__ U) {
+    const int64_t item = blockIdx.y;
+    const int64_t b = item / P;
+    const int64_t n = ntok * C;
+    const float* xp = X + b * n;
+    float* up = U + item * n;
+    const float* ap = a + item * C;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+        up[i] = xp[i] + ap[i % C];
+}
+
+void add_rowvec_launch(const float* X, const float* a, int NI, int P, int64_t ntok, int C, float* U, hipStream_t s) {
+    int blocks = (int)((ntok * C + 255) / 256);
+    if (blocks > 1024) blocks = 1024;
+    hipLaunchKernelGGL(add_rowvec_kernel, dim3(blocks, NI), dim3(256), 0, s, X, a, P, ntok, C, U);
+}
+
+__global__ __launch_bounds__(256) void text_vec_kernel(const float* __restrict__ text, int P, int per_item,
+                                                       const float* __restrict__ wv, const float* __restrict__ bv,
+                                                       const float* __restrict__ wiv, const float* __restrict__ biv,
+                                                       const float* __restrict__ wo, const float* __restrict__ bo,
+                                                       float* __restrict__ a) {
+    constexpr int D = 384, TD = 512;
+    __shared__ float t[TD];
+    __shared__ float v[D];
+    __shared__ float vi[D];
+    const int item = blockIdx.x;
+    const float* tp = text + (int64_t)(per_item ? item : (item % P)) * TD;
+    for (int i = threadIdx.x; i < TD; i += 256) t[i] = tp[i];
+    __syncthreads();
+    for (int o = threadIdx.x; o < D; o += 256) {
+        float s = 0.f;
+        for (int k = 0; k < TD; ++k) s += wv[(int64_t)o * TD + k] * t[k];
+        v[o] = s + bv[o];
+    }
+    __syncthreads();
+    for (int o = threadIdx.x; o < D; o += 256) {
+        float s = 0.f;
+        for (int k = 0; k < D; ++k) s += wiv[(int64_t)o * D + k] * v[k];
+        vi[o] = s + biv[o];
+    }
+    __syncthreads();
+    for (int o = threadIdx.x; o < D; o += 256) {
+        float s = 0.f;
+        for (int k = 0; k < D; ++k) s += wo[(int64_t)o * D + k] * vi[k];
+        a[(int64_t)item * D + o] = s + bo[o];
+    }
+}
+
+void text_vec_launch(const float* text, int NI, int P, int text_per_item, const float* wv, const float* bv,
+                     const float* wiv, const float* biv, const float* wo, const float* bo, float* a, hipStream_t s) {
+    hipLaunchKernelGGL(text_vec_kernel, dim3(NI), dim3(256), 0, s, text, P, text_per_item, wv, bv, wiv, biv, wo, bo, a);
+}
+
+// --------------------------------------------------------------------------------------------- decoder merge
+ATHD_DEV float merge_src(const MergeDesc& d, int64_t item, int i, int w, int c, float mean, float rstd) {
+    int slot = i;
+    int rows = d.H_src;
+    if (d.kept) {
+        slot = 2 * (i >> 2) + ((i & 3) == 2 ? 1 : 0);
+        rows = 2 * (d.H_src >> 2);
+    }
+    float x = d.src[((item * rows + slot) * (int64_t)d.W + w) * d.C + c];
+    if (d.stats) x = gelu_erf((x - mean) * rstd * d.gn_w[c] + d.gn_b[c]);
+    return x;
+}
+
+ATHD_DEV float merge_one(const MergeDesc& d, int64_t item, int ho, int w, int c, float mean, float rstd) {
+    float val;
+    if (d.H_src == d.H_out) {
+        val = merge_src(d, item, ho, w, c, mean, rstd);
+    } else {
+        const LinIdx li = lin_index(ho, d.H_src, d.H_out);
+        val = li.l0 * merge_src(d, item, li.i0, w, c, mean, rstd) + li.l1 * merge_src(d, item, li.i1, w, c, mean, rstd);
+    }
+    const int64_t sb = item / d.P;
+    const float* sk = d.skip + sb * (int64_t)d.H_skip * d.W * d.C_skip;
+    float sv;
+    if (d.H_skip == d.H_out) {
+        sv = sk[((int64_t)ho * d.W + w) * d.C_skip + c];
+    } else {
+        const LinIdx lj = lin_index(ho, d.H_skip, d.H_out);
+        sv = lj.l0 * sk[((int64_t)lj.i0 * d.W + w) * d.C_skip + c] + lj.l1 * sk[((int64_t)lj.i1 * d.W + w) * d.C_skip + c];
+    }
+    return val + sv * 0.1f;
+}
+
+__global__ __launch_bounds__(256) void dec_merge_kernel(const MergeDesc d) {
+    const int64_t item = blockIdx.y;
+    float mean = 0.f, rstd = 1.f;
+    if (d.stats) gn_params(d.stats, item, d.gn_count, mean, rstd);
+    const int64_t n = (int64_t)d.H_out * d.W * d.C;
+    float* op = d.out + item * n;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+        const int c = (int)(i % d.C);
+        const int64_t pw = i / d.C;
+        const int w = (int)(pw % d.W);
+        const int ho = (int)(pw / d.W);
+        op[i] = merge_one(d, item, ho, w, c, mean, rstd);
+    }
+}
+
+__global__ __launch_bounds__(256) void dec_merge_proj_kernel(const MergeDesc d) {
+    const int64_t item = blockIdx.y;
+    float mean = 0.f, rstd = 1.f;
+    if (d.stats) gn_params(d.stats, item, d.gn_count, mean, rstd);
+    const int64_t n = (int64_t)d.H_out * d.W;
+    float* op = d.out + item * n * 2;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+        const int w = (int)(i % d.W);
+        const int ho = (int)(i / d.W);
+        float m[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) m[c] = merge_one(d, item, ho, w, c, mean, rstd);
+#pragma unroll
+        for (int o = 0; o < 2; ++o)
+            op[i * 2 + o] = d.proj_b[o] + (d.proj_w[o * 4 + 0] * m[0] + d.proj_w[o * 4 + 1] * m[1] +
+                                           d.proj_w[o * 4 + 2] * m[2] + d.proj_w[o * 4 + 3] * m[3]);
+    }
+}
+
+void dec_merge_launch(const MergeDesc& d, hipStream_t s) {
+    const int64_t n = (int64_t)d.H_out * d.W * (d.proj_w ? 1 : d.C);
+    int blocks = (int)((n + 255) / 256);
+    if (blocks > 2048) blocks = 2048;
+    if (d.proj_w) hipLaunchKernelGGL(dec_merge_proj_kernel, dim3(blocks, d.NI), dim3(256), 0, s, d);
+    else hipLaunchKernelGGL(dec_merge_kernel, dim3(blocks, d.NI), dim3(256), 0, s, d);
+}
+
+// --------------------------------------------------------------------------------------------- position tables
+__global__ void pos2d_kernel(float* out, int Fr, int T1, int C) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t n = (int64_t)Fr * T1 * C;
+    if (i >= n) return;
+    const int c = (int)(i % C);
+    const int64_t tok = i / C;
+    const int t = (int)(tok % T1), f = (int)(tok / T1);
+    const int half = C / 2;                              // d_model/2 channels per axis
+    const float k = -(float)(log(10000.0) / (double)half);
+    const int cc = c < half ? c : c - half;
+    const float div = expf((float)(cc & ~1) * k);        // arange(0, half, 2)[cc/2] * -(ln(1e4)/half)
+    const float pos = (float)(c < half ? t : f);         // first half: width (time) axis, second: height (freq)
+    const float ph = pos * div;
+    out[i] = (cc & 1) ? cosf(ph) : sinf(ph);
+}
+
+void pos2d_launch(float* out, int Fr, int T1, int C, hipStream_t s) {
+    const int64_t n = (int64_t)Fr * T1 * C;
+    hipLaunchKernelGGL(pos2d_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, out, Fr, T1, C);
+}
+
+__global__ void pos1d_kernel(float* out, int T2, int C) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (int64_t)T2 * C) return;
+    const int c = (int)(i % C);
+    const int t = (int)(i / C);
+    const int half = C / 2;
+    const int a = c < half ? c : c - half;
+    const float e = (float)a / (float)(half - 1);
+    const float den = powf(10000.0f, e);
+    const float ph = (float)t / den;
+    out[i] = c < half ? cosf(ph) : sinf(ph);
+}
+
+void pos1d_launch(float* out, int T2, int C, hipStream_t s) {
+    hipLaunchKernelGGL(pos1d_kernel, dim3((unsigned)(((int64_t)T2 * C + 255) / 256)), dim3(256), 0, s, out, T2, C);
+}
+
+}  // namespace athd

@@ -1,0 +1,84 @@
+/*
+ * athd - C ABI of the MI355X-native AudioTextHTDemucs hot path (libathd.so).
+ *
+ * Replaces, for the per-segment inference path, the reference's Python surface:
+ *   AudioTextHTDemucs(htdemucs, clap, tokenizer)          /root/reference/src/models/stem_separation/ATHTDemucs_v2.py:151-188
+ *   model.load_state_dict(ckpt["model_state_dict"], strict=False)   test_inference.py:34-35
+ *   model.forward(wav, text) -> (B,2,T)                   ATHTDemucs_v2.py:250-326
+ * The CLAP text tower (ATHTDemucs_v2.py:238-248) stays on the host side: callers pass prompt embeddings
+ * (B x 512 or P x 512 fp32, L2-normalised as ClapModel.get_text_features returns them).
+ *
+ * Conventions: plain pointers and sizes, no torch types.  All device pointers are HIP device memory owned by
+ * the caller (wav, text embeddings, output, workspace); the context owns the packed weights.  Every call
+ * returns 0 on success or a negative athd_status; the message is in athd_last_error().  Nothing is thrown
+ * across the ABI.  Work is enqueued on the caller's stream (a hipStream_t passed as void*, NULL = default
+ * stream); athd_forward* do not synchronise the host and do not allocate, so they can be captured in a graph.
+ * One context per device; calls on one context must be serialised by the caller.
+ */
+#ifndef ATHD_H
+#define ATHD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct athd_ctx athd_ctx;
+
+enum athd_status {
+    ATHD_OK = 0,
+    ATHD_EINVAL = -1,      /* bad argument / shape */
+    ATHD_EKEY = -2,        /* unknown, missing or mis-shaped weight */
+    ATHD_ESTATE = -3,      /* not finalized / already finalized */
+    ATHD_EHIP = -4,        /* HIP runtime error */
+    ATHD_EWORKSPACE = -5   /* workspace too small */
+};
+
+enum athd_dtype { ATHD_F32 = 0, ATHD_BF16 = 1 };
+
+/* ABI version (major*100 + minor). */
+int athd_version(void);
+
+/* Create a context on HIP device `device`.  dtype: ATHD_F32 = exact fp32 MFMA everywhere (parity mode),
+ * ATHD_BF16 = bf16 MFMA operands with fp32 accumulation/normalisation (throughput mode). */
+int athd_create(athd_ctx** out, int device, int dtype);
+
+/* Stage one weight tensor under its reference state-dict key (e.g. "htdemucs.encoder.0.conv.weight",
+ * "text_attn.out_mlp.0.weight", "freq_decoder.layers.1.0.weight").  host points to contiguous fp32
+ * (src_dtype 0) with the given shape.  Keys outside the hot path (clap.*, htdemucs.decoder.*, ...) are
+ * accepted and ignored, mirroring load_state_dict(strict=False). */
+int athd_set_weight(athd_ctx* ctx, const char* key, const void* host, const int64_t* shape, int ndim,
+                    int src_dtype);
+
+/* Number / names of the weight keys the hot path requires (reference names). */
+int athd_num_required_keys(void);
+const char* athd_required_key(int i);
+
+/* Validate that every required key is present with the right shape, pack (transpose, tap-major, GLU pair
+ * order, ConvTranspose residue split, bf16 conversion) and upload. */
+int athd_finalize(athd_ctx* ctx);
+
+/* Workspace bytes needed by athd_forward (P = 1) / athd_forward_prompts (P prompts) for B segments of
+ * T samples. */
+size_t athd_workspace_bytes(athd_ctx* ctx, int64_t B, int64_t T, int P);
+
+/* wav: (B,2,T) f32, text_emb: (B,512) f32 -> out: (B,2,T) f32.  == AudioTextHTDemucs.forward(wav, text). */
+int athd_forward(athd_ctx* ctx, const float* wav, int64_t B, int64_t T, const float* text_emb, float* out,
+                 void* workspace, size_t workspace_bytes, void* stream);
+
+/* Encode once, decode once per prompt: wav (B,2,T), text_table (P,512) -> out (B,P,2,T); equal to P calls of
+ * athd_forward because the encoder and cross-transformer do not see the prompt (ATHTDemucs_v2.py:278-283). */
+int athd_forward_prompts(athd_ctx* ctx, const float* wav, int64_t B, int64_t T, const float* text_table, int P,
+                         float* out, void* workspace, size_t workspace_bytes, void* stream);
+
+/* Last error message of this context ("" if none). */
+const char* athd_last_error(athd_ctx* ctx);
+
+void athd_destroy(athd_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ATHD_H */

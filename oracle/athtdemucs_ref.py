@@ -162,6 +162,8 @@ class AudioTextHTDemucsRef:
         x_cond, xt_cond = self.text_attn(x_enc, xt_enc, text_emb)
         x_dec = self.freq_decoder(x_cond, saved[::-1], lengths[::-1])
         x_dec = F.conv2d(x_dec, *self.freq_out)
+        if capture is not None:
+            capture["x_fo"] = x_dec
         x_dec = F.interpolate(x_dec, size=(Fq, T_spec), mode="bilinear", align_corners=False)
         mask = torch.sigmoid(x_dec)
         mag_stereo = mag[:, :2]
@@ -170,6 +172,8 @@ class AudioTextHTDemucsRef:
         masked_z = masked_spec * phase
         freq_wav = self.htdemucs._ispec(masked_z, original_length)
         xt_dec = self.time_decoder(xt_cond, saved_t[::-1], lengths_t[::-1])
+        if capture is not None:
+            capture["xt_dec3"] = xt_dec
         xt_dec = F.conv1d(xt_dec, *self.time_out)
         if xt_dec.shape[-1] != original_length:
             xt_dec = F.interpolate(xt_dec, size=original_length, mode="linear", align_corners=False)
