@@ -33,6 +33,8 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmDesc d) {
     constexpr int AROWS = BM / 64;                 // A rows loaded per thread (8 k each)
     constexpr int BGROUPS = (BN * 4 + 255) / 256;  // B groups per thread
     __shared__ __attribute__((aligned(16))) T lds[2][(BM + BN) * LD];
+    constexpr int MAXG = 32;                       // GroupNorm groups tracked per block in LDS
+    __shared__ double st_lds[2 * MAXG];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -101,6 +103,21 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmDesc d) {
                 } else {
 #pragma unroll
                     for (int j = 0; j < 8; ++j) v[j] = 0.f;
+                }
+            } else if (d.ntaps == 1) {
+                const int row = a_h0[i];
+                const bool rok = a_ok[i] && row >= 0 && row < d.H_in;
+                const int64_t rb = a_base[i] + (int64_t)row * rowpitch;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const int kk = k + j;
+                    float x = 0.f;
+                    if (rok && kk < d.K) {
+                        const int64_t off = rb + (int64_t)kk * d.a_cs;
+                        x = d.a_bf16 ? bf2f(((const bf16_t*)d.A)[off]) : ((const float*)d.A)[off];
+                        if (d.a_norm) x = (x - d.a_norm[2 * a_b[i]]) / d.a_norm[2 * a_b[i] + 1];
+                    }
+                    v[j] = x;
                 }
             } else {
 #pragma unroll
@@ -176,6 +193,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmDesc d) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
+    if (d.stats && threadIdx.x < 2 * MAXG) st_lds[threadIdx.x] = 0.0;
     load_tile(0);
     store_tile(0);
     __syncthreads();
@@ -230,22 +248,15 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmDesc d) {
     const int64_t HW = (int64_t)d.H_out * d.W;
     const int64_t c_bs = d.c_bs >= 0 ? d.c_bs : (int64_t)d.H_out_total * d.W * d.ldo;
     const int Nout = (d.act == ACT_GLU) ? d.N / 2 : d.N;
-    float s1 = 0.f, s2 = 0.f;
     const bool want_stats = d.stats != nullptr;
-    bool single_batch = true;
-    int64_t blk_b = 0;
-    if (want_stats) {
-        int64_t mlast = m0 + BM - 1;
-        if (mlast >= M) mlast = M - 1;
-        blk_b = m0 / HW;
-        single_batch = (mlast / HW) == blk_b;
-    }
+    const int64_t g0 = m0 / HW;                 // first GroupNorm group (batch index) touched by this block
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int64_t m = m0 + wm0 + 16 * i + 4 * (lane >> 4) + r;
-            if (m >= M) continue;
+            float p1 = 0.f, p2 = 0.f;                 // this lane's part of the row sums (stats)
+            if (m < M) {
             const int w = (int)(m % d.W);
             const int64_t t = m / d.W;
             const int ho = (int)(t % d.H_out);
@@ -278,23 +289,43 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmDesc d) {
                     if (d.act == ACT_GELU) v = gelu_erf(v);
                     if (d.row_add) v += d.row_add[(int64_t)ho * Nout + n];
                     if (d.res) v = d.res[obase + n] + (d.res_scale ? d.res_scale[n] : 1.f) * v;
-                    if (want_stats) {   // statistics of the final value (GroupNorm input)
-                        if (single_batch) { s1 += v; s2 += v * v; }
-                        else { atomicAdd(&d.stats[2 * b], (double)v); atomicAdd(&d.stats[2 * b + 1], (double)v * (double)v); }
-                    }
+                    p1 += v;                  // statistics of the final value (GroupNorm input)
+                    p2 += v * v;
                     if (d.store) {
                         if (d.c_bf16) ((bf16_t*)d.C)[obase + n] = f2bf(v);
                         else ((float*)d.C)[obase + n] = v;
                     }
                 }
             }
+            }  // m < M
+            if (want_stats) {
+                // the 16 lanes sharing (lane >> 4) hold the same row: reduce across them, one LDS add per row
+#pragma unroll
+                for (int o = 1; o < 16; o <<= 1) {
+                    p1 += __shfl_xor(p1, o, 64);
+                    p2 += __shfl_xor(p2, o, 64);
+                }
+                if (fr == 0 && m < M) {
+                    const int64_t gi = m / HW - g0;
+                    if (gi < MAXG) {
+                        atomicAdd(&st_lds[2 * gi], (double)p1);
+                        atomicAdd(&st_lds[2 * gi + 1], (double)p2);
+                    } else {
+                        atomicAdd(&d.stats[2 * (g0 + gi)], (double)p1);
+                        atomicAdd(&d.stats[2 * (g0 + gi) + 1], (double)p2);
+                    }
+                }
+            }
         }
     }
-    if (want_stats && single_batch) {
-        double t1 = wave_sum_d((double)s1), t2 = wave_sum_d((double)s2);
-        if (lane == 0) {
-            atomicAdd(&d.stats[2 * blk_b], t1);
-            atomicAdd(&d.stats[2 * blk_b + 1], t2);
+    if (want_stats) {
+        __syncthreads();
+        if (threadIdx.x < MAXG) {
+            const double a = st_lds[2 * threadIdx.x], q = st_lds[2 * threadIdx.x + 1];
+            if (a != 0.0 || q != 0.0) {
+                atomicAdd(&d.stats[2 * (g0 + threadIdx.x)], a);
+                atomicAdd(&d.stats[2 * (g0 + threadIdx.x) + 1], q);
+            }
         }
     }
 }

@@ -97,7 +97,8 @@ def test_full_segment_6s(models, oracle_model, text_table, dt):
 
 
 def test_forward_prompts_matches_forward(models):
-    """Encode-once/decode-P path == P separate forwards (bit-identical: same kernels, same order)."""
+    """Encode-once/decode-P path == P separate forwards (same kernels; GroupNorm statistics are summed with
+    fp64 atomics whose order varies, so equality is to fp32 rounding, not bitwise)."""
     from athd.synth import synthetic_batch
     wav = torch.as_tensor(synthetic_batch(3, 50000)).cuda()
     m = models["bf16"]
@@ -105,7 +106,7 @@ def test_forward_prompts_matches_forward(models):
     multi = m.forward_prompts(wav, prompts)
     for p, name in enumerate(prompts):
         single = m(wav, name)
-        assert torch.equal(multi[:, p], single), name
+        assert torch.allclose(multi[:, p], single, atol=1e-5, rtol=1e-4), name
 
 
 def test_batch_independence(models):
