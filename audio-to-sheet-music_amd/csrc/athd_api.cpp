@@ -199,12 +199,26 @@ int athd_finalize(athd_ctx* c) {
             for (int d = 0; d < 2; ++d) {
                 const std::string q = p + ".dconv.layers." + std::to_string(d);
                 e.dc.c3[d] = c->conv_gemm(q + ".0.weight", q + ".0.bias", C / 8, C, 3);
-                e.dc.c1[d] = c->conv_gemm(q + ".3.weight", q + ".3.bias", 2 * C, C / 8, 1);
+                // 1x1 conv in GLU pair order; its GroupNorm affine permuted identically (fused GN->GLU epilogue)
+                e.dc.c1[d] = c->conv_gemm(q + ".3.weight", q + ".3.bias", 2 * C, C / 8, 1, true);
                 e.dc.g1w[d] = c->up_key(q + ".1.weight");
                 e.dc.g1b[d] = c->up_key(q + ".1.bias");
-                e.dc.g2w[d] = c->up_key(q + ".4.weight");
-                e.dc.g2b[d] = c->up_key(q + ".4.bias");
+                e.dc.g2w[d] = c->up_f32(athd_ctx::glu_order(c->W(q + ".4.weight").v));
+                e.dc.g2b[d] = c->up_f32(athd_ctx::glu_order(c->W(q + ".4.bias").v));
                 e.dc.scale[d] = c->up_key(q + ".6.scale");
+                if (C <= 96) {
+                    const auto& w3 = c->W(q + ".0.weight").v;      // [H][C][3] -> [H][tap*C + c]
+                    const int H = C / 8;
+                    std::vector<float> t3((size_t)H * 3 * C);
+                    for (int j = 0; j < H; ++j)
+                        for (int ci = 0; ci < C; ++ci)
+                            for (int t = 0; t < 3; ++t) t3[((size_t)j * 3 + t) * C + ci] = w3[((size_t)j * C + ci) * 3 + t];
+                    e.dc.w3f[d] = c->up_f32(t3);
+                    e.dc.w1f[d] = c->up_key(q + ".3.weight");        // [2C][H][1] == [2C][H]
+                    e.dc.b1f[d] = c->up_key(q + ".3.bias");
+                    e.dc.g2wf[d] = c->up_key(q + ".4.weight");
+                    e.dc.g2bf[d] = c->up_key(q + ".4.bias");
+                }
             }
         }
         cf = ct = ENC_CH[i];
@@ -283,14 +297,21 @@ int athd_finalize(athd_ctx* c) {
             dw.cout = DEC_CH[i + 1];
             const auto& w = c->W(p + ".0.weight").v;
             const auto& b = c->W(p + ".0.bias").v;
-            for (int r = 0; r < 4; ++r) {
-                std::vector<float> pk((size_t)dw.cout * 2 * dw.cin);
-                for (int co = 0; co < dw.cout; ++co)
-                    for (int ci = 0; ci < dw.cin; ++ci) {
-                        pk[(size_t)co * 2 * dw.cin + ci] = w[((size_t)ci * dw.cout + co) * 8 + RES_K0[r]];
-                        pk[(size_t)co * 2 * dw.cin + dw.cin + ci] = w[((size_t)ci * dw.cout + co) * 8 + RES_K1[r]];
+            for (int pi = 0; pi < 2; ++pi) {          // rows [residue 2pi | residue 2pi+1], K = [tap0 | tap1]
+                std::vector<float> pk((size_t)2 * dw.cout * 2 * dw.cin);
+                std::vector<float> bb(2 * dw.cout);
+                for (int h = 0; h < 2; ++h) {
+                    const int r = 2 * pi + h;
+                    for (int co = 0; co < dw.cout; ++co) {
+                        const size_t row = (size_t)(h * dw.cout + co) * 2 * dw.cin;
+                        for (int ci = 0; ci < dw.cin; ++ci) {
+                            pk[row + ci] = w[((size_t)ci * dw.cout + co) * 8 + RES_K0[r]];
+                            pk[row + dw.cin + ci] = w[((size_t)ci * dw.cout + co) * 8 + RES_K1[r]];
+                        }
+                        bb[h * dw.cout + co] = b[co];
                     }
-                dw.res[r] = c->up_gemm(pk, dw.cout, 2 * dw.cin, b);
+                }
+                dw.pair[pi] = c->up_gemm(pk, 2 * dw.cout, 2 * dw.cin, bb);
             }
             if (i < 3) {
                 dw.gnw = c->up_key(p + ".1.weight");

@@ -23,6 +23,10 @@ struct GemmW {
 struct DConvW {
     GemmW c3[2], c1[2];
     float *g1w[2], *g1b[2], *g2w[2], *g2b[2], *scale[2];
+    // natural-order fp32 copies for the VALU kernels of the narrow levels (C <= 96): conv3 [H][3C] (tap-major k),
+    // 1x1 [2C][H], its bias and GroupNorm affine
+    float *w3f[2] = {nullptr, nullptr}, *w1f[2] = {nullptr, nullptr}, *b1f[2] = {nullptr, nullptr};
+    float *g2wf[2] = {nullptr, nullptr}, *g2bf[2] = {nullptr, nullptr};
 };
 
 struct EncW {
@@ -39,7 +43,7 @@ struct TLayerW {
 
 struct DecW {
     int cin = 0, cout = 0;
-    GemmW res[4];
+    GemmW pair[2];          // ConvTranspose residue pairs {0,1} (taps u-1,u) and {2,3} (taps u,u+1), N = 2*cout
     float *gnw = nullptr, *gnb = nullptr;
 };
 
@@ -122,7 +126,7 @@ struct athd_ctx {
         GemmW g;
         g.N = N;
         g.K = K;
-        g.Kp = (int)rup(K, 32);
+        g.Kp = (int)rup(K, 64);
         if (mode == 1) {
             std::vector<uint16_t> p((size_t)N * g.Kp, 0);
             for (int n = 0; n < N; ++n)
@@ -148,19 +152,23 @@ struct athd_ctx {
                 for (int t = 0; t < taps; ++t) p[((size_t)co * taps + t) * cin + ci] = w[((size_t)co * cin + ci) * taps + t];
         std::vector<float> b = W(bk).v;
         if (glu) {   // pair order: per 32 packed rows [a(16q..16q+15) | gate(C+16q..)]
-            const int C = cout / 2;
-            std::vector<float> q(p.size()), qb(b.size());
+            std::vector<float> q(p.size());
             const int K = taps * cin;
-            for (int pr = 0; pr < cout; ++pr) {
-                int qq = pr / 32, s = pr % 32;
-                int src = s < 16 ? 16 * qq + s : C + 16 * qq + (s - 16);
-                std::memcpy(&q[(size_t)pr * K], &p[(size_t)src * K], K * 4);
-                qb[pr] = b[src];
-            }
+            for (int pr = 0; pr < cout; ++pr)
+                std::memcpy(&q[(size_t)pr * K], &p[(size_t)glu_src(pr, cout) * K], K * 4);
             p.swap(q);
-            b.swap(qb);
+            b = glu_order(b);
         }
         return up_gemm(p, cout, taps * cin, b);
+    }
+    static int glu_src(int pr, int n) {
+        const int C = n / 2, qq = pr / 32, s = pr % 32;
+        return s < 16 ? 16 * qq + s : C + 16 * qq + (s - 16);
+    }
+    static std::vector<float> glu_order(const std::vector<float>& v) {
+        std::vector<float> o(v.size());
+        for (size_t i = 0; i < v.size(); ++i) o[i] = v[glu_src((int)i, (int)v.size())];
+        return o;
     }
     GemmW lin_gemm(const std::string& wk, const std::string& bk, int row0 = 0, int rows = -1) {
         const HostT& w = W(wk);

@@ -51,7 +51,7 @@ struct Bufs {
     float *snorm, *tnorm_div, *tnorm_std;
     float* saved[4];
     float* saved_t[4];
-    float *ybuf, *hbuf, *y2buf;
+    float *ybuf, *hbuf;
     float *X, *XT;
     void *H[4], *QKV, *O, *F1;
     float *pos2d, *pos1d, *x_enc, *xt_enc;
@@ -88,7 +88,6 @@ size_t plan(Arena& ar, const Dims& d, Bufs& b, bool actbf) {
     }
     b.ybuf = ar.take<float>(ymax);
     b.hbuf = ar.take<float>(hmax);
-    b.y2buf = ar.take<float>(2 * ymax);
     b.X = ar.take<float>(B * d.Nf * 512);
     b.XT = ar.take<float>(B * d.Nt * 512);
     for (int i = 0; i < 4; ++i) b.H[i] = act(B * d.Nmax * 512);
@@ -168,12 +167,21 @@ struct Run {
 };
 
 // One encoder level's DConv (2 residual layers) on x viewed as [nb][L][C] (freq: nb = B*F rows along time).
+// Per layer: h = conv3(x) (+stats) -> GN+GELU in place -> 1x1 conv twice: pass 1 only accumulates the GroupNorm
+// statistics of its 2C outputs, pass 2 recomputes them (K = C/8 is tiny) and applies GN -> GLU -> LayerScale
+// -> residual in the epilogue, writing x in place.  The 2C-channel intermediate never touches HBM.
 void dconv(Run& r, const EncW& e, const Bufs& b, float* x, int64_t nb, int64_t L) {
     const int C = e.cout, Hh = C / 8;
     for (int dd = 0; dd < 2; ++dd) {
         const int dil = 1 << dd;
         double* st_h = r.stats(nb);
         double* st_y = r.stats(nb);
+        if (C <= 96) {   // narrow levels: HBM-bound VALU kernels (dconv.hip)
+            r.check(dconv_small_launch(x, b.hbuf, nb, L, C, dil, e.dc.w3f[dd], e.dc.c3[dd].bias, e.dc.g1w[dd],
+                                       e.dc.g1b[dd], e.dc.w1f[dd], e.dc.b1f[dd], e.dc.g2wf[dd], e.dc.g2bf[dd],
+                                       e.dc.scale[dd], st_h, st_y, r.s), "dconv_small");
+            continue;
+        }
         GemmDesc g;
         g.A = x; g.nb = (int)nb; g.H_in = (int)L; g.W = 1; g.C_in = C; g.a_ld = C;
         g.ntaps = 3; g.in_stride = 1; g.in_off = -dil; g.dil = dil; g.H_out = (int)L;
@@ -184,9 +192,13 @@ void dconv(Run& r, const EncW& e, const Bufs& b, float* x, int64_t nb, int64_t L
         GemmDesc g2;
         g2.A = b.hbuf; g2.nb = (int)nb; g2.H_in = (int)L; g2.W = 1; g2.C_in = Hh; g2.a_ld = Hh; g2.H_out = (int)L;
         g2.Wp = e.dc.c1[dd].w; g2.N = 2 * C; g2.K = Hh; g2.Kp = e.dc.c1[dd].Kp; g2.bias = e.dc.c1[dd].bias;
-        g2.C = b.y2buf; g2.H_out_total = (int)L; g2.ldo = 2 * C; g2.stats = st_y;
-        r.gemm(g2, "dconv.conv1x1");
-        dconv_out_launch(x, b.y2buf, (int)nb, L, C, st_y, e.dc.g2w[dd], e.dc.g2b[dd], e.dc.scale[dd], r.s);
+        g2.C = x; g2.H_out_total = (int)L; g2.ldo = C;
+        GemmDesc g1 = g2;
+        g1.stats = st_y; g1.store = 0;
+        r.gemm(g1, "dconv.conv1x1.stats");
+        g2.act = ACT_GLU; g2.gn_stats = st_y; g2.gn_count = L * 2 * C; g2.gn_w = e.dc.g2w[dd]; g2.gn_b = e.dc.g2b[dd];
+        g2.res = x; g2.res_scale = e.dc.scale[dd];
+        r.gemm(g2, "dconv.conv1x1.apply");
     }
 }
 
@@ -359,21 +371,24 @@ void encode(Run& r, const Dims& d, const Bufs& b, const float* wav) {
     }
 }
 
-// ConvTranspose (k8, s4, p2) along H as 4 residue GEMMs; rows 4u+rho.  keep: -1 = store all rows (4*H_in rows),
-// 1 = store only rho 1, 2 as slots 2u, 2u+1 (stats of all 4 if st != null), 2 = only rho 1, 2 (no stats).
-void conv_t(Run& r, const DecW& w, const void* A, int nb, int H_in, int W, float* out, double* st, int keep) {
-    for (int rho = 0; rho < 4; ++rho) {
-        const bool kept_row = (rho == 1 || rho == 2);
-        if (keep == 2 && !kept_row) continue;
+// ConvTranspose (k8, s4, p2) along H as two GEMMs, one per residue pair: output rows 4u+{0,1} read input rows
+// u-1, u; rows 4u+{2,3} read u, u+1.  Each GEMM has N = 2*cout (columns >= cout belong to the odd residue).
+// keep < 0: store all rows (4*H_in rows).  keep > 0: store only rows 4u+1, 4u+2 as slots 2u, 2u+1 (the only
+// rows the following exact /4 bilinear resize reads); statistics (if st) still cover all four residues.
+void conv_t(Run& r, const DecW& w, const void* A, int a_bf16, int nb, int H_in, int W, void* out, int out_bf16,
+            double* st, int keep) {
+    for (int pi = 0; pi < 2; ++pi) {
         GemmDesc g;
-        g.A = A; g.nb = nb; g.H_in = H_in; g.W = W; g.C_in = w.cin; g.a_ld = w.cin;
-        g.ntaps = 2; g.in_stride = 1; g.in_off = RES_OFF[rho]; g.dil = 1; g.H_out = H_in;
-        g.Wp = w.res[rho].w; g.N = w.cout; g.K = w.res[rho].K; g.Kp = w.res[rho].Kp; g.bias = w.res[rho].bias;
-        g.C = out; g.ldo = w.cout; g.stats = st;
+        g.A = A; g.a_bf16 = a_bf16; g.nb = nb; g.H_in = H_in; g.W = W; g.C_in = w.cin; g.a_ld = w.cin;
+        g.ntaps = 2; g.in_stride = 1; g.in_off = pi == 0 ? -1 : 0; g.dil = 1; g.H_out = H_in;
+        g.Wp = w.pair[pi].w; g.N = 2 * w.cout; g.K = w.pair[pi].K; g.Kp = w.pair[pi].Kp; g.bias = w.pair[pi].bias;
+        g.C = out; g.c_bf16 = out_bf16; g.ldo = w.cout; g.stats = st; g.col_split = w.cout;
         if (keep < 0) {
-            g.H_out_total = 4 * H_in; g.o_stride = 4; g.o_off = rho;
+            g.H_out_total = 4 * H_in; g.o_stride = 4; g.o_off = 2 * pi; g.hi_row_off = 1; g.store_mask = 3;
         } else {
-            g.H_out_total = 2 * H_in; g.o_stride = 2; g.o_off = rho == 2 ? 1 : 0; g.store = kept_row ? 1 : 0;
+            g.H_out_total = 2 * H_in; g.o_stride = 2;
+            if (pi == 0) { g.o_off = 0; g.hi_row_off = 0; g.store_mask = 2; }   // residue 1 -> slot 2u
+            else { g.o_off = 1; g.store_mask = 1; }                              // residue 2 -> slot 2u+1
         }
         r.gemm(g, "conv_transpose");
     }
@@ -398,7 +413,7 @@ void decode_chunk(Run& r, const Dims& d, const Bufs& b, int64_t s0, int64_t Bc, 
         g2.C = b.Yb; g2.res = b.U;
         r.gemm(g2, "text.mlp2");
         LnDesc l;
-        l.x = b.Yb; l.nb = NI; l.N = ntok; l.C = 384; l.w = c->ta_nw; l.b = c->ta_nb; l.out = cond;
+        l.x = b.Yb; l.nb = NI; l.N = ntok; l.C = 384; l.w = c->ta_nw; l.b = c->ta_nb; l.out = cond; l.out_bf16 = ab;
         layernorm_launch(l, r.s);
     };
     text_attn(b.x_enc + s0 * d.Nf * 384, d.Nf, b.x_cond);
@@ -408,14 +423,15 @@ void decode_chunk(Run& r, const Dims& d, const Bufs& b, int64_t s0, int64_t Bc, 
     float* const sv[4] = {b.saved[0] + s0 * 512 * Ts * 48, b.saved[1] + s0 * 128 * Ts * 96,
                           b.saved[2] + s0 * 32 * Ts * 192, b.saved[3] + s0 * 8 * Ts * 384};
     {
-        // level 0: 8 -> 32 rows, GN+GELU, resize to Tspec rows, + 0.1 * resize(saved[3][:, :192])
+        // level 0: 8 -> 32 rows, GN+GELU (in place, fp32: every source row feeds ~Ts/32 output rows), resize to
+        // Tspec rows, + 0.1 * resize(saved[3][:, :192])
         double* st = r.stats(NI);
-        conv_t(r, c->fdec[0], b.x_cond, NI, 8, (int)Ts, b.G, st, -1);
+        conv_t(r, c->fdec[0], b.x_cond, ab, NI, 8, (int)Ts, b.G, 0, st, -1);
+        gn_gelu_launch(b.G, NI, 32 * Ts * 192, 192, st, c->fdec[0].gnw, c->fdec[0].gnb, r.s);
         MergeDesc m;
-        m.src = b.G; m.H_src = 32; m.kept = 0; m.C = 192; m.stats = st; m.gn_count = 32 * Ts * 192;
-        m.gn_w = c->fdec[0].gnw; m.gn_b = c->fdec[0].gnb;
+        m.src = b.G; m.H_src = 32; m.kept = 0; m.C = 192;
         m.skip = sv[3]; m.H_skip = 8; m.C_skip = 384; m.P = P;
-        m.out = b.D; m.H_out = (int)Ts; m.W = (int)Ts; m.NI = NI;
+        m.out = b.D; m.out_bf16 = ab; m.H_out = (int)Ts; m.W = (int)Ts; m.NI = NI;
         dec_merge_launch(m, r.s);
         // levels 1..3: Tspec -> 4 Tspec rows; the /4 bilinear resize reads only rows 4d+1, 4d+2
         const int skH[3] = {32, 128, 512};
@@ -424,16 +440,16 @@ void decode_chunk(Run& r, const Dims& d, const Bufs& b, int64_t s0, int64_t Bc, 
             const DecW& w = c->fdec[i];
             const bool last = i == 3;
             double* sti = last ? nullptr : r.stats(NI);
-            conv_t(r, w, b.D, NI, (int)Ts, (int)Ts, b.G, sti, last ? 2 : 1);
+            conv_t(r, w, b.D, ab, NI, (int)Ts, (int)Ts, b.G, ab, sti, last ? 2 : 1);
             MergeDesc mm;
-            mm.src = b.G; mm.H_src = 4 * (int)Ts; mm.kept = 1; mm.C = w.cout;
+            mm.src = b.G; mm.src_bf16 = ab; mm.H_src = 4 * (int)Ts; mm.kept = 1; mm.C = w.cout;
             mm.stats = sti; mm.gn_count = 4 * Ts * Ts * w.cout; mm.gn_w = w.gnw; mm.gn_b = w.gnb;
             mm.skip = sv[3 - i]; mm.H_skip = skH[i - 1]; mm.C_skip = skC[i - 1]; mm.P = P;
             mm.H_out = (int)Ts; mm.W = (int)Ts; mm.NI = NI;
             if (last) {
                 mm.out = b.FO; mm.proj_w = c->fout_w; mm.proj_b = c->fout_b;     // freq_out 1x1 (4 -> 2)
             } else {
-                mm.out = b.D;
+                mm.out = b.D; mm.out_bf16 = ab;
             }
             dec_merge_launch(mm, r.s);
         }
@@ -451,13 +467,13 @@ void decode_chunk(Run& r, const Dims& d, const Bufs& b, int64_t s0, int64_t Bc, 
             const DecW& w = c->tdec[i];
             const bool last = i == 3;
             double* st = last ? nullptr : r.stats(NI);
-            conv_t(r, w, A, NI, (int)Lin, 1, b.G, st, -1);
+            conv_t(r, w, A, ab, NI, (int)Lin, 1, b.G, ab, st, -1);
             const int64_t target = d.L[3 - i];       // lengths_t reversed
             MergeDesc m;
-            m.src = b.G; m.H_src = (int)(4 * Lin); m.kept = 0; m.C = w.cout;
+            m.src = b.G; m.src_bf16 = ab; m.H_src = (int)(4 * Lin); m.kept = 0; m.C = w.cout;
             m.stats = st; m.gn_count = 4 * Lin * w.cout; m.gn_w = w.gnw; m.gn_b = w.gnb;
             m.skip = svt[3 - i]; m.H_skip = (int)d.L[4 - i]; m.C_skip = ENC_CH[3 - i]; m.P = P;
-            m.out = b.D; m.H_out = (int)target; m.W = 1; m.NI = NI;
+            m.out = b.D; m.out_bf16 = last ? 0 : ab; m.H_out = (int)target; m.W = 1; m.NI = NI;
             dec_merge_launch(m, r.s);
             A = b.D;
             Lin = target;

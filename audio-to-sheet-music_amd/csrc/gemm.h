@@ -38,12 +38,19 @@ struct GemmDesc {
     int col_off = 0;
     int64_t c_bs = -1;        // elements between output batches (-1: H_out_total*W*ldo)
     int store = 1;            // 0: compute statistics only
+    int col_split = 0;        // >0: columns >= col_split go to output row + hi_row_off, column n - col_split
+    int hi_row_off = 1;       //     (two ConvTranspose residue classes computed by one GEMM)
+    int store_mask = 3;       //     bit0: store columns < col_split, bit1: store columns >= col_split
     // epilogue
     int act = ACT_NONE;       // ACT_GLU: packed pairs [a(16) | gate(16)] per 32 columns, output N/2 channels
     const float* res = nullptr;       // residual (same layout as C, f32); out = res + rs[n]*v
     const float* res_scale = nullptr;
     const float* row_add = nullptr;   // out += row_add[ho][n]   (freq embedding after encoder level 0)
     double* stats = nullptr;          // per-batch {sum, sumsq} of the final output value
+    const double* gn_stats = nullptr; // GroupNorm(1) applied to v (after bias, before act) with per-batch
+    int64_t gn_count = 0;             //   statistics {sum, sumsq} over gn_count elements and per-column
+    const float* gn_w = nullptr;      //   affine (packed in the same column order as the weights)
+    const float* gn_b = nullptr;
 };
 
 // mode: 0 = exact fp32 (v_mfma_f32_16x16x4_f32), 1 = bf16 (v_mfma_f32_16x16x32_bf16, fp32 accumulate)

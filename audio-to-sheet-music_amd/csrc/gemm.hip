@@ -10,6 +10,7 @@
 // tile t and written to the other LDS buffer after them; one barrier per k-step.
 #include "common.h"
 #include "gemm.h"
+#include "gemm_epi.h"
 
 namespace athd {
 
@@ -33,8 +34,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmDesc d) {
     constexpr int AROWS = BM / 64;                 // A rows loaded per thread (8 k each)
     constexpr int BGROUPS = (BN * 4 + 255) / 256;  // B groups per thread
     __shared__ __attribute__((aligned(16))) T lds[2][(BM + BN) * LD];
-    constexpr int MAXG = 32;                       // GroupNorm groups tracked per block in LDS
-    __shared__ double st_lds[2 * MAXG];
+    __shared__ double st_lds[2 * EPI_MAXG];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -193,7 +193,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmDesc d) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-    if (d.stats && threadIdx.x < 2 * MAXG) st_lds[threadIdx.x] = 0.0;
+    if (d.stats && threadIdx.x < 2 * EPI_MAXG) st_lds[threadIdx.x] = 0.0;
     load_tile(0);
     store_tile(0);
     __syncthreads();
@@ -244,90 +244,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmDesc d) {
         __syncthreads();
     }
 
-    // ---------------- epilogue ----------------
-    const int64_t HW = (int64_t)d.H_out * d.W;
-    const int64_t c_bs = d.c_bs >= 0 ? d.c_bs : (int64_t)d.H_out_total * d.W * d.ldo;
-    const int Nout = (d.act == ACT_GLU) ? d.N / 2 : d.N;
-    const bool want_stats = d.stats != nullptr;
-    const int64_t g0 = m0 / HW;                 // first GroupNorm group (batch index) touched by this block
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int64_t m = m0 + wm0 + 16 * i + 4 * (lane >> 4) + r;
-            float p1 = 0.f, p2 = 0.f;                 // this lane's part of the row sums (stats)
-            if (m < M) {
-            const int w = (int)(m % d.W);
-            const int64_t t = m / d.W;
-            const int ho = (int)(t % d.H_out);
-            const int64_t b = t / d.H_out;
-            const int64_t obase = b * c_bs + ((int64_t)(ho * d.o_stride + d.o_off) * d.W + w) * d.ldo + d.col_off;
-            if (d.act == ACT_GLU) {
-#pragma unroll
-                for (int j = 0; j + 1 < TN; j += 2) {
-                    const int na = n0 + wn0 + 16 * j + fr;
-                    const int ng = na + 16;
-                    const int oc = (n0 + wn0 + 16 * j) / 2 + fr;
-                    if (oc >= Nout) continue;
-                    float a = acc[i][j][r], g = acc[i][j + 1][r];
-                    if (d.bias) { a += d.bias[na]; g += d.bias[ng]; }
-                    float v = a * sigmoidf_(g);
-                    if (d.row_add) v += d.row_add[(int64_t)ho * Nout + oc];
-                    if (d.res) v = d.res[obase + oc] + (d.res_scale ? d.res_scale[oc] : 1.f) * v;
-                    if (d.store) {
-                        if (d.c_bf16) ((bf16_t*)d.C)[obase + oc] = f2bf(v);
-                        else ((float*)d.C)[obase + oc] = v;
-                    }
-                }
-            } else {
-#pragma unroll
-                for (int j = 0; j < TN; ++j) {
-                    const int n = n0 + wn0 + 16 * j + fr;
-                    if (n >= d.N) continue;
-                    float v = acc[i][j][r];
-                    if (d.bias) v += d.bias[n];
-                    if (d.act == ACT_GELU) v = gelu_erf(v);
-                    if (d.row_add) v += d.row_add[(int64_t)ho * Nout + n];
-                    if (d.res) v = d.res[obase + n] + (d.res_scale ? d.res_scale[n] : 1.f) * v;
-                    p1 += v;                  // statistics of the final value (GroupNorm input)
-                    p2 += v * v;
-                    if (d.store) {
-                        if (d.c_bf16) ((bf16_t*)d.C)[obase + n] = f2bf(v);
-                        else ((float*)d.C)[obase + n] = v;
-                    }
-                }
-            }
-            }  // m < M
-            if (want_stats) {
-                // the 16 lanes sharing (lane >> 4) hold the same row: reduce across them, one LDS add per row
-#pragma unroll
-                for (int o = 1; o < 16; o <<= 1) {
-                    p1 += __shfl_xor(p1, o, 64);
-                    p2 += __shfl_xor(p2, o, 64);
-                }
-                if (fr == 0 && m < M) {
-                    const int64_t gi = m / HW - g0;
-                    if (gi < MAXG) {
-                        atomicAdd(&st_lds[2 * gi], (double)p1);
-                        atomicAdd(&st_lds[2 * gi + 1], (double)p2);
-                    } else {
-                        atomicAdd(&d.stats[2 * (g0 + gi)], (double)p1);
-                        atomicAdd(&d.stats[2 * (g0 + gi) + 1], (double)p2);
-                    }
-                }
-            }
-        }
-    }
-    if (want_stats) {
-        __syncthreads();
-        if (threadIdx.x < MAXG) {
-            const double a = st_lds[2 * threadIdx.x], q = st_lds[2 * threadIdx.x + 1];
-            if (a != 0.0 || q != 0.0) {
-                atomicAdd(&d.stats[2 * (g0 + threadIdx.x)], a);
-                atomicAdd(&d.stats[2 * (g0 + threadIdx.x) + 1], q);
-            }
-        }
-    }
+    gemm_epilogue<TM, TN, F_ALL>(d, acc, m0, n0, wm0, wn0, lane, st_lds, BM);
 }
 
 template <int MODE, int BM, int BN, int WM, int WN>
@@ -347,9 +264,13 @@ static void launch_mode(const GemmDesc& d, hipStream_t s) {
     else launch_cfg<MODE, 128, 128, 2, 2>(d, s);
 }
 
+bool gemm2_supported(const GemmDesc& d);
+int gemm2_launch(const GemmDesc& d, hipStream_t s);
+
 int gemm_launch(const GemmDesc& d, int mode, hipStream_t s) {
     if (d.Kp % BK != 0 || d.Kp < d.K || d.C_in <= 0 || d.N <= 0) return -2;
     if (d.act == ACT_GLU && (d.N % 32 != 0)) return -2;
+    if (mode == 1 && gemm2_supported(d)) return gemm2_launch(d, s);
     if (mode == 1) launch_mode<1>(d, s);
     else launch_mode<0>(d, s);
     return (int)hipGetLastError();

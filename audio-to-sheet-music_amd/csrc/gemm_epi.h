@@ -1,0 +1,183 @@
+// Shared GEMM epilogue (both MFMA GEMM kernels).  Accumulator layout of v_mfma_f32_16x16x{32,4}:
+// lane l holds rows 4(l>>4)+r (r = 0..3), column l&15 of each 16x16 tile.
+//   v = acc + bias[n]; [GroupNorm(v) with per-batch stats]; act (GELU | GLU over packed column pairs);
+//   + row_add[ho][n]; out = res + res_scale[n] * v; {sum, sumsq} of out per batch -> stats; store f32/bf16.
+// The feature set is a compile-time bitmask F so that each instantiation only carries the code it runs (a fully
+// general epilogue unrolled over 16 rows x 4 column tiles is ~25k instructions and thrashes the I-cache).
+#pragma once
+#include "common.h"
+#include "gemm.h"
+
+namespace athd {
+
+constexpr int EPI_MAXG = 32;   // GroupNorm groups tracked per block in LDS
+
+enum EpiFlag : unsigned {
+    F_GELU = 1u, F_GLU = 2u, F_RES = 4u, F_STATS = 8u, F_GN = 16u, F_ROWADD = 32u, F_SPLIT = 64u, F_CBF16 = 128u,
+    F_NOSTORE = 256u, F_ALL = 0xFFFFu
+};
+
+inline unsigned epi_flags(const GemmDesc& d) {
+    unsigned f = 0;
+    if (d.act == ACT_GELU) f |= F_GELU;
+    if (d.act == ACT_GLU) f |= F_GLU;
+    if (d.res) f |= F_RES;
+    if (d.stats) f |= F_STATS;
+    if (d.gn_stats) f |= F_GN;
+    if (d.row_add) f |= F_ROWADD;
+    if (d.col_split) f |= F_SPLIT;
+    if (d.c_bf16) f |= F_CBF16;
+    if (!d.store) f |= F_NOSTORE;
+    return f;
+}
+
+// The combinations the forward uses; anything else runs the general (F_ALL) instantiation.
+#define ATHD_EPI_LIST(X)                                                                                         \
+    X(0u) X(F_CBF16) X(F_GELU) X(F_GELU | F_CBF16) X(F_RES) X(F_RES | F_STATS) X(F_GLU) X(F_GLU | F_ROWADD)    \
+    X(F_STATS | F_NOSTORE) X(F_GN | F_GLU | F_RES) X(F_STATS) X(F_SPLIT | F_STATS) X(F_SPLIT)                  \
+    X(F_SPLIT | F_STATS | F_CBF16) X(F_SPLIT | F_CBF16)
+
+template <unsigned F>
+ATHD_DEV bool on(unsigned flag) { return (F & flag) != 0; }
+
+template <int TM, int TN, unsigned F>
+ATHD_DEV void gemm_epilogue(const GemmDesc& d, const f32x4_t (&acc)[TM][TN], int64_t m0, int n0, int wm0, int wn0,
+                            int lane, double* st_lds, int BM) {
+    constexpr bool GEN = F == F_ALL;
+    const bool f_gelu = GEN ? d.act == ACT_GELU : on<F>(F_GELU);
+    const bool f_glu = GEN ? d.act == ACT_GLU : on<F>(F_GLU);
+    const bool f_res = GEN ? d.res != nullptr : on<F>(F_RES);
+    const bool f_stats = GEN ? d.stats != nullptr : on<F>(F_STATS);
+    const bool f_gn = GEN ? d.gn_stats != nullptr : on<F>(F_GN);
+    const bool f_row = GEN ? d.row_add != nullptr : on<F>(F_ROWADD);
+    const bool f_split = GEN ? d.col_split != 0 : on<F>(F_SPLIT);
+    const bool f_cbf = GEN ? d.c_bf16 != 0 : on<F>(F_CBF16);
+    const bool f_store = GEN ? d.store != 0 : !on<F>(F_NOSTORE);
+
+    const int fr = lane & 15;
+    const uint32_t M = (uint32_t)d.nb * d.H_out * d.W;       // < 2^31 on every use
+    const uint32_t HW = (uint32_t)d.H_out * d.W;
+    const int64_t c_bs = d.c_bs >= 0 ? d.c_bs : (int64_t)d.H_out_total * d.W * d.ldo;
+    const int Nout = f_glu ? d.N / 2 : d.N;
+    const uint32_t g0 = (uint32_t)(m0 / HW);                  // first GroupNorm group touched by this block
+    // fast path: every row of this block in one group -> accumulate over the whole tile, one reduction at the end
+    uint32_t mlast = (uint32_t)m0 + (uint32_t)BM - 1;
+    if (mlast >= M) mlast = M - 1;
+    const bool one_group = (mlast / HW) == g0;
+    float q1 = 0.f, q2 = 0.f;
+    const float* bias = d.bias;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const uint32_t m = (uint32_t)m0 + wm0 + 16 * i + 4 * (lane >> 4) + r;
+            float p1 = 0.f, p2 = 0.f;                 // this lane's part of the row sums (stats)
+            if (m < M) {
+                const uint32_t w = m % (uint32_t)d.W;
+                const uint32_t t = m / (uint32_t)d.W;
+                const uint32_t ho = t % (uint32_t)d.H_out;
+                const uint32_t b = t / (uint32_t)d.H_out;
+                const int64_t obase = (int64_t)b * c_bs + ((int64_t)(ho * d.o_stride + d.o_off) * d.W + w) * d.ldo + d.col_off;
+                float gm = 0.f, gr = 1.f;
+                if (f_gn) {
+                    const double mm = d.gn_stats[2 * b] / (double)d.gn_count;
+                    double var = d.gn_stats[2 * b + 1] / (double)d.gn_count - mm * mm;
+                    if (var < 0) var = 0;
+                    gm = (float)mm;
+                    gr = (float)(1.0 / sqrt(var + 1e-5));
+                }
+                if (f_glu) {
+#pragma unroll
+                    for (int j = 0; j + 1 < TN; j += 2) {
+                        const int na = n0 + wn0 + 16 * j + fr;
+                        const int ng = na + 16;
+                        const int oc = (n0 + wn0 + 16 * j) / 2 + fr;
+                        if (oc >= Nout) continue;
+                        float a = acc[i][j][r], g = acc[i][j + 1][r];
+                        if (bias) { a += bias[na]; g += bias[ng]; }
+                        if (f_gn) {
+                            a = (a - gm) * gr * d.gn_w[na] + d.gn_b[na];
+                            g = (g - gm) * gr * d.gn_w[ng] + d.gn_b[ng];
+                        }
+                        float v = a * sigmoidf_(g);
+                        if (f_row) v += d.row_add[(int64_t)ho * Nout + oc];
+                        if (f_res) v = d.res[obase + oc] + (d.res_scale ? d.res_scale[oc] : 1.f) * v;
+                        if (f_store) {
+                            if (f_cbf) ((bf16_t*)d.C)[obase + oc] = f2bf(v);
+                            else ((float*)d.C)[obase + oc] = v;
+                        }
+                    }
+                } else {
+#pragma unroll
+                    for (int j = 0; j < TN; ++j) {
+                        const int n = n0 + wn0 + 16 * j + fr;
+                        if (n >= d.N) continue;
+                        float v = acc[i][j][r];
+                        if (bias) v += bias[n];
+                        if (f_gn) v = (v - gm) * gr * d.gn_w[n] + d.gn_b[n];
+                        if (f_gelu) v = gelu_erf(v);
+                        if (f_row) v += d.row_add[(int64_t)ho * Nout + n];
+                        if (f_res) v = d.res[obase + n] + (d.res_scale ? d.res_scale[n] : 1.f) * v;
+                        if (f_stats) {            // statistics of the final value (GroupNorm input)
+                            p1 += v;
+                            p2 += v * v;
+                        }
+                        if (f_store) {
+                            int64_t o = obase + n;
+                            bool st = true;
+                            if (f_split) {
+                                const bool hi = n >= d.col_split;
+                                st = (d.store_mask >> (hi ? 1 : 0)) & 1;
+                                if (hi) o += (int64_t)d.hi_row_off * d.W * d.ldo - d.col_split;
+                            }
+                            if (st) {
+                                if (f_cbf) ((bf16_t*)d.C)[o] = f2bf(v);
+                                else ((float*)d.C)[o] = v;
+                            }
+                        }
+                    }
+                }
+            }  // m < M
+            if (f_stats && one_group) {
+                q1 += p1;
+                q2 += p2;
+            } else if (f_stats) {
+                // the 16 lanes sharing (lane >> 4) hold the same row: reduce across them, one LDS add per row
+#pragma unroll
+                for (int o = 1; o < 16; o <<= 1) {
+                    p1 += __shfl_xor(p1, o, 64);
+                    p2 += __shfl_xor(p2, o, 64);
+                }
+                if (fr == 0 && m < M) {
+                    const uint32_t gi = m / HW - g0;
+                    if (gi < (uint32_t)EPI_MAXG) {
+                        atomicAdd(&st_lds[2 * gi], (double)p1);
+                        atomicAdd(&st_lds[2 * gi + 1], (double)p2);
+                    } else {
+                        atomicAdd(&d.stats[2 * (g0 + gi)], (double)p1);
+                        atomicAdd(&d.stats[2 * (g0 + gi) + 1], (double)p2);
+                    }
+                }
+            }
+        }
+    }
+    if (f_stats && one_group) {
+        const double t1 = wave_sum_d((double)q1), t2 = wave_sum_d((double)q2);
+        if (lane == 0) {
+            atomicAdd(&st_lds[0], t1);
+            atomicAdd(&st_lds[1], t2);
+        }
+    }
+    if (f_stats) {
+        __syncthreads();
+        if (threadIdx.x < EPI_MAXG) {
+            const double a = st_lds[2 * threadIdx.x], q = st_lds[2 * threadIdx.x + 1];
+            if (a != 0.0 || q != 0.0) {
+                atomicAdd(&d.stats[2 * (g0 + threadIdx.x)], a);
+                atomicAdd(&d.stats[2 * (g0 + threadIdx.x) + 1], q);
+            }
+        }
+    }
+}
+
+}  // namespace athd

@@ -67,8 +67,9 @@ __global__ __launch_bounds__(256) void gn_gelu_kernel(float* __restrict__ h, int
     float mean, rstd;
     gn_params(st, b, per_batch, mean, rstd);
     float* p = h + b * per_batch;
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < per_batch; i += (int64_t)gridDim.x * 256) {
-        const int c = (int)(i % H);
+    const int n = (int)per_batch;      // < 2^31 per batch on every use
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+        const int c = i % H;
         p[i] = gelu_erf((p[i] - mean) * rstd * w[c] + bb[c]);
     }
 }
@@ -80,32 +81,6 @@ void gn_gelu_launch(float* h, int nb, int64_t per_batch, int H, const double* st
     hipLaunchKernelGGL(gn_gelu_kernel, dim3(blocks, nb), dim3(256), 0, s, h, per_batch, H, stats, w, b);
 }
 
-__global__ __launch_bounds__(256) void dconv_out_kernel(float* __restrict__ x, const float* __restrict__ y, int64_t L,
-                                                        int C, const double* __restrict__ st,
-                                                        const float* __restrict__ w, const float* __restrict__ bb,
-                                                        const float* __restrict__ sc) {
-    const int64_t b = blockIdx.y;
-    float mean, rstd;
-    gn_params(st, b, L * 2 * C, mean, rstd);
-    const int64_t n = L * C;
-    float* xp = x + b * n;
-    const float* yp = y + b * n * 2;
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-        const int c = (int)(i % C);
-        const int64_t l = i / C;
-        const float a = (yp[l * 2 * C + c] - mean) * rstd * w[c] + bb[c];
-        const float g = (yp[l * 2 * C + C + c] - mean) * rstd * w[C + c] + bb[C + c];
-        xp[i] = xp[i] + sc[c] * (a * sigmoidf_(g));
-    }
-}
-
-void dconv_out_launch(float* x, const float* y, int nb, int64_t L, int C, const double* stats, const float* w,
-                      const float* b, const float* scale, hipStream_t s) {
-    int blocks = (int)((L * C + 255) / 256);
-    if (blocks > 1024) blocks = 1024;
-    hipLaunchKernelGGL(dconv_out_kernel, dim3(blocks, nb), dim3(256), 0, s, x, y, L, C, stats, w, b, scale);
-}
-
 __global__ __launch_bounds__(256) void gn_apply_kernel(float* __restrict__ x, int64_t per_batch, int C,
                                                        const double* __restrict__ st, const float* __restrict__ w,
                                                        const float* __restrict__ bb) {
@@ -113,8 +88,9 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(float* __restrict__ x, in
     float mean, rstd;
     gn_params(st, b, per_batch, mean, rstd);
     float* p = x + b * per_batch;
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < per_batch; i += (int64_t)gridDim.x * 256) {
-        const int c = (int)(i % C);
+    const int n = (int)per_batch;
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+        const int c = i % C;
         p[i] = (p[i] - mean) * rstd * w[c] + bb[c];
     }
 }
@@ -181,11 +157,11 @@ __global__ __launch_bounds__(256) void add_rowvec_kernel(const float* __restrict
                                                          int P, int64_t ntok, int C, float* __restrict__ U) {
     const int64_t item = blockIdx.y;
     const int64_t b = item / P;
-    const int64_t n = ntok * C;
+    const int n = (int)(ntok * C);
     const float* xp = X + b * n;
     float* up = U + item * n;
     const float* ap = a + item * C;
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256)
         up[i] = xp[i] + ap[i % C];
 }
 
@@ -233,50 +209,104 @@ void text_vec_launch(const float* text, int NI, int P, int text_per_item, const 
 }
 
 // --------------------------------------------------------------------------------------------- decoder merge
-ATHD_DEV float merge_src(const MergeDesc& d, int64_t item, int i, int w, int c, float mean, float rstd) {
+// out[item][ho][w][c] = resize_H(act(GN(src)))[ho][w][c] + 0.1 * resize_H(skip[item/P])[ho][w][c]   (FreqDecoder /
+// TimeDecoder body, ATHTDemucs_v2.py:90-103 / :127-138).  Each thread produces V consecutive channels of one
+// position (V = 8: one 16-B bf16 / two 16-B fp32 accesses per row touched).  Per-item counts are < 2^31.
+template <int V>
+ATHD_DEV void ldv(const void* p, int bf, int64_t i, float* v) {
+    if constexpr (V == 8) {
+        if (bf) {
+            const uint4 q = *reinterpret_cast<const uint4*>((const bf16_t*)p + i);
+            const bf16_t* h = reinterpret_cast<const bf16_t*>(&q);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = bf2f(h[j]);
+        } else {
+            const float4 a = *reinterpret_cast<const float4*>((const float*)p + i);
+            const float4 b = *reinterpret_cast<const float4*>((const float*)p + i + 4);
+            v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+        }
+    } else {   // V == 4
+        if (bf) {
+            const uint2 q = *reinterpret_cast<const uint2*>((const bf16_t*)p + i);
+            const bf16_t* h = reinterpret_cast<const bf16_t*>(&q);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[j] = bf2f(h[j]);
+        } else {
+            const float4 a = *reinterpret_cast<const float4*>((const float*)p + i);
+            v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+        }
+    }
+}
+
+template <int V>
+ATHD_DEV void merge_src_v(const MergeDesc& d, int64_t item, int i, int w, int c, float mean, float rstd, float* x) {
     int slot = i;
     int rows = d.H_src;
     if (d.kept) {
         slot = 2 * (i >> 2) + ((i & 3) == 2 ? 1 : 0);
         rows = 2 * (d.H_src >> 2);
     }
-    float x = d.src[((item * rows + slot) * (int64_t)d.W + w) * d.C + c];
-    if (d.stats) x = gelu_erf((x - mean) * rstd * d.gn_w[c] + d.gn_b[c]);
-    return x;
+    ldv<V>(d.src, d.src_bf16, item * (int64_t)rows * d.W * d.C + ((int64_t)slot * d.W + w) * d.C + c, x);
+    if (d.stats) {
+#pragma unroll
+        for (int j = 0; j < V; ++j) x[j] = gelu_erf((x[j] - mean) * rstd * d.gn_w[c + j] + d.gn_b[c + j]);
+    }
 }
 
-ATHD_DEV float merge_one(const MergeDesc& d, int64_t item, int ho, int w, int c, float mean, float rstd) {
-    float val;
+template <int V>
+ATHD_DEV void merge_v(const MergeDesc& d, int64_t item, int ho, int w, int c, float mean, float rstd, float* out) {
+    float a[V], b[V];
     if (d.H_src == d.H_out) {
-        val = merge_src(d, item, ho, w, c, mean, rstd);
+        merge_src_v<V>(d, item, ho, w, c, mean, rstd, out);
     } else {
         const LinIdx li = lin_index(ho, d.H_src, d.H_out);
-        val = li.l0 * merge_src(d, item, li.i0, w, c, mean, rstd) + li.l1 * merge_src(d, item, li.i1, w, c, mean, rstd);
+        merge_src_v<V>(d, item, li.i0, w, c, mean, rstd, a);
+        merge_src_v<V>(d, item, li.i1, w, c, mean, rstd, b);
+#pragma unroll
+        for (int j = 0; j < V; ++j) out[j] = li.l0 * a[j] + li.l1 * b[j];
     }
     const int64_t sb = item / d.P;
     const float* sk = d.skip + sb * (int64_t)d.H_skip * d.W * d.C_skip;
-    float sv;
     if (d.H_skip == d.H_out) {
-        sv = sk[((int64_t)ho * d.W + w) * d.C_skip + c];
+        ldv<V>(sk, 0, (int64_t)(ho * d.W + w) * d.C_skip + c, a);
+#pragma unroll
+        for (int j = 0; j < V; ++j) out[j] = out[j] + a[j] * 0.1f;
     } else {
         const LinIdx lj = lin_index(ho, d.H_skip, d.H_out);
-        sv = lj.l0 * sk[((int64_t)lj.i0 * d.W + w) * d.C_skip + c] + lj.l1 * sk[((int64_t)lj.i1 * d.W + w) * d.C_skip + c];
+        ldv<V>(sk, 0, (int64_t)(lj.i0 * d.W + w) * d.C_skip + c, a);
+        ldv<V>(sk, 0, (int64_t)(lj.i1 * d.W + w) * d.C_skip + c, b);
+#pragma unroll
+        for (int j = 0; j < V; ++j) out[j] = out[j] + (lj.l0 * a[j] + lj.l1 * b[j]) * 0.1f;
     }
-    return val + sv * 0.1f;
 }
 
+template <int V>
 __global__ __launch_bounds__(256) void dec_merge_kernel(const MergeDesc d) {
     const int64_t item = blockIdx.y;
     float mean = 0.f, rstd = 1.f;
     if (d.stats) gn_params(d.stats, item, d.gn_count, mean, rstd);
-    const int64_t n = (int64_t)d.H_out * d.W * d.C;
-    float* op = d.out + item * n;
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-        const int c = (int)(i % d.C);
-        const int64_t pw = i / d.C;
-        const int w = (int)(pw % d.W);
-        const int ho = (int)(pw / d.W);
-        op[i] = merge_one(d, item, ho, w, c, mean, rstd);
+    const int cv = d.C / V;
+    const int n = d.H_out * d.W * cv;
+    const int64_t obase = item * (int64_t)d.H_out * d.W * d.C;
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+        const int c = (i % cv) * V;
+        const int pw = i / cv;
+        const int w = pw % d.W;
+        const int ho = pw / d.W;
+        float v[V];
+        merge_v<V>(d, item, ho, w, c, mean, rstd, v);
+        const int64_t o = obase + (int64_t)pw * d.C + c;
+        if (d.out_bf16) {
+            bf16_t h[V];
+#pragma unroll
+            for (int j = 0; j < V; ++j) h[j] = f2bf(v[j]);
+            if constexpr (V == 8) *reinterpret_cast<uint4*>((bf16_t*)d.out + o) = *reinterpret_cast<uint4*>(h);
+            else *reinterpret_cast<uint2*>((bf16_t*)d.out + o) = *reinterpret_cast<uint2*>(h);
+        } else {
+#pragma unroll
+            for (int j = 0; j < V; j += 4)
+                *reinterpret_cast<float4*>((float*)d.out + o + j) = make_float4(v[j], v[j + 1], v[j + 2], v[j + 3]);
+        }
     }
 }
 
@@ -284,27 +314,28 @@ __global__ __launch_bounds__(256) void dec_merge_proj_kernel(const MergeDesc d) 
     const int64_t item = blockIdx.y;
     float mean = 0.f, rstd = 1.f;
     if (d.stats) gn_params(d.stats, item, d.gn_count, mean, rstd);
-    const int64_t n = (int64_t)d.H_out * d.W;
-    float* op = d.out + item * n * 2;
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-        const int w = (int)(i % d.W);
-        const int ho = (int)(i / d.W);
+    const int n = d.H_out * d.W;
+    float* op = (float*)d.out + item * (int64_t)n * 2;
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+        const int w = i % d.W;
+        const int ho = i / d.W;
         float m[4];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) m[c] = merge_one(d, item, ho, w, c, mean, rstd);
-#pragma unroll
-        for (int o = 0; o < 2; ++o)
-            op[i * 2 + o] = d.proj_b[o] + (d.proj_w[o * 4 + 0] * m[0] + d.proj_w[o * 4 + 1] * m[1] +
-                                           d.proj_w[o * 4 + 2] * m[2] + d.proj_w[o * 4 + 3] * m[3]);
+        merge_v<4>(d, item, ho, w, 0, mean, rstd, m);
+        float2 o;
+        o.x = d.proj_b[0] + (d.proj_w[0] * m[0] + d.proj_w[1] * m[1] + d.proj_w[2] * m[2] + d.proj_w[3] * m[3]);
+        o.y = d.proj_b[1] + (d.proj_w[4] * m[0] + d.proj_w[5] * m[1] + d.proj_w[6] * m[2] + d.proj_w[7] * m[3]);
+        *reinterpret_cast<float2*>(op + i * 2) = o;
     }
 }
 
 void dec_merge_launch(const MergeDesc& d, hipStream_t s) {
-    const int64_t n = (int64_t)d.H_out * d.W * (d.proj_w ? 1 : d.C);
+    const int V = (d.C % 8 == 0) ? 8 : 4;    // C is 192/96/48 (8) or 4
+    const int64_t n = (int64_t)d.H_out * d.W * (d.proj_w ? 1 : d.C / V);
     int blocks = (int)((n + 255) / 256);
-    if (blocks > 2048) blocks = 2048;
+    if (blocks > 4096) blocks = 4096;
     if (d.proj_w) hipLaunchKernelGGL(dec_merge_proj_kernel, dim3(blocks, d.NI), dim3(256), 0, s, d);
-    else hipLaunchKernelGGL(dec_merge_kernel, dim3(blocks, d.NI), dim3(256), 0, s, d);
+    else if (V == 8) hipLaunchKernelGGL(dec_merge_kernel<8>, dim3(blocks, d.NI), dim3(256), 0, s, d);
+    else hipLaunchKernelGGL(dec_merge_kernel<4>, dim3(blocks, d.NI), dim3(256), 0, s, d);
 }
 
 // --------------------------------------------------------------------------------------------- position tables

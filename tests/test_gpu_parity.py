@@ -97,16 +97,21 @@ def test_full_segment_6s(models, oracle_model, text_table, dt):
 
 
 def test_forward_prompts_matches_forward(models):
-    """Encode-once/decode-P path == P separate forwards (same kernels; GroupNorm statistics are summed with
-    fp64 atomics whose order varies, so equality is to fp32 rounding, not bitwise)."""
+    """Encode-once/decode-P path == P separate forwards.  f32 model: equal to fp32 rounding (GroupNorm statistics
+    are fp64 atomics whose order varies); bf16 model: the two paths agree to >= 40 dB (order-dependent statistics
+    can flip individual bf16 roundings of intermediates)."""
     from athd.synth import synthetic_batch
     wav = torch.as_tensor(synthetic_batch(3, 50000)).cuda()
-    m = models["bf16"]
     prompts = ["drums", "bass", "other", "vocals"]
-    multi = m.forward_prompts(wav, prompts)
-    for p, name in enumerate(prompts):
-        single = m(wav, name)
-        assert torch.allclose(multi[:, p], single, atol=1e-5, rtol=1e-4), name
+    for dt in ("f32", "bf16"):
+        m = models[dt]
+        multi = m.forward_prompts(wav, prompts)
+        for p, name in enumerate(prompts):
+            single = m(wav, name)
+            if dt == "f32":
+                assert torch.allclose(multi[:, p], single, atol=1e-5, rtol=1e-4), name
+            else:
+                assert sdr_db(single.cpu().numpy(), multi[:, p].cpu().numpy()) >= 40.0, name
 
 
 def test_batch_independence(models):

@@ -1,0 +1,33 @@
+// Kernel micro-benchmark entry points (test tooling, not part of libathd.so): plain-C launchers for the GEMM and
+// attention kernels on caller-provided device buffers, used by tools/kbench.py to time variants against
+// torch/hipBLASLt on identical shapes in one process.
+#include "../audio-to-sheet-music_amd/csrc/gemm.h"
+#include "../audio-to-sheet-music_amd/csrc/attn.h"
+#include <hip/hip_runtime.h>
+
+using namespace athd;
+namespace athd {
+int gemm2_launch(const GemmDesc& d, hipStream_t s);
+}
+
+extern "C" {
+// out[M][N] = act(A[M][K] @ W[N][Kp]^T + bias); variant 1 = v1 kernel, 2 = v2 kernel
+int kb_gemm(int variant, const void* A, int a_bf16, const void* W, const float* bias, void* C, int c_bf16, int M, int N,
+            int K, int Kp, int act, void* stream) {
+    GemmDesc d;
+    d.A = A; d.a_bf16 = a_bf16; d.nb = 1; d.H_in = M; d.W = 1; d.C_in = K; d.a_ld = K; d.H_out = M;
+    d.Wp = W; d.N = N; d.K = K; d.Kp = Kp; d.bias = bias; d.C = C; d.c_bf16 = c_bf16; d.H_out_total = M; d.ldo = N;
+    d.act = act;
+    if (variant == 2) return gemm2_launch(d, (hipStream_t)stream);
+    return gemm_launch(d, 1, (hipStream_t)stream);
+}
+int kb_attn(const void* qkv, int nb, int N, void* out, void* stream) {
+    AttnDesc a;
+    a.nb = nb; a.Nq = N; a.Nk = N; a.heads = 8; a.scale = 0.125f;
+    a.Q = qkv; a.q_bf16 = 1; a.q_bs = (int64_t)N * 1536; a.q_ld = 1536; a.q_off = 0;
+    a.K = qkv; a.k_bf16 = 1; a.k_bs = (int64_t)N * 1536; a.k_ld = 1536; a.k_off = 512;
+    a.V = qkv; a.v_bf16 = 1; a.v_bs = (int64_t)N * 1536; a.v_ld = 1536; a.v_off = 1024;
+    a.O = out; a.o_bf16 = 1; a.o_bs = (int64_t)N * 512; a.o_ld = 512;
+    return attn_launch(a, 1, (hipStream_t)stream);
+}
+}

@@ -1,0 +1,75 @@
+"""Time GEMM / attention kernel variants vs torch (hipBLASLt / SDPA) on the GPU box (tooling, not a test)."""
+import ctypes
+import os
+import sys
+
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+lib = ctypes.CDLL(os.path.join(HERE, "libkbench.so"))
+vp = ctypes.c_void_p
+
+
+def timeit(fn, iters=20):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters * 1e3   # us
+
+
+def gemm_case(M, N, K, act=0):
+    dev = "cuda"
+    A = (torch.randn(M, K, device=dev) * 0.5).to(torch.bfloat16)
+    Kp = (K + 63) // 64 * 64
+    W = torch.zeros(N, Kp, device=dev, dtype=torch.bfloat16)
+    W[:, :K] = (torch.randn(N, K, device=dev) * 0.05).to(torch.bfloat16)
+    bias = torch.randn(N, device=dev) * 0.1
+    C = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    st = torch.cuda.current_stream().cuda_stream
+    ref = (A.float() @ W[:, :K].float().t() + bias)
+    if act == 1:
+        ref = torch.nn.functional.gelu(ref)
+    flops = 2.0 * M * N * K
+    res = {}
+    for v in (1, 2):
+        f = lambda: lib.kb_gemm(v, vp(A.data_ptr()), 1, vp(W.data_ptr()), vp(bias.data_ptr()), vp(C.data_ptr()), 1,
+                                M, N, K, Kp, act, vp(st))
+        us = timeit(f)
+        err = (C.float() - ref).abs().max().item() / (ref.abs().max().item() + 1e-9)
+        res[f"v{v}"] = (us, flops / us / 1e6, err)
+    Wt = W[:, :K].t().contiguous()
+    us = timeit(lambda: torch.addmm(bias.to(torch.bfloat16), A, W[:, :K].t()))
+    res["torch"] = (us, flops / us / 1e6, 0.0)
+    print(f"GEMM M={M} N={N} K={K} act={act}: " + "  ".join(f"{k}: {v[0]:8.1f}us {v[1]:7.1f}TF err={v[2]:.1e}" for k, v in res.items()), flush=True)
+
+
+def attn_case(B, N):
+    qkv = (torch.randn(B, N, 1536, device="cuda")).to(torch.bfloat16)
+    out = torch.empty(B, N, 512, device="cuda", dtype=torch.bfloat16)
+    st = torch.cuda.current_stream().cuda_stream
+    us = timeit(lambda: lib.kb_attn(vp(qkv.data_ptr()), B, N, vp(out.data_ptr()), vp(st)))
+    flops = 4.0 * B * 8 * N * N * 64
+    q, k, v = qkv.view(B, N, 3, 8, 64).permute(2, 0, 3, 1, 4)
+    ref = torch.nn.functional.scaled_dot_product_attention(q, k, v)
+    err = (out.view(B, N, 8, 64).permute(0, 2, 1, 3).float() - ref.float()).abs().max().item()
+    ust = timeit(lambda: torch.nn.functional.scaled_dot_product_attention(q, k, v))
+    print(f"ATTN B={B} N={N}: athd {us:8.1f}us {flops / us / 1e6:7.1f}TF err={err:.1e} | torch sdpa {ust:8.1f}us {flops / ust / 1e6:7.1f}TF", flush=True)
+
+
+if __name__ == "__main__":
+    torch.manual_seed(0)
+    M = 64 * 2072
+    gemm_case(M, 1536, 512)
+    gemm_case(M, 2048, 512, act=1)
+    gemm_case(M, 512, 2048)
+    gemm_case(M, 512, 512)
+    gemm_case(64 * 259 * 259, 192, 384)
+    gemm_case(64 * 259 * 259, 96, 192)
+    attn_case(64, 2072)
+    attn_case(64, 1034)
