@@ -215,7 +215,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmDesc d) {
             for (int i = 0; i < TM; ++i)
 #pragma unroll
                 for (int j = 0; j < TN; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
         } else {
             float af[TM][8], bfr[TN][8];
 #pragma unroll
@@ -238,7 +238,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmDesc d) {
                 for (int i = 0; i < TM; ++i)
 #pragma unroll
                     for (int j = 0; j < TN; ++j)
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i][s], bfr[j][s], acc[i][j], 0, 0, 0);
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(bfr[j][s], af[i][s], acc[i][j], 0, 0, 0);
         }
         if (kt + 1 < nk) store_tile(st ^ 1);
         __syncthreads();

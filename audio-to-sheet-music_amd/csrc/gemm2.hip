@@ -158,7 +158,7 @@ __global__ __launch_bounds__(256) void gemm2_kernel(const GemmDesc d) {
             for (int i = 0; i < TM; ++i)
 #pragma unroll
                 for (int j = 0; j < TN; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
         }
         if (kt + 1 < nk) write_a(cur ^ 1);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

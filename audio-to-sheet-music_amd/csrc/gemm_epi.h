@@ -1,5 +1,6 @@
-// Shared GEMM epilogue (both MFMA GEMM kernels).  Accumulator layout of v_mfma_f32_16x16x{32,4}:
-// lane l holds rows 4(l>>4)+r (r = 0..3), column l&15 of each 16x16 tile.
+// Shared GEMM epilogue (both MFMA GEMM kernels).  The kernels compute C^T tiles (weights as the MFMA A operand),
+// so with the v_mfma_f32_16x16x{32,4} C/D map (col = l&15, row = 4(l>>4)+r) each lane owns one output row and
+// four consecutive output columns: vector bias/residual loads and 8-B (bf16) / 16-B (f32) stores.
 //   v = acc + bias[n]; [GroupNorm(v) with per-batch stats]; act (GELU | GLU over packed column pairs);
 //   + row_add[ho][n]; out = res + res_scale[n] * v; {sum, sumsq} of out per batch -> stats; store f32/bf16.
 // The feature set is a compile-time bitmask F so that each instantiation only carries the code it runs (a fully
@@ -43,6 +44,8 @@ ATHD_DEV bool on(unsigned flag) { return (F & flag) != 0; }
 template <int TM, int TN, unsigned F>
 ATHD_DEV void gemm_epilogue(const GemmDesc& d, const f32x4_t (&acc)[TM][TN], int64_t m0, int n0, int wm0, int wn0,
                             int lane, double* st_lds, int BM) {
+    // Transposed accumulators (the kernels issue mfma(W_frag, A_frag)): lane l holds, for tile (i, j), output row
+    // m = m0 + wm0 + 16 i + (l & 15) and the 4 consecutive columns n = n0 + wn0 + 16 j + 4 (l >> 4) + {0..3}.
     constexpr bool GEN = F == F_ALL;
     const bool f_gelu = GEN ? d.act == ACT_GELU : on<F>(F_GELU);
     const bool f_glu = GEN ? d.act == ACT_GLU : on<F>(F_GLU);
@@ -54,109 +57,148 @@ ATHD_DEV void gemm_epilogue(const GemmDesc& d, const f32x4_t (&acc)[TM][TN], int
     const bool f_cbf = GEN ? d.c_bf16 != 0 : on<F>(F_CBF16);
     const bool f_store = GEN ? d.store != 0 : !on<F>(F_NOSTORE);
 
-    const int fr = lane & 15;
+    const int fr = lane & 15, fg = lane >> 4;
     const uint32_t M = (uint32_t)d.nb * d.H_out * d.W;       // < 2^31 on every use
     const uint32_t HW = (uint32_t)d.H_out * d.W;
     const int64_t c_bs = d.c_bs >= 0 ? d.c_bs : (int64_t)d.H_out_total * d.W * d.ldo;
     const int Nout = f_glu ? d.N / 2 : d.N;
     const uint32_t g0 = (uint32_t)(m0 / HW);                  // first GroupNorm group touched by this block
-    // fast path: every row of this block in one group -> accumulate over the whole tile, one reduction at the end
     uint32_t mlast = (uint32_t)m0 + (uint32_t)BM - 1;
     if (mlast >= M) mlast = M - 1;
-    const bool one_group = (mlast / HW) == g0;
+    const bool one_group = (mlast / HW) == g0;                // fast path: the whole tile in one group
+    const int64_t hi_off = f_split ? (int64_t)d.hi_row_off * d.W * d.ldo - d.col_split : 0;
     float q1 = 0.f, q2 = 0.f;
-    const float* bias = d.bias;
+
+    // per-column constants (hoisted out of the row loop): columns n = nb_j + {0..3}
+    float4 bj[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        const int nb = n0 + wn0 + 16 * j + 4 * fg;
+        bj[j] = (d.bias && nb + 3 < d.N) ? *reinterpret_cast<const float4*>(d.bias + nb) : make_float4(0.f, 0.f, 0.f, 0.f);
+        if (d.bias && nb < d.N && nb + 3 >= d.N) {   // ragged N (N % 4 != 0 never occurs; keep it exact anyway)
+            float t[4] = {0.f, 0.f, 0.f, 0.f};
+            for (int q = 0; q < 4 && nb + q < d.N; ++q) t[q] = d.bias[nb + q];
+            bj[j] = make_float4(t[0], t[1], t[2], t[3]);
+        }
+    }
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
+        const uint32_t m = (uint32_t)m0 + wm0 + 16 * i + fr;
+        float p1 = 0.f, p2 = 0.f;
+        if (m < M) {
+            const uint32_t w = m % (uint32_t)d.W;
+            const uint32_t t = m / (uint32_t)d.W;
+            const uint32_t ho = t % (uint32_t)d.H_out;
+            const uint32_t b = t / (uint32_t)d.H_out;
+            const int64_t obase = (int64_t)b * c_bs + ((int64_t)(ho * d.o_stride + d.o_off) * d.W + w) * d.ldo + d.col_off;
+            float gm = 0.f, gr = 1.f;
+            if (f_gn) {
+                const double mm = d.gn_stats[2 * b] / (double)d.gn_count;
+                double var = d.gn_stats[2 * b + 1] / (double)d.gn_count - mm * mm;
+                if (var < 0) var = 0;
+                gm = (float)mm;
+                gr = (float)(1.0 / sqrt(var + 1e-5));
+            }
+            if (f_glu) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const uint32_t m = (uint32_t)m0 + wm0 + 16 * i + 4 * (lane >> 4) + r;
-            float p1 = 0.f, p2 = 0.f;                 // this lane's part of the row sums (stats)
-            if (m < M) {
-                const uint32_t w = m % (uint32_t)d.W;
-                const uint32_t t = m / (uint32_t)d.W;
-                const uint32_t ho = t % (uint32_t)d.H_out;
-                const uint32_t b = t / (uint32_t)d.H_out;
-                const int64_t obase = (int64_t)b * c_bs + ((int64_t)(ho * d.o_stride + d.o_off) * d.W + w) * d.ldo + d.col_off;
-                float gm = 0.f, gr = 1.f;
-                if (f_gn) {
-                    const double mm = d.gn_stats[2 * b] / (double)d.gn_count;
-                    double var = d.gn_stats[2 * b + 1] / (double)d.gn_count - mm * mm;
-                    if (var < 0) var = 0;
-                    gm = (float)mm;
-                    gr = (float)(1.0 / sqrt(var + 1e-5));
-                }
-                if (f_glu) {
+                for (int j = 0; j + 1 < TN; j += 2) {
+                    const int na = n0 + wn0 + 16 * j + 4 * fg;        // packed columns of the 'a' half
+                    const int oc = (n0 + wn0 + 16 * j) / 2 + 4 * fg;  // output channels oc..oc+3
+                    if (oc >= Nout) continue;
+                    const float bav[4] = {bj[j].x, bj[j].y, bj[j].z, bj[j].w};
+                    const float bgv[4] = {bj[j + 1].x, bj[j + 1].y, bj[j + 1].z, bj[j + 1].w};
+                    float o[4];
 #pragma unroll
-                    for (int j = 0; j + 1 < TN; j += 2) {
-                        const int na = n0 + wn0 + 16 * j + fr;
-                        const int ng = na + 16;
-                        const int oc = (n0 + wn0 + 16 * j) / 2 + fr;
-                        if (oc >= Nout) continue;
-                        float a = acc[i][j][r], g = acc[i][j + 1][r];
-                        if (bias) { a += bias[na]; g += bias[ng]; }
+                    for (int q = 0; q < 4; ++q) {
+                        float a = acc[i][j][q] + bav[q], g = acc[i][j + 1][q] + bgv[q];
                         if (f_gn) {
-                            a = (a - gm) * gr * d.gn_w[na] + d.gn_b[na];
-                            g = (g - gm) * gr * d.gn_w[ng] + d.gn_b[ng];
+                            a = (a - gm) * gr * d.gn_w[na + q] + d.gn_b[na + q];
+                            g = (g - gm) * gr * d.gn_w[na + 16 + q] + d.gn_b[na + 16 + q];
                         }
                         float v = a * sigmoidf_(g);
-                        if (f_row) v += d.row_add[(int64_t)ho * Nout + oc];
-                        if (f_res) v = d.res[obase + oc] + (d.res_scale ? d.res_scale[oc] : 1.f) * v;
-                        if (f_store) {
-                            if (f_cbf) ((bf16_t*)d.C)[obase + oc] = f2bf(v);
-                            else ((float*)d.C)[obase + oc] = v;
+                        if (f_row) v += d.row_add[(int64_t)ho * Nout + oc + q];
+                        o[q] = v;
+                    }
+                    if (f_res) {
+                        const float4 rv = *reinterpret_cast<const float4*>(d.res + obase + oc);
+                        const float rr[4] = {rv.x, rv.y, rv.z, rv.w};
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) o[q] = rr[q] + (d.res_scale ? d.res_scale[oc + q] : 1.f) * o[q];
+                    }
+                    if (f_store) {
+                        if (f_cbf) {
+                            bf16_t h[4] = {f2bf(o[0]), f2bf(o[1]), f2bf(o[2]), f2bf(o[3])};
+                            *reinterpret_cast<uint2*>((bf16_t*)d.C + obase + oc) = *reinterpret_cast<uint2*>(h);
+                        } else {
+                            *reinterpret_cast<float4*>((float*)d.C + obase + oc) = make_float4(o[0], o[1], o[2], o[3]);
                         }
                     }
-                } else {
+                }
+            } else {
 #pragma unroll
-                    for (int j = 0; j < TN; ++j) {
-                        const int n = n0 + wn0 + 16 * j + fr;
-                        if (n >= d.N) continue;
-                        float v = acc[i][j][r];
-                        if (bias) v += bias[n];
-                        if (f_gn) v = (v - gm) * gr * d.gn_w[n] + d.gn_b[n];
+                for (int j = 0; j < TN; ++j) {
+                    const int n = n0 + wn0 + 16 * j + 4 * fg;
+                    if (n >= d.N) continue;
+                    const float bv[4] = {bj[j].x, bj[j].y, bj[j].z, bj[j].w};
+                    float o[4];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        float v = acc[i][j][q] + bv[q];
+                        if (f_gn) v = (v - gm) * gr * d.gn_w[n + q] + d.gn_b[n + q];
                         if (f_gelu) v = gelu_erf(v);
-                        if (f_row) v += d.row_add[(int64_t)ho * Nout + n];
-                        if (f_res) v = d.res[obase + n] + (d.res_scale ? d.res_scale[n] : 1.f) * v;
-                        if (f_stats) {            // statistics of the final value (GroupNorm input)
-                            p1 += v;
-                            p2 += v * v;
-                        }
-                        if (f_store) {
-                            int64_t o = obase + n;
-                            bool st = true;
-                            if (f_split) {
-                                const bool hi = n >= d.col_split;
-                                st = (d.store_mask >> (hi ? 1 : 0)) & 1;
-                                if (hi) o += (int64_t)d.hi_row_off * d.W * d.ldo - d.col_split;
-                            }
-                            if (st) {
-                                if (f_cbf) ((bf16_t*)d.C)[o] = f2bf(v);
-                                else ((float*)d.C)[o] = v;
-                            }
-                        }
+                        if (f_row) v += d.row_add[(int64_t)ho * Nout + n + q];
+                        o[q] = v;
                     }
-                }
-            }  // m < M
-            if (f_stats && one_group) {
-                q1 += p1;
-                q2 += p2;
-            } else if (f_stats) {
-                // the 16 lanes sharing (lane >> 4) hold the same row: reduce across them, one LDS add per row
+                    if (f_res) {
+                        const float4 rv = *reinterpret_cast<const float4*>(d.res + obase + n);
+                        const float rr[4] = {rv.x, rv.y, rv.z, rv.w};
 #pragma unroll
-                for (int o = 1; o < 16; o <<= 1) {
-                    p1 += __shfl_xor(p1, o, 64);
-                    p2 += __shfl_xor(p2, o, 64);
-                }
-                if (fr == 0 && m < M) {
-                    const uint32_t gi = m / HW - g0;
-                    if (gi < (uint32_t)EPI_MAXG) {
-                        atomicAdd(&st_lds[2 * gi], (double)p1);
-                        atomicAdd(&st_lds[2 * gi + 1], (double)p2);
-                    } else {
-                        atomicAdd(&d.stats[2 * (g0 + gi)], (double)p1);
-                        atomicAdd(&d.stats[2 * (g0 + gi) + 1], (double)p2);
+                        for (int q = 0; q < 4; ++q) o[q] = rr[q] + (d.res_scale ? d.res_scale[n + q] : 1.f) * o[q];
                     }
+                    if (f_stats) {            // statistics of the final value (GroupNorm input)
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) {
+                            p1 += o[q];
+                            p2 += o[q] * o[q];
+                        }
+                    }
+                    if (f_store) {
+                        int64_t off = obase + n;
+                        bool st = true;
+                        if (f_split) {
+                            const bool hi = n >= d.col_split;       // col_split % 4 == 0: a 4-group never straddles
+                            st = (d.store_mask >> (hi ? 1 : 0)) & 1;
+                            if (hi) off += hi_off;
+                        }
+                        if (st) {
+                            if (f_cbf) {
+                                bf16_t h[4] = {f2bf(o[0]), f2bf(o[1]), f2bf(o[2]), f2bf(o[3])};
+                                *reinterpret_cast<uint2*>((bf16_t*)d.C + off) = *reinterpret_cast<uint2*>(h);
+                            } else {
+                                *reinterpret_cast<float4*>((float*)d.C + off) = make_float4(o[0], o[1], o[2], o[3]);
+                            }
+                        }
+                    }
+                }
+            }
+        }  // m < M
+        if (f_stats && one_group) {
+            q1 += p1;
+            q2 += p2;
+        } else if (f_stats) {
+            // the 4 lane groups (lane >> 4) hold the same row m: reduce across them, one LDS add per row
+            p1 += __shfl_xor(p1, 16, 64);
+            p2 += __shfl_xor(p2, 16, 64);
+            p1 += __shfl_xor(p1, 32, 64);
+            p2 += __shfl_xor(p2, 32, 64);
+            if (fg == 0 && m < M) {
+                const uint32_t gi = m / HW - g0;
+                if (gi < (uint32_t)EPI_MAXG) {
+                    atomicAdd(&st_lds[2 * gi], (double)p1);
+                    atomicAdd(&st_lds[2 * gi + 1], (double)p2);
+                } else {
+                    atomicAdd(&d.stats[2 * (g0 + gi)], (double)p1);
+                    atomicAdd(&d.stats[2 * (g0 + gi) + 1], (double)p2);
                 }
             }
         }
