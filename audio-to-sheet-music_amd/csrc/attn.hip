@@ -230,10 +230,190 @@ __global__ __launch_bounds__(256) void attn_kernel(const AttnDesc d) {
     }
 }
 
+// ----------------------------------------------------------------------------------------------------------------
+// bf16 path.  K and V tiles (64 keys x 64 d) are stored row-major [key][d] (144-B rows) in a 2-deep LDS ring with
+// 16-B writes; the next tile is prefetched into registers while the current one is computed (T14 split).  The
+// PV A-operand V^T[d][keys] is read with ds_read_b64_tr_b16: lane 4q+p of a 16-lane group addresses row k0+q,
+// columns d0+4p..+3 and receives column d0+(lane&15) of rows k0..k0+3, i.e. 4 consecutive keys of one d.
+typedef short v4i16 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
+
+__global__ __launch_bounds__(256) void attn_bf16_kernel(const AttnDesc d) {
+    constexpr int LDK = 72;                        // bf16 per LDS row (64 + 8 pad)
+    __shared__ __attribute__((aligned(16))) bf16_t Ks[2][64 * LDK];
+    __shared__ __attribute__((aligned(16))) bf16_t Vs[2][64 * LDK];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int g = lane >> 4, c16 = lane & 15;
+    const int h = blockIdx.y;
+    const int64_t b = blockIdx.z;
+    const int q0 = blockIdx.x * 128 + wave * 32;
+    const float sl2 = d.scale * 1.4426950408889634f;
+
+    bf16v8 qb[2][2];
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+        const int q = q0 + 16 * nt + c16;
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            float v[8];
+            if (q < d.Nq) load8(d.Q, d.q_bf16, b * d.q_bs + (int64_t)q * d.q_ld + d.q_off + h * 64 + 32 * c + 8 * g, v);
+            else {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) v[j] = 0.f;
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) qb[nt][c][j] = (__bf16)v[j];
+        }
+    }
+    // tile staging: thread -> keys tid/8 and tid/8 + 32, columns 8 (tid % 8) .. +7.  Keys past Nk re-read the
+    // last key (finite data; their scores are masked to -inf so P = 0), which keeps the prefetch branch-free.
+    const bf16_t* Kb = (const bf16_t*)d.K + b * d.k_bs + d.k_off + h * 64;
+    const bf16_t* Vb = (const bf16_t*)d.V + b * d.v_bs + d.v_off + h * 64;
+    const int skey = tid >> 3, sd0 = 8 * (tid & 7);          // rows skey and skey + 32
+    const int soff = skey * LDK + sd0;
+    uint4 k0r, k1r, v0r, v1r;
+#define ATHD_FETCH(K0)                                                                                   \
+    do {                                                                                                 \
+        const int ka = min((K0) + skey, d.Nk - 1), kb = min((K0) + skey + 32, d.Nk - 1);                \
+        k0r = *reinterpret_cast<const uint4*>(Kb + (int64_t)ka * d.k_ld + sd0);                          \
+        k1r = *reinterpret_cast<const uint4*>(Kb + (int64_t)kb * d.k_ld + sd0);                          \
+        v0r = *reinterpret_cast<const uint4*>(Vb + (int64_t)ka * d.v_ld + sd0);                          \
+        v1r = *reinterpret_cast<const uint4*>(Vb + (int64_t)kb * d.v_ld + sd0);                          \
+    } while (0)
+#define ATHD_STASH(ST)                                                                                   \
+    do {                                                                                                 \
+        *reinterpret_cast<uint4*>(&Ks[ST][soff]) = k0r;                                                  \
+        *reinterpret_cast<uint4*>(&Ks[ST][soff + 32 * LDK]) = k1r;                                       \
+        *reinterpret_cast<uint4*>(&Vs[ST][soff]) = v0r;                                                  \
+        *reinterpret_cast<uint4*>(&Vs[ST][soff + 32 * LDK]) = v1r;                                       \
+    } while (0)
+
+    f32x4_t o[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) o[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    float mrun[2] = {-INFINITY, -INFINITY};
+    float lrun[2] = {0.f, 0.f};
+
+    ATHD_FETCH(0);
+    ATHD_STASH(0);
+    __syncthreads();
+    int cur = 0;
+    for (int k0 = 0; k0 < d.Nk; k0 += 64) {
+        const bool more = k0 + 64 < d.Nk;
+        if (more) ATHD_FETCH(k0 + 64);
+        const bf16_t* K_ = Ks[cur];
+        const bf16_t* V_ = Vs[cur];
+        // ---- S^T = K Q^T ----
+        f32x4_t s[4][2];
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+            for (int nt = 0; nt < 2; ++nt) s[mt][nt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                const bf16v8 a = *reinterpret_cast<const bf16v8*>(&K_[(16 * mt + c16) * LDK + 32 * c + 8 * g]);
+#pragma unroll
+                for (int nt = 0; nt < 2; ++nt)
+                    s[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, qb[nt][c], s[mt][nt], 0, 0, 0);
+            }
+        // ---- online softmax (per query column) ----
+        float p[4][2][4];
+        const bool tail = k0 + 64 > d.Nk;
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) {
+            float mx = -INFINITY;
+#pragma unroll
+            for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    float v = s[mt][nt][r] * sl2;
+                    if (tail && k0 + 16 * mt + 4 * g + r >= d.Nk) v = -INFINITY;
+                    p[mt][nt][r] = v;
+                    mx = fmaxf(mx, v);
+                }
+            mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+            mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+            const float mnew = fmaxf(mrun[nt], mx);
+            const float alpha = __builtin_amdgcn_exp2f(mrun[nt] - mnew);
+            mrun[nt] = mnew;
+            float ls = 0.f;
+#pragma unroll
+            for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float e = __builtin_amdgcn_exp2f(p[mt][nt][r] - mnew);
+                    p[mt][nt][r] = e;
+                    ls += e;
+                }
+            lrun[nt] = lrun[nt] * alpha + ls;
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) o[dt][nt][r] *= alpha;
+        }
+        // ---- O^T += V^T P^T ----
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+            bf16v8 pb[2];
+#pragma unroll
+            for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    pb[nt][j] = (__bf16)p[2 * kk][nt][j];
+                    pb[nt][4 + j] = (__bf16)p[2 * kk + 1][nt][j];
+                }
+            // tr-read addresses: lane 4q+p of group g -> row (key) k0' + q, columns d0 + 4p
+            const int qrow = c16 >> 2, pcol = c16 & 3;
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt) {
+                const bf16_t* base = &V_[(32 * kk + 4 * g + qrow) * LDK + 16 * dt + 4 * pcol];
+                const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)base);
+                const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(base + 16 * LDK));
+                const bf16v8 a = __builtin_shufflevector(__builtin_bit_cast(bf16v4, lo), __builtin_bit_cast(bf16v4, hi),
+                                                         0, 1, 2, 3, 4, 5, 6, 7);
+#pragma unroll
+                for (int nt = 0; nt < 2; ++nt)
+                    o[dt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, pb[nt], o[dt][nt], 0, 0, 0);
+            }
+        }
+        if (more) ATHD_STASH(cur ^ 1);
+        __syncthreads();
+        cur ^= 1;
+    }
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+        float l = lrun[nt];
+        l += __shfl_xor(l, 16, 64);
+        l += __shfl_xor(l, 32, 64);
+        const float inv = 1.f / l;
+        const int q = q0 + 16 * nt + c16;
+        if (q >= d.Nq) continue;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+            const int64_t off = b * d.o_bs + (int64_t)q * d.o_ld + h * 64 + 16 * dt + 4 * g;
+            const float4 v = make_float4(o[dt][nt][0] * inv, o[dt][nt][1] * inv, o[dt][nt][2] * inv, o[dt][nt][3] * inv);
+            if (d.o_bf16) {
+                bf16_t t4[4] = {f2bf(v.x), f2bf(v.y), f2bf(v.z), f2bf(v.w)};
+                *reinterpret_cast<uint2*>((bf16_t*)d.O + off) = *reinterpret_cast<uint2*>(t4);
+            } else {
+                *reinterpret_cast<float4*>((float*)d.O + off) = v;
+            }
+        }
+    }
+}
+#undef ATHD_FETCH
+#undef ATHD_STASH
+
 int attn_launch(const AttnDesc& d, int mode, hipStream_t s) {
     if (d.heads * 64 > d.o_ld && d.o_ld != 0) return -2;
     dim3 grid((unsigned)((d.Nq + 127) / 128), (unsigned)d.heads, (unsigned)d.nb);
-    if (mode == 1) hipLaunchKernelGGL(attn_kernel<1>, grid, dim3(256), 0, s, d);
+    if (mode == 1 && d.q_bf16 && d.k_bf16 && d.v_bf16) hipLaunchKernelGGL(attn_bf16_kernel, grid, dim3(256), 0, s, d);
+    else if (mode == 1) hipLaunchKernelGGL(attn_kernel<1>, grid, dim3(256), 0, s, d);
     else hipLaunchKernelGGL(attn_kernel<0>, grid, dim3(256), 0, s, d);
     return (int)hipGetLastError();
 }

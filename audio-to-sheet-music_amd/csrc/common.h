@@ -19,6 +19,22 @@ ATHD_DEV bf16_t f2bf(float f) {
 ATHD_DEV float bf2f(bf16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
 
 ATHD_DEV float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752440f)); }
+// bf16-mode GELU: branch-free erf (Abramowitz & Stegun 7.1.26, |error| <= 1.5e-7 absolute), ~15 VALU ops vs ~60
+// with two branches for erff.  The f32 parity mode always uses gelu_erf.
+ATHD_DEV float erf_fast(float x) {
+    const float ax = fabsf(x);
+    const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, ax, 1.0f));
+    float p = fmaf(1.061405429f, t, -1.453152027f);
+    p = fmaf(p, t, 1.421413741f);
+    p = fmaf(p, t, -0.284496736f);
+    p = fmaf(p, t, 0.254829592f);
+    p *= t;
+    const float e = __builtin_amdgcn_exp2f(-ax * ax * 1.4426950408889634f);
+    return copysignf(fmaf(-p, e, 1.0f), x);
+}
+ATHD_DEV float gelu_fast(float x) { return 0.5f * x * (1.0f + erf_fast(x * 0.70710678118654752440f)); }
+template <bool FAST>
+ATHD_DEV float gelu(float x) { if constexpr (FAST) return gelu_fast(x); else return gelu_erf(x); }
 ATHD_DEV float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
 
 ATHD_DEV float wave_sum(float v) {

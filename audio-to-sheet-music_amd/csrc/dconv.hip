@@ -155,7 +155,7 @@ __global__ __launch_bounds__(256) void dconv_c1_kernel(float* __restrict__ x, co
 
 int dconv_small_launch(float* x, float* h, int64_t nb, int64_t L, int C, int dil, const float* w3, const float* b3,
                        const float* g1w, const float* g1b, const float* w1, const float* b1, const float* g2w,
-                       const float* g2b, const float* scale, double* st_h, double* st_y, hipStream_t s) {
+                       const float* g2b, const float* scale, double* st_h, double* st_y, hipStream_t s, bool fast) {
     const int64_t P = nb * L;
     const dim3 grid((unsigned)((P + 255) / 256));
     const int H = C / 8;
@@ -166,7 +166,7 @@ int dconv_small_launch(float* x, float* h, int64_t nb, int64_t L, int C, int dil
     } else {
         return -2;
     }
-    gn_gelu_launch(h, (int)nb, L * H, H, st_h, g1w, g1b, s);
+    gn_gelu_launch(h, (int)nb, L * H, H, st_h, g1w, g1b, s, fast);
     if (C == 48) {
         hipLaunchKernelGGL((dconv_c1_kernel<48, false>), grid, dim3(256), 0, s, x, h, nb, L, w1, b1, st_y, g2w, g2b, scale);
         hipLaunchKernelGGL((dconv_c1_kernel<48, true>), grid, dim3(256), 0, s, x, h, nb, L, w1, b1, st_y, g2w, g2b, scale);

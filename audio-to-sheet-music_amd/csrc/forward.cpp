@@ -179,7 +179,7 @@ void dconv(Run& r, const EncW& e, const Bufs& b, float* x, int64_t nb, int64_t L
         if (C <= 96) {   // narrow levels: HBM-bound VALU kernels (dconv.hip)
             r.check(dconv_small_launch(x, b.hbuf, nb, L, C, dil, e.dc.w3f[dd], e.dc.c3[dd].bias, e.dc.g1w[dd],
                                        e.dc.g1b[dd], e.dc.w1f[dd], e.dc.b1f[dd], e.dc.g2wf[dd], e.dc.g2bf[dd],
-                                       e.dc.scale[dd], st_h, st_y, r.s), "dconv_small");
+                                       e.dc.scale[dd], st_h, st_y, r.s, r.actbf), "dconv_small");
             continue;
         }
         GemmDesc g;
@@ -188,7 +188,7 @@ void dconv(Run& r, const EncW& e, const Bufs& b, float* x, int64_t nb, int64_t L
         g.Wp = e.dc.c3[dd].w; g.N = Hh; g.K = e.dc.c3[dd].K; g.Kp = e.dc.c3[dd].Kp; g.bias = e.dc.c3[dd].bias;
         g.C = b.hbuf; g.H_out_total = (int)L; g.ldo = Hh; g.stats = st_h;
         r.gemm(g, "dconv.conv3");
-        gn_gelu_launch(b.hbuf, (int)nb, L * Hh, Hh, st_h, e.dc.g1w[dd], e.dc.g1b[dd], r.s);
+        gn_gelu_launch(b.hbuf, (int)nb, L * Hh, Hh, st_h, e.dc.g1w[dd], e.dc.g1b[dd], r.s, r.actbf);
         GemmDesc g2;
         g2.A = b.hbuf; g2.nb = (int)nb; g2.H_in = (int)L; g2.W = 1; g2.C_in = Hh; g2.a_ld = Hh; g2.H_out = (int)L;
         g2.Wp = e.dc.c1[dd].w; g2.N = 2 * C; g2.K = Hh; g2.Kp = e.dc.c1[dd].Kp; g2.bias = e.dc.c1[dd].bias;
@@ -427,7 +427,7 @@ void decode_chunk(Run& r, const Dims& d, const Bufs& b, int64_t s0, int64_t Bc, 
         // Tspec rows, + 0.1 * resize(saved[3][:, :192])
         double* st = r.stats(NI);
         conv_t(r, c->fdec[0], b.x_cond, ab, NI, 8, (int)Ts, b.G, 0, st, -1);
-        gn_gelu_launch(b.G, NI, 32 * Ts * 192, 192, st, c->fdec[0].gnw, c->fdec[0].gnb, r.s);
+        gn_gelu_launch(b.G, NI, 32 * Ts * 192, 192, st, c->fdec[0].gnw, c->fdec[0].gnb, r.s, r.actbf);
         MergeDesc m;
         m.src = b.G; m.H_src = 32; m.kept = 0; m.C = 192;
         m.skip = sv[3]; m.H_skip = 8; m.C_skip = 384; m.P = P;
@@ -442,7 +442,7 @@ void decode_chunk(Run& r, const Dims& d, const Bufs& b, int64_t s0, int64_t Bc, 
             double* sti = last ? nullptr : r.stats(NI);
             conv_t(r, w, b.D, ab, NI, (int)Ts, (int)Ts, b.G, ab, sti, last ? 2 : 1);
             MergeDesc mm;
-            mm.src = b.G; mm.src_bf16 = ab; mm.H_src = 4 * (int)Ts; mm.kept = 1; mm.C = w.cout;
+            mm.src = b.G; mm.src_bf16 = ab; mm.H_src = 4 * (int)Ts; mm.kept = 1; mm.C = w.cout; mm.fast_gelu = ab;
             mm.stats = sti; mm.gn_count = 4 * Ts * Ts * w.cout; mm.gn_w = w.gnw; mm.gn_b = w.gnb;
             mm.skip = sv[3 - i]; mm.H_skip = skH[i - 1]; mm.C_skip = skC[i - 1]; mm.P = P;
             mm.H_out = (int)Ts; mm.W = (int)Ts; mm.NI = NI;
@@ -470,7 +470,7 @@ void decode_chunk(Run& r, const Dims& d, const Bufs& b, int64_t s0, int64_t Bc, 
             conv_t(r, w, A, ab, NI, (int)Lin, 1, b.G, ab, st, -1);
             const int64_t target = d.L[3 - i];       // lengths_t reversed
             MergeDesc m;
-            m.src = b.G; m.src_bf16 = ab; m.H_src = (int)(4 * Lin); m.kept = 0; m.C = w.cout;
+            m.src = b.G; m.src_bf16 = ab; m.H_src = (int)(4 * Lin); m.kept = 0; m.C = w.cout; m.fast_gelu = ab;
             m.stats = st; m.gn_count = 4 * Lin * w.cout; m.gn_w = w.gnw; m.gn_b = w.gnb;
             m.skip = svt[3 - i]; m.H_skip = (int)d.L[4 - i]; m.C_skip = ENC_CH[3 - i]; m.P = P;
             m.out = b.D; m.out_bf16 = last ? 0 : ab; m.H_out = (int)target; m.W = 1; m.NI = NI;

@@ -244,7 +244,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmDesc d) {
         __syncthreads();
     }
 
-    gemm_epilogue<TM, TN, F_ALL>(d, acc, m0, n0, wm0, wn0, lane, st_lds, BM);
+    gemm_epilogue<TM, TN, F_ALL, MODE == 1>(d, acc, m0, n0, wm0, wn0, lane, st_lds, BM);
 }
 
 template <int MODE, int BM, int BN, int WM, int WN>
@@ -266,10 +266,14 @@ static void launch_mode(const GemmDesc& d, hipStream_t s) {
 
 bool gemm2_supported(const GemmDesc& d);
 int gemm2_launch(const GemmDesc& d, hipStream_t s);
+bool gemm3_supported(const GemmDesc& d);
+int gemm3_launch(const GemmDesc& d, hipStream_t s, int variant);
 
 int gemm_launch(const GemmDesc& d, int mode, hipStream_t s) {
     if (d.Kp % BK != 0 || d.Kp < d.K || d.C_in <= 0 || d.N <= 0) return -2;
     if (d.act == ACT_GLU && (d.N % 32 != 0)) return -2;
+    // bf16 activations with N >= 192: 256x192 tile, 8 waves (gemm3.hip); measured best on every large shape here
+    if (mode == 1 && gemm3_supported(d) && d.N >= 192) return gemm3_launch(d, s, 3);
     if (mode == 1 && gemm2_supported(d)) return gemm2_launch(d, s);
     if (mode == 1) launch_mode<1>(d, s);
     else launch_mode<0>(d, s);

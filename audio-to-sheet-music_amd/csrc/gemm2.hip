@@ -164,7 +164,7 @@ __global__ __launch_bounds__(256) void gemm2_kernel(const GemmDesc d) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
     }
-    gemm_epilogue<TM, TN, F>(d, acc, m0, n0, wm0, wn0, lane, st_lds, BM);
+    gemm_epilogue<TM, TN, F, true>(d, acc, m0, n0, wm0, wn0, lane, st_lds, BM);
 }
 
 bool gemm2_supported(const GemmDesc& d) {

@@ -1,0 +1,171 @@
+// GEMM v3 (bf16 MFMA, gfx950), for bf16 activations: BM x BN x 64 tiles, WM x WN waves, a STAGES-deep LDS ring
+// filled by global_load_lds_dwordx4 with a COUNTED vmcnt and raw s_barrier, so STAGES-2 tiles stay in flight
+// across every barrier (a __syncthreads() would drain them: cdna_hip_programming.md §5 "Pipelining across
+// barriers").  LDS image and swizzle as in gemm2.hip (per-lane source chunk (L%8)^(L/8), slot = chunk ^ (row&7)).
+// Same descriptor and epilogue (C^T tiles) as the other GEMM kernels.
+#include "common.h"
+#include "gemm.h"
+#include "gemm_epi.h"
+
+namespace athd {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16v8;
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) void gbl_void;
+
+static __device__ __attribute__((aligned(64))) uint4 g_zero_page3[4];
+
+template <int N>
+ATHD_DEV void wait_vm() {
+    static_assert(N >= 0 && N < 64, "vmcnt");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int BM, int BN, int WM, int WN, int STAGES, unsigned F>
+__global__ __launch_bounds__(WM * WN * 64) void gemm3_kernel(const GemmDesc d) {
+    constexpr int NW = WM * WN;
+    constexpr int ROWB = 128;
+    constexpr int STAGE = (BM + BN) * ROWB;
+    constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
+    constexpr int AQ = BM / 8 / NW, BQ = BN / 8 / NW;
+    static_assert(AQ * 8 * NW == BM && BQ * 8 * NW == BN, "tile / wave count");
+    constexpr int LPT = AQ + BQ;                 // LDS-DMA instructions per wave per tile
+    __shared__ __attribute__((aligned(16))) char smem[STAGES * STAGE + 2 * EPI_MAXG * 8];
+    double* st_lds = reinterpret_cast<double*>(smem + STAGES * STAGE);
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm0 = (wave / WN) * (BM / WM), wn0 = (wave % WN) * (BN / WN);
+    const int64_t M = (int64_t)d.nb * d.H_out * d.W;
+    const int64_t m0 = (int64_t)blockIdx.x * BM;
+    const int n0 = blockIdx.y * BN;
+    const int64_t a_bs = d.a_bs >= 0 ? d.a_bs : (int64_t)d.H_in * d.W * d.a_ld;
+    const int64_t rowpitch = (int64_t)d.W * d.a_ld;
+    const int lrow = lane >> 3;
+    const int chunk = (lane & 7) ^ lrow;
+
+    int64_t a_base[AQ];
+    int a_h0[AQ];
+    bool a_ok[AQ];
+#pragma unroll
+    for (int q = 0; q < AQ; ++q) {
+        const uint32_t m = (uint32_t)(m0 + 8 * (wave + NW * q) + lrow);
+        a_ok[q] = m < (uint32_t)M;
+        const uint32_t mm = a_ok[q] ? m : 0u;
+        const uint32_t w = mm % (uint32_t)d.W;
+        const uint32_t t = mm / (uint32_t)d.W;
+        const uint32_t ho = t % (uint32_t)d.H_out;
+        const uint32_t b = t / (uint32_t)d.H_out;
+        a_base[q] = (int64_t)b * a_bs + (int64_t)w * d.a_ld;
+        a_h0[q] = (int)ho * d.in_stride + d.in_off;
+    }
+    const char* bptr[BQ];
+#pragma unroll
+    for (int q = 0; q < BQ; ++q) {
+        const int n = n0 + 8 * (wave + NW * q) + lrow;
+        bptr[q] = n < d.N ? (const char*)d.Wp + ((int64_t)n * d.Kp + 8 * chunk) * 2 : nullptr;
+    }
+    int k_cur = 8 * chunk, tap = k_cur / d.C_in, ci = k_cur - tap * d.C_in;
+    const char* zero = reinterpret_cast<const char*>(g_zero_page3);
+    const int nk = d.Kp / 64;
+
+    auto issue = [&](int kt, int st) {
+        char* sA = smem + st * STAGE;
+        char* sB = sA + BM * ROWB;
+        const bool kok = k_cur < d.K;
+#pragma unroll
+        for (int q = 0; q < AQ; ++q) {
+            const int row = a_h0[q] + tap * d.dil;
+            const bool ok = a_ok[q] && kok && row >= 0 && row < d.H_in;
+            const char* src = ok ? (const char*)d.A + (a_base[q] + (int64_t)row * rowpitch + ci) * 2 : zero;
+            __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(sA + (wave + NW * q) * 1024), 16, 0, 0);
+        }
+#pragma unroll
+        for (int q = 0; q < BQ; ++q) {
+            const char* src = bptr[q] ? bptr[q] + (int64_t)kt * 128 : zero;
+            __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(sB + (wave + NW * q) * 1024), 16, 0, 0);
+        }
+        k_cur += 64;
+        ci += 64;
+        while (ci >= d.C_in) { ci -= d.C_in; ++tap; }
+    };
+
+    f32x4_t acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    if (d.stats && tid < 2 * EPI_MAXG) st_lds[tid] = 0.0;
+
+    // prologue: STAGES-1 tiles in flight, wait for tile 0
+#pragma unroll
+    for (int s = 0; s < STAGES - 1; ++s)
+        if (s < nk) issue(s, s);
+    if (nk >= STAGES - 1) wait_vm<(STAGES - 2) * LPT>();
+    else wait_vm<0>();
+    __builtin_amdgcn_s_barrier();
+
+    const int fr = lane & 15, g = lane >> 4;
+    int cur = 0;
+    for (int kt = 0; kt < nk; ++kt) {
+        const int nxt = kt + STAGES - 1;
+        if (nxt < nk) issue(nxt, nxt % STAGES);
+        const char* sA = smem + cur * STAGE;
+        const char* sB = sA + BM * ROWB;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            const int slot = ((4 * ks + g) ^ (fr & 7)) * 16;
+            bf16v8 af[TM], bfr[TN];
+#pragma unroll
+            for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const bf16v8*>(sA + (wm0 + 16 * i + fr) * ROWB + slot);
+#pragma unroll
+            for (int j = 0; j < TN; ++j) bfr[j] = *reinterpret_cast<const bf16v8*>(sB + (wn0 + 16 * j + fr) * ROWB + slot);
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+        }
+        // tile kt+1 must have landed before the next iteration; tiles issued after it may stay in flight
+        if (nxt < nk) wait_vm<(STAGES - 2) * LPT>();
+        else wait_vm<0>();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        cur = cur + 1 == STAGES ? 0 : cur + 1;
+    }
+    gemm_epilogue<TM, TN, F, true>(d, acc, m0, n0, wm0, wn0, lane, st_lds, BM);
+}
+
+bool gemm3_supported(const GemmDesc& d) {
+    return d.a_bf16 && !d.a_norm && d.C_in % 8 == 0 && d.a_ld % 8 == 0 && d.a_cs == 1 && d.Kp % 64 == 0 && d.N >= 96 && d.col_split % 4 == 0 &&
+           (d.act != ACT_GLU || d.N % 32 == 0);
+}
+
+template <int BM, int BN, int WM, int WN, int ST, unsigned F>
+static void launch3f(const GemmDesc& d, hipStream_t s) {
+    const int64_t M = (int64_t)d.nb * d.H_out * d.W;
+    dim3 grid((unsigned)((M + BM - 1) / BM), (unsigned)((d.N + BN - 1) / BN));
+    hipLaunchKernelGGL((gemm3_kernel<BM, BN, WM, WN, ST, F>), grid, dim3(WM * WN * 64), 0, s, d);
+}
+
+template <int BM, int BN, int WM, int WN, int ST>
+static void launch3(const GemmDesc& d, hipStream_t s) {
+    switch (epi_flags(d)) {
+#define ATHD_CASE(FL) \
+    case (FL): launch3f<BM, BN, WM, WN, ST, (FL)>(d, s); return;
+        ATHD_EPI_LIST(ATHD_CASE)
+#undef ATHD_CASE
+        default: launch3f<BM, BN, WM, WN, ST, F_ALL>(d, s); return;
+    }
+}
+
+// variant: 0 = auto, 1 = 256x128 (8 waves, 3 stages), 2 = 128x128 (4 waves, 3 stages), 3 = 256x192 (8 waves, 2 st)
+int gemm3_launch(const GemmDesc& d, hipStream_t s, int variant) {
+    if (variant == 0) variant = (d.N % 192 == 0 && d.N % 128 != 0) ? 3 : 1;
+    if (variant == 1) launch3<256, 128, 4, 2, 3>(d, s);
+    else if (variant == 2) launch3<128, 128, 2, 2, 3>(d, s);
+    else launch3<256, 192, 4, 2, 2>(d, s);
+    return (int)hipGetLastError();
+}
+
+}  // namespace athd

@@ -41,7 +41,7 @@ inline unsigned epi_flags(const GemmDesc& d) {
 template <unsigned F>
 ATHD_DEV bool on(unsigned flag) { return (F & flag) != 0; }
 
-template <int TM, int TN, unsigned F>
+template <int TM, int TN, unsigned F, bool FASTG>
 ATHD_DEV void gemm_epilogue(const GemmDesc& d, const f32x4_t (&acc)[TM][TN], int64_t m0, int n0, int wm0, int wn0,
                             int lane, double* st_lds, int BM) {
     // Transposed accumulators (the kernels issue mfma(W_frag, A_frag)): lane l holds, for tile (i, j), output row
@@ -145,7 +145,7 @@ ATHD_DEV void gemm_epilogue(const GemmDesc& d, const f32x4_t (&acc)[TM][TN], int
                     for (int q = 0; q < 4; ++q) {
                         float v = acc[i][j][q] + bv[q];
                         if (f_gn) v = (v - gm) * gr * d.gn_w[n + q] + d.gn_b[n + q];
-                        if (f_gelu) v = gelu_erf(v);
+                        if (f_gelu) v = gelu<FASTG>(v);
                         if (f_row) v += d.row_add[(int64_t)ho * Nout + n + q];
                         o[q] = v;
                     }

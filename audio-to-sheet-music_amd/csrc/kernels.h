@@ -29,7 +29,7 @@ void input_norm_params_launch(const double* stats, int nb, int64_t n, float* mea
                               hipStream_t s);
 // h[nb][L*H] = GELU(GN(h)) in place (GroupNorm(1,H), stats over L*H per nb)
 void gn_gelu_launch(float* h, int nb, int64_t per_batch, int H, const double* stats, const float* w,
-                    const float* b, hipStream_t s);
+                    const float* b, hipStream_t s, bool fast);
 // x[nb][N][C] = GN(x) in place
 void gn_apply_launch(float* x, int nb, int64_t N, int C, const double* stats, const float* w, const float* b,
                      hipStream_t s);
@@ -57,12 +57,13 @@ struct MergeDesc {
     const float* skip = nullptr; int H_skip = 0; int C_skip = 0; int P = 1;
     void* out = nullptr; int out_bf16 = 0; int H_out = 0; int W = 1; int NI = 1;
     const float* proj_w = nullptr; const float* proj_b = nullptr;   // optional 1x1 C(=4) -> 2 projection
+    int fast_gelu = 0;                            // bf16 mode: branch-free erf
 };
 void dec_merge_launch(const MergeDesc& d, hipStream_t s);
 // dconv.hip: one DConv layer (conv3 -> GN -> GELU -> 1x1 -> GN -> GLU -> LayerScale -> residual) for C in {48, 96}
 int dconv_small_launch(float* x, float* h, int64_t nb, int64_t L, int C, int dil, const float* w3, const float* b3,
                        const float* g1w, const float* g1b, const float* w1, const float* b1, const float* g2w,
-                       const float* g2b, const float* scale, double* st_h, double* st_y, hipStream_t s);
+                       const float* g2b, const float* scale, double* st_h, double* st_y, hipStream_t s, bool fast);
 // positional tables of the cross-transformer (computed on device with the fp32 op order of demucs)
 void pos2d_launch(float* out, int Fr, int T1, int C, hipStream_t s);   // out[(f*T1+t)][C]
 void pos1d_launch(float* out, int T2, int C, hipStream_t s);           // out[t][C]

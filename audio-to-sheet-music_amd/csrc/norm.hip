@@ -60,6 +60,7 @@ ATHD_DEV void gn_params(const double* st, int64_t b, int64_t count, float& mean,
 }
 
 // --------------------------------------------------------------------------------------------- GroupNorm users
+template <bool FAST>
 __global__ __launch_bounds__(256) void gn_gelu_kernel(float* __restrict__ h, int64_t per_batch, int H,
                                                       const double* __restrict__ st, const float* __restrict__ w,
                                                       const float* __restrict__ bb) {
@@ -70,15 +71,16 @@ __global__ __launch_bounds__(256) void gn_gelu_kernel(float* __restrict__ h, int
     const int n = (int)per_batch;      // < 2^31 per batch on every use
     for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
         const int c = i % H;
-        p[i] = gelu_erf((p[i] - mean) * rstd * w[c] + bb[c]);
+        p[i] = gelu<FAST>((p[i] - mean) * rstd * w[c] + bb[c]);
     }
 }
 
 void gn_gelu_launch(float* h, int nb, int64_t per_batch, int H, const double* stats, const float* w, const float* b,
-                    hipStream_t s) {
+                    hipStream_t s, bool fast) {
     int blocks = (int)((per_batch + 255) / 256);
     if (blocks > 1024) blocks = 1024;
-    hipLaunchKernelGGL(gn_gelu_kernel, dim3(blocks, nb), dim3(256), 0, s, h, per_batch, H, stats, w, b);
+    if (fast) hipLaunchKernelGGL(gn_gelu_kernel<true>, dim3(blocks, nb), dim3(256), 0, s, h, per_batch, H, stats, w, b);
+    else hipLaunchKernelGGL(gn_gelu_kernel<false>, dim3(blocks, nb), dim3(256), 0, s, h, per_batch, H, stats, w, b);
 }
 
 __global__ __launch_bounds__(256) void gn_apply_kernel(float* __restrict__ x, int64_t per_batch, int C,
@@ -248,8 +250,13 @@ ATHD_DEV void merge_src_v(const MergeDesc& d, int64_t item, int i, int w, int c,
     }
     ldv<V>(d.src, d.src_bf16, item * (int64_t)rows * d.W * d.C + ((int64_t)slot * d.W + w) * d.C + c, x);
     if (d.stats) {
+        if (d.fast_gelu) {
 #pragma unroll
-        for (int j = 0; j < V; ++j) x[j] = gelu_erf((x[j] - mean) * rstd * d.gn_w[c + j] + d.gn_b[c + j]);
+            for (int j = 0; j < V; ++j) x[j] = gelu_fast((x[j] - mean) * rstd * d.gn_w[c + j] + d.gn_b[c + j]);
+        } else {
+#pragma unroll
+            for (int j = 0; j < V; ++j) x[j] = gelu_erf((x[j] - mean) * rstd * d.gn_w[c + j] + d.gn_b[c + j]);
+        }
     }
 }
 

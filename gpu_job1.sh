@@ -10,5 +10,5 @@ timeout -k 10 400 python bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpuru
 rc=$?
 echo "bench rc=$rc"; tail -5 gpurun_out/bench.log
 if [ $rc -ne 0 ]; then exit $rc; fi
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof5 -o run -- python bench.py --steps 2 --warmup 1 --batch 16 --no-cpu-baseline > gpurun_out/prof1.log 2>&1
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof6 -o run -- python bench.py --steps 2 --warmup 1 --batch 16 --no-cpu-baseline > gpurun_out/prof1.log 2>&1
 echo "rocprof rc=$?"

@@ -167,3 +167,47 @@ def test_intermediates_f32(models, oracle_model, text_table):
     _report("intermediates_f32", res)
     bad = {k: v for k, v in res.items() if v["sdr_db"] < F32_SDR_DB}
     assert not bad, bad
+
+
+SHARP_SCALE = 6.0          # Q and K in-projection rows x6: logits x36, mean max softmax prob ~0.1-0.3 (vs ~0.005)
+SHARP_BF16_SDR_DB = 20.0   # bf16 logit rounding is amplified by the sharpening
+
+
+def test_sharp_attention_encoder(state_dict, text_table):
+    """With the synthetic weights every attention row is nearly uniform (max prob ~ 1/Nk), so a kernel that pairs
+    P with the wrong V rows inside a key tile would still pass the model-level tests.  Sharpen all ten transformer
+    attentions (scale W_q, W_k) and compare the transformer output x_enc / xt_enc with the oracle."""
+    from athd.model import AudioTextHTDemucs
+    from athd.synth import synthetic_batch
+    from athd.weights import STEMS
+    from oracle.athtdemucs_ref import AudioTextHTDemucsRef
+    sd = dict(state_dict)
+    for k in sd:
+        if "crosstransformer" in k and k.endswith("in_proj_weight"):
+            w = np.array(sd[k], dtype=np.float32, copy=True)
+            w[:1024] *= SHARP_SCALE
+            sd[k] = w
+    wav = torch.as_tensor(synthetic_batch(2, 30000, seed0=11))
+    te = torch.as_tensor(text_table[[1, 2]])
+    cap = {}
+    AudioTextHTDemucsRef(sd).forward(wav, te, capture=cap)
+    ref = {"x_enc": cap["x_enc"].permute(0, 2, 3, 1).numpy(), "xt_enc": cap["xt_enc"].permute(0, 2, 1).numpy()}
+    table = {s: text_table[i] for i, s in enumerate(STEMS)}
+    res = {}
+    for dt in ("f32", "bf16"):
+        m = AudioTextHTDemucs(dtype=dt, text_table=table)
+        m.load_state_dict(sd)
+        m = m.to("cuda").eval()
+        with tempfile.TemporaryDirectory() as tmp:
+            os.environ["ATHD_DUMP"] = tmp
+            try:
+                m(wav.cuda(), ["bass", "other"])
+                torch.cuda.synchronize()
+            finally:
+                del os.environ["ATHD_DUMP"]
+            for name in ("x_enc", "xt_enc"):
+                got = np.fromfile(os.path.join(tmp, name + ".f32"), dtype=np.float32)
+                res[f"{dt}/{name}"] = sdr_db(ref[name].reshape(-1), got)
+    _report("sharp_attention", res)
+    for key, v in res.items():
+        assert v >= (F32_SDR_DB if key.startswith("f32") else SHARP_BF16_SDR_DB), res

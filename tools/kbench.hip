@@ -8,6 +8,7 @@
 using namespace athd;
 namespace athd {
 int gemm2_launch(const GemmDesc& d, hipStream_t s);
+int gemm3_launch(const GemmDesc& d, hipStream_t s, int variant);
 }
 
 extern "C" {
@@ -19,6 +20,7 @@ int kb_gemm(int variant, const void* A, int a_bf16, const void* W, const float* 
     d.Wp = W; d.N = N; d.K = K; d.Kp = Kp; d.bias = bias; d.C = C; d.c_bf16 = c_bf16; d.H_out_total = M; d.ldo = N;
     d.act = act;
     if (variant == 2) return gemm2_launch(d, (hipStream_t)stream);
+    if (variant >= 30) return gemm3_launch(d, (hipStream_t)stream, variant - 30);
     return gemm_launch(d, 1, (hipStream_t)stream);
 }
 int kb_attn(const void* qkv, int nb, int N, void* out, void* stream) {
@@ -30,4 +32,20 @@ int kb_attn(const void* qkv, int nb, int N, void* out, void* stream) {
     a.O = out; a.o_bf16 = 1; a.o_bs = (int64_t)N * 512; a.o_ld = 512;
     return attn_launch(a, 1, (hipStream_t)stream);
 }
+}
+
+// probe: lane -> elements returned by ds_read_b64_tr_b16 with the attention kernel's addressing
+typedef short kb_v4i16 __attribute__((ext_vector_type(4)));
+__global__ void kb_tr_kernel(short* out) {
+    __shared__ __attribute__((aligned(16))) short t[64 * 72];
+    for (int i = threadIdx.x; i < 64 * 72; i += 64) t[i] = (short)((i / 72) * 256 + (i % 72));
+    __syncthreads();
+    const int lane = threadIdx.x, g = lane >> 4, c16 = lane & 15;
+    const short* base = &t[(4 * g + (c16 >> 2)) * 72 + 4 * (c16 & 3)];
+    kb_v4i16 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) kb_v4i16*)base);
+    for (int j = 0; j < 4; ++j) out[4 * lane + j] = v[j];
+}
+extern "C" int kb_tr(void* out) {
+    hipLaunchKernelGGL(kb_tr_kernel, dim3(1), dim3(64), 0, 0, (short*)out);
+    return (int)hipDeviceSynchronize();
 }

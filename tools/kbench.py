@@ -6,6 +6,7 @@ import sys
 import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
+VARIANTS = (2, 31, 32, 33)
 lib = ctypes.CDLL(os.path.join(HERE, "libkbench.so"))
 vp = ctypes.c_void_p
 
@@ -37,7 +38,7 @@ def gemm_case(M, N, K, act=0):
         ref = torch.nn.functional.gelu(ref)
     flops = 2.0 * M * N * K
     res = {}
-    for v in (1, 2):
+    for v in VARIANTS:
         f = lambda: lib.kb_gemm(v, vp(A.data_ptr()), 1, vp(W.data_ptr()), vp(bias.data_ptr()), vp(C.data_ptr()), 1,
                                 M, N, K, Kp, act, vp(st))
         us = timeit(f)
@@ -62,8 +63,22 @@ def attn_case(B, N):
     print(f"ATTN B={B} N={N}: athd {us:8.1f}us {flops / us / 1e6:7.1f}TF err={err:.1e} | torch sdpa {ust:8.1f}us {flops / ust / 1e6:7.1f}TF", flush=True)
 
 
+def tr_probe():
+    out = torch.zeros(64, 4, dtype=torch.int16, device="cuda")
+    lib.kb_tr(vp(out.data_ptr()))
+    o = out.cpu().numpy().astype(int)
+    for lane in range(0, 64, 5):
+        print(f"TR lane {lane:2d}: " + " ".join(f"({v // 256},{v % 256})" for v in o[lane]), flush=True)
+
+
 if __name__ == "__main__":
     torch.manual_seed(0)
+    if "tr" in sys.argv[1:]:
+        tr_probe()
+    if "attn" in sys.argv[1:]:
+        attn_case(4, 200)
+        attn_case(64, 2072)
+        sys.exit(0)
     M = 64 * 2072
     gemm_case(M, 1536, 512)
     gemm_case(M, 2048, 512, act=1)
