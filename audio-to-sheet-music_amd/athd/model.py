@@ -112,6 +112,13 @@ class AudioTextHTDemucs:
         self._ctx = ctx
         return ctx
 
+    def profile_start(self, kernel: Optional[str] = None):
+        """Measurement aid (bench.py): HIP-event timing of one kernel (or all) in the following forwards."""
+        self._ensure_ctx().profile_start(kernel)
+
+    def profile_stop(self) -> list:
+        return self._ensure_ctx().profile_stop()
+
     def _workspace(self, nbytes: int) -> torch.Tensor:
         if self._ws is None or self._ws.numel() < nbytes or self._ws.device != self.device:
             self._ws = None

@@ -34,14 +34,23 @@ lib.athd_forward.restype = _c.c_int
 lib.athd_forward_prompts.argtypes = [_c.c_void_p, _c.c_void_p, _c.c_int64, _c.c_int64, _c.c_void_p, _c.c_int,
                                      _c.c_void_p, _c.c_void_p, _c.c_size_t, _c.c_void_p]
 lib.athd_forward_prompts.restype = _c.c_int
+lib.athd_profile_start.argtypes = [_c.c_void_p, _c.c_char_p]
+lib.athd_profile_start.restype = _c.c_int
+lib.athd_profile_stop.argtypes = [_c.c_void_p]
+lib.athd_profile_stop.restype = _c.c_int
+lib.athd_profile_count.argtypes = [_c.c_void_p]
+lib.athd_profile_count.restype = _c.c_int
+lib.athd_profile_get.argtypes = [_c.c_void_p, _c.c_int, _c.POINTER(_c.c_char_p), _c.POINTER(_c.c_longlong),
+                                 _c.POINTER(_c.c_double), _c.POINTER(_c.c_double), _c.POINTER(_c.c_double)]
+lib.athd_profile_get.restype = _c.c_int
 lib.athd_last_error.argtypes = [_c.c_void_p]
 lib.athd_last_error.restype = _c.c_char_p
 lib.athd_destroy.argtypes = [_c.c_void_p]
 lib.athd_destroy.restype = None
 
 EXPORTED = ["athd_version", "athd_create", "athd_set_weight", "athd_num_required_keys", "athd_required_key",
-            "athd_finalize", "athd_workspace_bytes", "athd_forward", "athd_forward_prompts", "athd_last_error",
-            "athd_destroy"]
+            "athd_finalize", "athd_workspace_bytes", "athd_forward", "athd_forward_prompts", "athd_profile_start",
+            "athd_profile_stop", "athd_profile_count", "athd_profile_get", "athd_last_error", "athd_destroy"]
 
 F32, BF16 = 0, 1
 
@@ -89,6 +98,23 @@ class Context:
     def forward_prompts(self, wav_ptr, B, T, table_ptr, P, out_ptr, ws_ptr, ws_bytes, stream_ptr):
         self._check(lib.athd_forward_prompts(self.h, wav_ptr, B, T, table_ptr, P, out_ptr, ws_ptr, ws_bytes,
                                              stream_ptr), "athd_forward_prompts")
+
+    def profile_start(self, kernel: str | None = None):
+        """Time every launch of `kernel` (rocprof symbol short form; None = all kernels) with HIP events."""
+        self._check(lib.athd_profile_start(self.h, kernel.encode() if kernel else None), "athd_profile_start")
+
+    def profile_stop(self) -> list:
+        """Synchronise the profile window; per kernel: launches, ms (summed event time), algorithmic flops/bytes."""
+        self._check(lib.athd_profile_stop(self.h), "athd_profile_stop")
+        out = []
+        for i in range(lib.athd_profile_count(self.h)):
+            name, n = _c.c_char_p(), _c.c_longlong()
+            ms, fl, by = _c.c_double(), _c.c_double(), _c.c_double()
+            self._check(lib.athd_profile_get(self.h, i, _c.byref(name), _c.byref(n), _c.byref(ms), _c.byref(fl),
+                                             _c.byref(by)), "athd_profile_get")
+            out.append({"kernel": name.value.decode(), "launches": n.value, "ms": ms.value, "flops": fl.value,
+                        "bytes": by.value})
+        return out
 
     def close(self):
         if getattr(self, "h", None):

@@ -347,11 +347,44 @@ int athd_finalize(athd_ctx* c) {
     return ATHD_OK;
 }
 
+int athd_profile_start(athd_ctx* c, const char* kernel) {
+    if (!c) return ATHD_EINVAL;
+    delete c->prof;
+    c->prof = new KProf();
+    c->prof->only = kernel ? kernel : "";
+    c->prof_done.agg.clear();
+    return ATHD_OK;
+}
+
+int athd_profile_stop(athd_ctx* c) {
+    if (!c || !c->prof) return c ? c->fail(ATHD_ESTATE, "athd_profile_stop without start") : ATHD_EINVAL;
+    const int rc = c->prof->collect();
+    c->prof_done.agg = c->prof->agg;
+    delete c->prof;
+    c->prof = nullptr;
+    return rc == 0 ? ATHD_OK : c->fail(ATHD_EHIP, "profile event query failed");
+}
+
+int athd_profile_count(athd_ctx* c) { return c ? (int)c->prof_done.agg.size() : 0; }
+
+int athd_profile_get(athd_ctx* c, int i, const char** kernel, long long* launches, double* ms, double* flops,
+                     double* bytes) {
+    if (!c || i < 0 || i >= (int)c->prof_done.agg.size()) return ATHD_EINVAL;
+    const auto& g = c->prof_done.agg[i];
+    if (kernel) *kernel = g.label.c_str();
+    if (launches) *launches = g.n;
+    if (ms) *ms = g.ms;
+    if (flops) *flops = g.flops;
+    if (bytes) *bytes = g.bytes;
+    return ATHD_OK;
+}
+
 const char* athd_last_error(athd_ctx* c) { return c ? c->err.c_str() : "null context"; }
 
 void athd_destroy(athd_ctx* c) {
     if (!c) return;
     for (void* p : c->allocs) hipFree(p);
+    delete c->prof;
     delete c;
 }
 

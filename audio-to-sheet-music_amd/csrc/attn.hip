@@ -6,6 +6,7 @@
 // O^T += V^T . P^T (the k order inside a step is permuted identically for A and B; see common comments in
 // gemm.hip).  K is staged in LDS as [key][d], V transposed as [d][key].  Grid: (ceil(Nq/128), heads, batch).
 #include "common.h"
+#include "prof.h"
 #include "attn.h"
 
 namespace athd {
@@ -412,6 +413,15 @@ __global__ __launch_bounds__(256) void attn_bf16_kernel(const AttnDesc d) {
 int attn_launch(const AttnDesc& d, int mode, hipStream_t s) {
     if (d.heads * 64 > d.o_ld && d.o_ld != 0) return -2;
     dim3 grid((unsigned)((d.Nq + 127) / 128), (unsigned)d.heads, (unsigned)d.nb);
+    KScope ks(s);
+    if (ks.on()) {
+        const bool v2 = mode == 1 && d.q_bf16 && d.k_bf16 && d.v_bf16;
+        const double nh = (double)d.nb * d.heads;
+        const double fl = 4.0 * nh * d.Nq * d.Nk * 64;
+        const double by = nh * 64 * (d.Nq * (d.q_bf16 ? 2 : 4) + d.Nk * ((d.k_bf16 ? 2 : 4) + (d.v_bf16 ? 2 : 4)) +
+                                     d.Nq * (d.o_bf16 ? 2 : 4));
+        ks.begin(v2 ? std::string("attn_bf16_kernel") : klabel("attn_kernel<%d>", mode), fl, by);
+    }
     if (mode == 1 && d.q_bf16 && d.k_bf16 && d.v_bf16) hipLaunchKernelGGL(attn_bf16_kernel, grid, dim3(256), 0, s, d);
     else if (mode == 1) hipLaunchKernelGGL(attn_kernel<1>, grid, dim3(256), 0, s, d);
     else hipLaunchKernelGGL(attn_kernel<0>, grid, dim3(256), 0, s, d);

@@ -7,6 +7,8 @@
 #include <string>
 #include <vector>
 
+#include "prof.h"
+
 namespace athd {
 
 struct HostT {
@@ -89,6 +91,8 @@ struct athd_ctx {
     std::string err;
     std::map<std::string, HostT> host;
     std::vector<void*> allocs;
+    athd::KProf* prof = nullptr;     // non-null between athd_profile_start / _stop
+    athd::KProf prof_done;           // aggregated results of the last profile window
 
     EncW fenc[4], tenc[4];
     float* femb = nullptr;           // [512][48] = (w * 10) * 0.2

@@ -6,6 +6,7 @@
 //   c1app:  x[p][c] += scale[c] * GLU(GN(y))[c]                                 (recomputes y: K = H is tiny)
 // A "group" is the GroupNorm(1) sample: nb index of [nb][L][C] (freq rows (b,f) along time, or time samples).
 #include "common.h"
+#include "prof.h"
 #include "kernels.h"
 
 namespace athd {
@@ -159,20 +160,26 @@ int dconv_small_launch(float* x, float* h, int64_t nb, int64_t L, int C, int dil
     const int64_t P = nb * L;
     const dim3 grid((unsigned)((P + 255) / 256));
     const int H = C / 8;
-    if (C == 48) {
-        hipLaunchKernelGGL((dconv_c3_kernel<48>), grid, dim3(256), 0, s, x, nb, L, dil, w3, b3, h, st_h);
-    } else if (C == 96) {
-        hipLaunchKernelGGL((dconv_c3_kernel<96>), grid, dim3(256), 0, s, x, nb, L, dil, w3, b3, h, st_h);
-    } else {
-        return -2;
+    const double px = (double)P;
+    if (C != 48 && C != 96) return -2;
+    {
+        KScope ks(s);
+        if (ks.on()) ks.begin(klabel("dconv_c3_kernel<%d>", C), 2.0 * px * H * 3 * C, px * (C + H) * 4);
+        if (C == 48) hipLaunchKernelGGL((dconv_c3_kernel<48>), grid, dim3(256), 0, s, x, nb, L, dil, w3, b3, h, st_h);
+        else hipLaunchKernelGGL((dconv_c3_kernel<96>), grid, dim3(256), 0, s, x, nb, L, dil, w3, b3, h, st_h);
     }
     gn_gelu_launch(h, (int)nb, L * H, H, st_h, g1w, g1b, s, fast);
-    if (C == 48) {
-        hipLaunchKernelGGL((dconv_c1_kernel<48, false>), grid, dim3(256), 0, s, x, h, nb, L, w1, b1, st_y, g2w, g2b, scale);
-        hipLaunchKernelGGL((dconv_c1_kernel<48, true>), grid, dim3(256), 0, s, x, h, nb, L, w1, b1, st_y, g2w, g2b, scale);
-    } else {
-        hipLaunchKernelGGL((dconv_c1_kernel<96, false>), grid, dim3(256), 0, s, x, h, nb, L, w1, b1, st_y, g2w, g2b, scale);
-        hipLaunchKernelGGL((dconv_c1_kernel<96, true>), grid, dim3(256), 0, s, x, h, nb, L, w1, b1, st_y, g2w, g2b, scale);
+    {
+        KScope ks(s);
+        if (ks.on()) ks.begin(klabel("dconv_c1_kernel<%d,false>", C), 2.0 * px * 2 * C * H, px * H * 4);
+        if (C == 48) hipLaunchKernelGGL((dconv_c1_kernel<48, false>), grid, dim3(256), 0, s, x, h, nb, L, w1, b1, st_y, g2w, g2b, scale);
+        else hipLaunchKernelGGL((dconv_c1_kernel<96, false>), grid, dim3(256), 0, s, x, h, nb, L, w1, b1, st_y, g2w, g2b, scale);
+    }
+    {
+        KScope ks(s);
+        if (ks.on()) ks.begin(klabel("dconv_c1_kernel<%d,true>", C), 2.0 * px * 2 * C * H, px * (H + 2 * C) * 4);
+        if (C == 48) hipLaunchKernelGGL((dconv_c1_kernel<48, true>), grid, dim3(256), 0, s, x, h, nb, L, w1, b1, st_y, g2w, g2b, scale);
+        else hipLaunchKernelGGL((dconv_c1_kernel<96, true>), grid, dim3(256), 0, s, x, h, nb, L, w1, b1, st_y, g2w, g2b, scale);
     }
     return (int)hipGetLastError();
 }

@@ -11,6 +11,7 @@
 #include "../../include/athd.h"
 #include "attn.h"
 #include "ctx.h"
+#include "prof.h"
 #include "gemm.h"
 #include "kernels.h"
 
@@ -543,6 +544,11 @@ int forward_impl(athd_ctx* c, const float* wav, int64_t B, int64_t T, const floa
     r.st_next = b.stats;
     if (hipMemsetAsync(b.stats, 0, (size_t)b.nstats * 2 * sizeof(double), r.s) != hipSuccess)
         return c->fail(ATHD_EHIP, "memset failed");
+    struct ProfBind {   // route this call's launches into the context's profile window (prof.h)
+        KProf* saved;
+        explicit ProfBind(KProf* p) : saved(t_kprof) { t_kprof = p; }
+        ~ProfBind() { t_kprof = saved; }
+    } prof_bind(c->prof);
     encode(r, d, b, wav);
     for (int64_t ch = 0; ch < d.chunks && r.err == 0; ++ch) {
         const int64_t s0 = ch * d.Bc;

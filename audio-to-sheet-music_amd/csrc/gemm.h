@@ -53,6 +53,17 @@ struct GemmDesc {
     const float* gn_b = nullptr;
 };
 
+// Algorithmic work of one launch (prof.h): 2 M N K flops; bytes = unique activations read once + packed weights +
+// outputs (+ residual read).  mode 1 weights are bf16, mode 0 f32.
+inline void gemm_work(const GemmDesc& d, int mode, double& flops, double& bytes) {
+    const double M = (double)d.nb * d.H_out * d.W;
+    flops = 2.0 * M * d.N * d.K;
+    const double nout = d.act == ACT_GLU ? d.N / 2 : d.N;
+    bytes = (double)d.nb * d.H_in * d.W * d.C_in * (d.a_bf16 ? 2 : 4) + (double)d.N * d.K * (mode == 1 ? 2 : 4);
+    if (d.store) bytes += M * nout * (d.c_bf16 ? 2 : 4);
+    if (d.res) bytes += M * nout * 4;
+}
+
 // mode: 0 = exact fp32 (v_mfma_f32_16x16x4_f32), 1 = bf16 (v_mfma_f32_16x16x32_bf16, fp32 accumulate)
 int gemm_launch(const GemmDesc& d, int mode, hipStream_t s);
 

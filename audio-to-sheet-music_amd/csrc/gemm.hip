@@ -9,6 +9,7 @@
 // Global->LDS is register staged and double buffered: tile t+1 is loaded into registers before the MFMAs of
 // tile t and written to the other LDS buffer after them; one barrier per k-step.
 #include "common.h"
+#include "prof.h"
 #include "gemm.h"
 #include "gemm_epi.h"
 
@@ -252,6 +253,12 @@ static void launch_cfg(const GemmDesc& d, hipStream_t s) {
     const int64_t M = (int64_t)d.nb * d.H_out * d.W;
     dim3 grid((unsigned)((M + BM - 1) / BM), (unsigned)((d.N + BN - 1) / BN));
     const bool vec8 = (d.C_in % 8 == 0) && (d.a_ld % 8 == 0) && d.a_cs == 1;
+    KScope ks(s);
+    if (ks.on()) {
+        double fl, by;
+        gemm_work(d, MODE, fl, by);
+        ks.begin(klabel("gemm_kernel<%d,%d,%d,%d,%d,%s>", MODE, BM, BN, WM, WN, vec8 ? "true" : "false"), fl, by);
+    }
     if (vec8) hipLaunchKernelGGL((gemm_kernel<MODE, BM, BN, WM, WN, true>), grid, dim3(256), 0, s, d);
     else hipLaunchKernelGGL((gemm_kernel<MODE, BM, BN, WM, WN, false>), grid, dim3(256), 0, s, d);
 }

@@ -11,6 +11,7 @@
 //     converted to bf16 and written with ds_write_b128 after the MFMAs of the current tile.
 // Two LDS stages: tile t+1 is issued before the MFMAs of tile t; one drain + barrier per k-tile.
 #include "common.h"
+#include "prof.h"
 #include "gemm.h"
 #include "gemm_epi.h"
 
@@ -178,6 +179,12 @@ template <int BM, int BN, unsigned F>
 static void launch2f(const GemmDesc& d, hipStream_t s) {
     const int64_t M = (int64_t)d.nb * d.H_out * d.W;
     dim3 grid((unsigned)((M + BM - 1) / BM), (unsigned)((d.N + BN - 1) / BN));
+    KScope ks(s);
+    if (ks.on()) {
+        double fl, by;
+        gemm_work(d, 1, fl, by);
+        ks.begin(klabel("gemm2_kernel<%d,%d,%s,%u>", BM, BN, d.a_bf16 ? "true" : "false", F), fl, by);
+    }
     if (d.a_bf16) hipLaunchKernelGGL((gemm2_kernel<BM, BN, true, F>), grid, dim3(256), 0, s, d);
     else hipLaunchKernelGGL((gemm2_kernel<BM, BN, false, F>), grid, dim3(256), 0, s, d);
 }

@@ -4,6 +4,7 @@
 // barriers").  LDS image and swizzle as in gemm2.hip (per-lane source chunk (L%8)^(L/8), slot = chunk ^ (row&7)).
 // Same descriptor and epilogue (C^T tiles) as the other GEMM kernels.
 #include "common.h"
+#include "prof.h"
 #include "gemm.h"
 #include "gemm_epi.h"
 
@@ -145,6 +146,12 @@ template <int BM, int BN, int WM, int WN, int ST, unsigned F>
 static void launch3f(const GemmDesc& d, hipStream_t s) {
     const int64_t M = (int64_t)d.nb * d.H_out * d.W;
     dim3 grid((unsigned)((M + BM - 1) / BM), (unsigned)((d.N + BN - 1) / BN));
+    KScope ks(s);
+    if (ks.on()) {
+        double fl, by;
+        gemm_work(d, 1, fl, by);
+        ks.begin(klabel("gemm3_kernel<%d,%d,%d,%d,%d,%u>", BM, BN, WM, WN, ST, F), fl, by);
+    }
     hipLaunchKernelGGL((gemm3_kernel<BM, BN, WM, WN, ST, F>), grid, dim3(WM * WN * 64), 0, s, d);
 }
 

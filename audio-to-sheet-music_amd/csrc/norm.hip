@@ -2,6 +2,7 @@
 // GroupNorm/LayerNorm statistics are accumulated in fp64 (sum, sum of squares) so that the one-pass
 // variance matches PyTorch's fp32 two-pass/Welford results to rounding.
 #include "common.h"
+#include "prof.h"
 #include "kernels.h"
 
 namespace athd {
@@ -32,6 +33,8 @@ void stats_launch(const float* x, int nb, int64_t n, double* stats, hipStream_t 
     int blocks = (int)((n + 256 * 16 - 1) / (256 * 16));
     if (blocks > 512) blocks = 512;
     if (blocks < 1) blocks = 1;
+    KScope ks(s);
+    if (ks.on()) ks.begin("stats_kernel", 0.0, (double)nb * n * 4);
     hipLaunchKernelGGL(stats_kernel, dim3(blocks, nb), dim3(256), 0, s, x, n, stats);
 }
 
@@ -79,6 +82,8 @@ void gn_gelu_launch(float* h, int nb, int64_t per_batch, int H, const double* st
                     hipStream_t s, bool fast) {
     int blocks = (int)((per_batch + 255) / 256);
     if (blocks > 1024) blocks = 1024;
+    KScope ks(s);
+    if (ks.on()) ks.begin(fast ? "gn_gelu_kernel<true>" : "gn_gelu_kernel<false>", 0.0, 2.0 * nb * per_batch * 4);
     if (fast) hipLaunchKernelGGL(gn_gelu_kernel<true>, dim3(blocks, nb), dim3(256), 0, s, h, per_batch, H, stats, w, b);
     else hipLaunchKernelGGL(gn_gelu_kernel<false>, dim3(blocks, nb), dim3(256), 0, s, h, per_batch, H, stats, w, b);
 }
@@ -102,6 +107,8 @@ void gn_apply_launch(float* x, int nb, int64_t N, int C, const double* stats, co
     int64_t per = N * C;
     int blocks = (int)((per + 255) / 256);
     if (blocks > 1024) blocks = 1024;
+    KScope ks(s);
+    if (ks.on()) ks.begin("gn_apply_kernel", 0.0, 2.0 * nb * per * 4);
     hipLaunchKernelGGL(gn_apply_kernel, dim3(blocks, nb), dim3(256), 0, s, x, per, C, stats, w, b);
 }
 
@@ -150,6 +157,12 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const LnDesc d) {
 void layernorm_launch(const LnDesc& d, hipStream_t s) {
     const int64_t rows = (int64_t)d.nb * d.N;
     dim3 grid((unsigned)((rows + 3) / 4));
+    KScope ks(s);
+    if (ks.on()) {
+        double by = (double)rows * d.C * (4 + (d.out_bf16 ? 2 : 4)) + (d.gn_stats ? (double)rows * d.C * 4 : 0.0);
+        if (d.pos) by += (double)d.N * d.C * 4;
+        ks.begin(d.C == 512 ? "layernorm_kernel<8>" : "layernorm_kernel<6>", 0.0, by);
+    }
     if (d.C == 512) hipLaunchKernelGGL(layernorm_kernel<8>, grid, dim3(256), 0, s, d);
     else hipLaunchKernelGGL(layernorm_kernel<6>, grid, dim3(256), 0, s, d);
 }
@@ -170,6 +183,8 @@ __global__ __launch_bounds__(256) void add_rowvec_kernel(const float* __restrict
 void add_rowvec_launch(const float* X, const float* a, int NI, int P, int64_t ntok, int C, float* U, hipStream_t s) {
     int blocks = (int)((ntok * C + 255) / 256);
     if (blocks > 1024) blocks = 1024;
+    KScope ks(s);
+    if (ks.on()) ks.begin("add_rowvec_kernel", 0.0, (double)(NI / P + NI) * ntok * C * 4);
     hipLaunchKernelGGL(add_rowvec_kernel, dim3(blocks, NI), dim3(256), 0, s, X, a, P, ntok, C, U);
 }
 
@@ -207,6 +222,8 @@ __global__ __launch_bounds__(256) void text_vec_kernel(const float* __restrict__
 
 void text_vec_launch(const float* text, int NI, int P, int text_per_item, const float* wv, const float* bv,
                      const float* wiv, const float* biv, const float* wo, const float* bo, float* a, hipStream_t s) {
+    KScope ks(s);
+    if (ks.on()) ks.begin("text_vec_kernel", 2.0 * NI * (512.0 * 512 * 2 + 384.0 * 512), (512.0 * 512 * 2 + 384.0 * 512) * 4);
     hipLaunchKernelGGL(text_vec_kernel, dim3(NI), dim3(256), 0, s, text, P, text_per_item, wv, bv, wiv, biv, wo, bo, a);
 }
 
@@ -340,6 +357,17 @@ void dec_merge_launch(const MergeDesc& d, hipStream_t s) {
     const int64_t n = (int64_t)d.H_out * d.W * (d.proj_w ? 1 : d.C / V);
     int blocks = (int)((n + 255) / 256);
     if (blocks > 4096) blocks = 4096;
+    KScope ks(s);
+    if (ks.on()) {
+        // unique bytes: the source rows the H-resize touches (<= 2 per output row), the skip rows likewise (once per
+        // segment, shared by its P prompt items), the output once
+        const double src_rows = std::min<double>(d.kept ? d.H_src / 2 : d.H_src, 2.0 * d.H_out);
+        const double skip_rows = std::min<double>(d.H_skip, 2.0 * d.H_out);
+        const double by = (double)d.NI * src_rows * d.W * d.C * (d.src_bf16 ? 2 : 4) +
+                          (double)(d.NI / d.P) * skip_rows * d.W * d.C_skip * 4 +
+                          (double)d.NI * d.H_out * d.W * (d.proj_w ? 2 * 4 : d.C * (d.out_bf16 ? 2 : 4));
+        ks.begin(d.proj_w ? "dec_merge_proj_kernel" : (V == 8 ? "dec_merge_kernel<8>" : "dec_merge_kernel<4>"), 0.0, by);
+    }
     if (d.proj_w) hipLaunchKernelGGL(dec_merge_proj_kernel, dim3(blocks, d.NI), dim3(256), 0, s, d);
     else if (V == 8) hipLaunchKernelGGL(dec_merge_kernel<8>, dim3(blocks, d.NI), dim3(256), 0, s, d);
     else hipLaunchKernelGGL(dec_merge_kernel<4>, dim3(blocks, d.NI), dim3(256), 0, s, d);

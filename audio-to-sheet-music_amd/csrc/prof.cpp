@@ -1,0 +1,60 @@
+#include "prof.h"
+
+#include <map>
+
+namespace athd {
+
+thread_local KProf* t_kprof = nullptr;
+
+void KScope::begin(const std::string& label, double flops, double bytes) {
+    KProf* p = t_kprof;
+    if (!p || (!p->only.empty() && p->only != label)) return;
+    hipEvent_t ev[2];
+    for (auto& e : ev) {
+        if (!p->pool.empty()) {
+            e = p->pool.back();
+            p->pool.pop_back();
+        } else if (hipEventCreate(&e) != hipSuccess) {
+            return;
+        }
+    }
+    if (hipEventRecord(ev[0], s_) != hipSuccess) return;
+    idx_ = (int)p->recs.size();
+    p->recs.push_back({label, ev[0], ev[1], flops, bytes});
+}
+
+KScope::~KScope() {
+    if (idx_ >= 0 && t_kprof) (void)hipEventRecord(t_kprof->recs[idx_].b, s_);
+}
+
+int KProf::collect() {
+    std::map<std::string, size_t> at;
+    for (size_t i = 0; i < agg.size(); ++i) at[agg[i].label] = i;
+    int rc = 0;
+    for (auto& r : recs) {
+        float ms = 0.f;
+        if (hipEventSynchronize(r.b) != hipSuccess || hipEventElapsedTime(&ms, r.a, r.b) != hipSuccess) rc = -1;
+        auto it = at.find(r.label);
+        if (it == at.end()) {
+            at[r.label] = agg.size();
+            agg.push_back({r.label, 0, 0.0, 0.0, 0.0});
+            it = at.find(r.label);
+        }
+        Agg& g = agg[it->second];
+        g.n += 1;
+        g.ms += ms;
+        g.flops += r.flops;
+        g.bytes += r.bytes;
+        pool.push_back(r.a);
+        pool.push_back(r.b);
+    }
+    recs.clear();
+    return rc;
+}
+
+KProf::~KProf() {
+    for (auto& r : recs) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
+    for (auto e : pool) (void)hipEventDestroy(e);
+}
+
+}  // namespace athd

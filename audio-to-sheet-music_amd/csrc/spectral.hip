@@ -15,6 +15,7 @@
 // divides by the window envelope of ALL le+4 frames (torch.istft), and adds the denormalised time branch after
 // its 1x1 output conv (ATHTDemucs_v2.py:314-324).
 #include "common.h"
+#include "prof.h"
 #include "kernels.h"
 
 namespace athd {
@@ -100,6 +101,8 @@ __global__ __launch_bounds__(256) void stft_kernel(const float* __restrict__ wav
 
 void stft_launch(const float* wav, int nb, int64_t T, const PadPlan& pp, int Tspec, const float2* tw,
                  const float* win, float* spec, hipStream_t s) {
+    KScope ks(s);
+    if (ks.on()) ks.begin("stft_kernel", 0.0, (double)nb * 2 * T * 4 + (double)nb * 2048 * Tspec * 4 * 4);
     hipLaunchKernelGGL(stft_kernel, dim3(Tspec, nb), dim3(256), 0, s, wav, T, pp, Tspec, tw, win, spec);
 }
 
@@ -152,6 +155,10 @@ __global__ __launch_bounds__(256) void istft_frames_kernel(const float* __restri
 
 void istft_frames_launch(const float* fo, int NI, int Tspec, int P, const float* spec, const float2* tw,
                          const float* win, float* frames, hipStream_t s) {
+    KScope ks(s);
+    if (ks.on())
+        ks.begin("istft_frames_kernel", 0.0, (double)NI * Tspec * Tspec * 2 * 4 + (double)(NI / P) * 2048 * Tspec * 4 * 4 +
+                                                 (double)NI * Tspec * 2 * 4096 * 4);
     hipLaunchKernelGGL(istft_frames_kernel, dim3(Tspec, NI), dim3(256), 0, s, fo, Tspec, P, spec, tw, win, frames);
 }
 
@@ -195,6 +202,9 @@ __global__ __launch_bounds__(256) void combine_kernel(const float* __restrict__ 
 void combine_launch(const float* frames, int NI, int Tspec, int64_t T, const float* win2, const float* xt3,
                     const float* tw_out, const float* tb_out, const float* tnorm, int P, float* out, hipStream_t s) {
     dim3 grid((unsigned)((T + 255) / 256), NI);
+    KScope ks(s);
+    if (ks.on())
+        ks.begin("combine_kernel", 0.0, (double)NI * Tspec * 2 * 4096 * 4 + (double)NI * T * 4 * 4 + (double)NI * 2 * T * 4);
     hipLaunchKernelGGL(combine_kernel, grid, dim3(256), 0, s, frames, Tspec, T, win2, xt3, tw_out, tb_out, tnorm, P, out);
 }
 

@@ -27,6 +27,22 @@ STEMS = ["drums", "bass", "other", "vocals"]
 ENC_GMAC, DEC_GMAC = 87.03, 10.31
 BF16_PEAK_TFLOPS = 2500.0     # MI355X dense bf16 MFMA (MI355X_MICROARCH.md chip table)
 F32_PEAK_TFLOPS = 157.3
+HBM_PEAK_GBS = 8000.0
+MFMA_KERNELS = ("gemm", "attn")   # kernel-name prefixes priced against the MFMA peak; the rest against HBM
+PMC_FILE = os.environ.get("ATHD_PMC_TRAFFIC", os.path.join(REPO, "profiles", "pmc_traffic.json"))
+
+
+def pmc_traffic(kernel, batch, dtype):
+    """HBM bytes per launch of `kernel` measured by tools/pmc_traffic.py (rocprofv3 FETCH_SIZE / WRITE_SIZE in
+    separate passes, FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM) for this build and workload, else None."""
+    try:
+        d = json.load(open(PMC_FILE))
+    except (OSError, ValueError):
+        return None, None
+    if d.get("batch") != batch or d.get("dtype") != dtype:
+        return None, None
+    k = d.get("kernels", {}).get(kernel)
+    return (k["hbm_bytes_per_launch"], os.path.relpath(PMC_FILE, REPO)) if k else (None, None)
 
 
 def cpu_baseline(sd, table, budget_s=15.0):
@@ -61,6 +77,7 @@ def main():
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--kernel", default=None, help="roofline kernel (default: largest summed time in warmup)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -89,9 +106,20 @@ def main():
     def step():
         return model.forward_prompts(wav, STEMS)
 
-    for _ in range(args.warmup):
+    # warmup; the last warmup step times every kernel (HIP events) to find the dominant one
+    for i in range(args.warmup):
+        if i == args.warmup - 1:
+            model.profile_start(None)
         step()
     torch.cuda.synchronize()
+    dominant = args.kernel
+    if args.warmup > 0:
+        allk = model.profile_stop()
+        if dominant is None:
+            dominant = max(allk, key=lambda r: r["ms"])["kernel"]
+    if dominant is None:
+        dominant = "gemm3_kernel<256,192,4,2,2,200>"
+    model.profile_start(dominant)
 
     def barrier():
         if world > 1:
@@ -105,6 +133,7 @@ def main():
     torch.cuda.synchronize()
     barrier()
     el = time.perf_counter() - t0
+    prof = model.profile_stop()
     if world > 1:
         t = torch.tensor([el], device=dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
@@ -112,8 +141,28 @@ def main():
     ms = el / args.steps * 1e3
     value = B * world * args.steps / el
     flops_step = 2e9 * (ENC_GMAC + 4 * DEC_GMAC) * B
-    ach = flops_step / (ms * 1e-3) / 1e12
-    peak = BF16_PEAK_TFLOPS if args.dtype == "bf16" else F32_PEAK_TFLOPS
+    step_tf = flops_step / (ms * 1e-3) / 1e12
+    kp = next((r for r in prof if r["kernel"] == dominant), None)
+    if kp is None or kp["launches"] == 0:
+        raise RuntimeError(f"roofline kernel {dominant!r} was not launched in the timed region")
+    per_launch_ms = kp["ms"] / kp["launches"]
+    if dominant.startswith(MFMA_KERNELS):
+        peak = BF16_PEAK_TFLOPS if args.dtype == "bf16" else F32_PEAK_TFLOPS
+        ach = kp["flops"] / (kp["ms"] * 1e-3) / 1e12
+        bound, unit = "mfma", "TFLOP/s"
+    else:
+        peak, bound, unit = HBM_PEAK_GBS, "hbm", "GB/s"
+        ach = kp["bytes"] / (kp["ms"] * 1e-3) / 1e9
+    traffic, traffic_src = pmc_traffic(dominant, B, args.dtype)
+    roofline = {"bound": bound, "achieved": round(ach, 2), "peak": peak, "unit": unit, "frac": round(ach / peak, 4),
+                "traffic": traffic, "kernel": dominant, "launches_per_step": kp["launches"] / args.steps,
+                "avg_launch_us": round(per_launch_ms * 1e3, 2),
+                "share_of_step": round(kp["ms"] / args.steps / ms, 4),
+                "algorithmic_per_launch": {"flops": kp["flops"] / kp["launches"],
+                                           "bytes": kp["bytes"] / kp["launches"]},
+                "timing": "HIP events on the launch stream around every launch of the kernel in the timed region"}
+    if traffic_src:
+        roofline["traffic_source"] = traffic_src
     rec = {
         "metric": "6s-segments/sec (each separated into 4 stems; encode once, decode 4x)",
         "value": round(value, 3),
@@ -130,11 +179,10 @@ def main():
         "config": {"workload": "BASELINE configs[2]: B=64 x 6 s segments x 4 prompts per GPU", "global_batch": B * world,
                    "seq_len": SEG, "prompts": 4, "parallelism": f"segment-sharded dp{world}"},
         "stems_per_s": round(4 * value, 3),
-        "roofline": {"bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
-                     "frac": round(ach / peak, 4), "traffic": None,
-                     "basis": "whole step, essential FLOPs (SURVEY §8(d)) / step time"},
+        "roofline": roofline,
+        "step_essential_tflops": round(step_tf, 2),
     }
-    if rank == 0 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
         rec["cpu_baseline"] = cpu_baseline(sd, table)
     if rank == 0:
         print(json.dumps(rec), flush=True)

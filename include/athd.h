@@ -73,6 +73,17 @@ int athd_forward(athd_ctx* ctx, const float* wav, int64_t B, int64_t T, const fl
 int athd_forward_prompts(athd_ctx* ctx, const float* wav, int64_t B, int64_t T, const float* text_table, int P,
                          float* out, void* workspace, size_t workspace_bytes, void* stream);
 
+/* Kernel timing (measurement aid for bench.py; not part of the reference interface).  Between
+ * athd_profile_start and athd_profile_stop every launch of kernel `kernel` (its rocprofv3 symbol without
+ * "void athd::", the argument list and 'u' suffixes, e.g. "attn_bf16_kernel"; NULL or "" = all kernels) made
+ * by this context's forwards is bracketed by HIP events on the launch stream.  athd_profile_stop synchronises
+ * those events and aggregates per kernel: launches, summed event time, summed ALGORITHMIC flops and bytes. */
+int athd_profile_start(athd_ctx* ctx, const char* kernel);
+int athd_profile_stop(athd_ctx* ctx);
+int athd_profile_count(athd_ctx* ctx);
+int athd_profile_get(athd_ctx* ctx, int i, const char** kernel, long long* launches, double* ms, double* flops,
+                     double* bytes);
+
 /* Last error message of this context ("" if none). */
 const char* athd_last_error(athd_ctx* ctx);
 

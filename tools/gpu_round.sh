@@ -1,0 +1,26 @@
+#!/bin/bash
+# Full GPU pass: parity tests, bench (with CPU baseline), kernel-trace profile at the bench config, HBM traffic from
+# two PMC passes, and a final bench line carrying the measured traffic.  Usage: tools/gpu_round.sh <tag>
+TAG=${1:-r01}
+O=gpurun_out
+mkdir -p $O
+export TMPDIR=/tmp
+step() { echo "== $1"; }
+step pytest
+timeout -k 10 900 python -m pytest tests -m gpu -q -rA -p no:cacheprovider > $O/pytest_gpu.log 2>&1
+rc=$?; grep -E "passed|failed" $O/pytest_gpu.log | tail -2
+if [ $rc -gt 1 ]; then tail -30 $O/pytest_gpu.log; exit $rc; fi
+step bench
+timeout -k 10 600 python bench.py > $O/bench_full.log 2>&1 || { tail -20 $O/bench_full.log; exit 1; }
+tail -1 $O/bench_full.log
+step kernel-trace
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$TAG -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline > $O/prof_$TAG.log 2>&1 || { tail -20 $O/prof_$TAG.log; exit 1; }
+tail -1 $O/prof_$TAG.log
+step pmc-fetch
+timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch_$TAG -o run -- python bench.py --steps 1 --warmup 1 --no-cpu-baseline > $O/pmc_fetch_$TAG.log 2>&1 || { tail -20 $O/pmc_fetch_$TAG.log; exit 1; }
+step pmc-write
+timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write_$TAG -o run -- python bench.py --steps 1 --warmup 1 --no-cpu-baseline > $O/pmc_write_$TAG.log 2>&1 || { tail -20 $O/pmc_write_$TAG.log; exit 1; }
+python tools/pmc_traffic.py $O/pmc_fetch_$TAG $O/pmc_write_$TAG --batch 64 --dtype bf16 -o $O/pmc_traffic.json || exit 1
+step bench-with-traffic
+ATHD_PMC_TRAFFIC=$O/pmc_traffic.json timeout -k 10 600 python bench.py --no-cpu-baseline > $O/bench_traffic.log 2>&1 || { tail -20 $O/bench_traffic.log; exit 1; }
+tail -1 $O/bench_traffic.log
