@@ -1,0 +1,168 @@
+"""Track-level surface of the reference around the hot path.
+
+Mirrors `test_inference.py`:
+  * `load_model`       <- `test_inference.py:21-40`
+  * `window_plan`      <- the window arithmetic of `test_inference.py:96-141`
+  * `separate_track`   <- the per-stem chunk loop `test_inference.py:92-141`, batched: all full windows of the track
+                          go through `forward_prompts` (encode once, decode once per stem), the fades and the
+                          additive overlap-add run in `athd_overlap_add` (same fp32 additions, same order)
+  * `sdr_loss`         <- `src/loss.py:9-30` (device reduction, fp64 sums); `test_inference.py:153` uses -sdr_loss
+  * `test_inference`   <- `test_inference.py:43-155` minus the MUSDB decode / wav writing / plotting
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import native
+from .model import AudioTextHTDemucs
+from .weights import STEMS
+
+
+def load_model(checkpoint_path: str, device: str = "cuda", dtype: str = "bf16",
+               text_table: Optional[Dict[str, np.ndarray]] = None, clap=None, tokenizer=None) -> AudioTextHTDemucs:
+    """`test_inference.py:21-40`.  The checkpoint is read with `torch.load(weights_only=True)` (no unpickling of
+    code); `checkpoint["model_state_dict"]` is loaded non-strictly.  The pretrained htdemucs object of the reference
+    is not needed: every `htdemucs.*` key the hot path uses is in the checkpoint, as the reference's own
+    `load_state_dict` overwrites the pretrained values with them.  Prompt embeddings: `text_table` or `clap`/`tokenizer`
+    (see athd/text.py)."""
+    ckpt = torch.load(checkpoint_path, map_location="cpu", weights_only=True)
+    sd = ckpt["model_state_dict"] if isinstance(ckpt, dict) and "model_state_dict" in ckpt else ckpt
+    model = AudioTextHTDemucs(None, clap, tokenizer, dtype=dtype, text_table=text_table)
+    model.load_state_dict(sd, strict=False)
+    model = model.to(device)
+    model.eval()
+    return model
+
+
+@dataclass(frozen=True)
+class Window:
+    start: int
+    end: int
+    fade_in: int
+    fade_out: int
+
+
+def window_plan(length: int, sample_rate: int = 44100, segment_seconds: float = 6.0,
+                overlap: float = 0.1) -> List[Window]:
+    """Windows of `test_inference.py:96-141` in loop order.  Raises like the reference when a window is shorter
+    than its fade (torchaudio's Fade then asks for a negative-size `torch.ones`)."""
+    chunk_len = int(sample_rate * segment_seconds)
+    overlap_frames = int(overlap * sample_rate)
+    if chunk_len <= overlap_frames:
+        raise ValueError("segment must be longer than the overlap")
+    plan = []
+    start = 0
+    while start < length:
+        end = min(start + chunk_len, length)
+        fade_in = 0 if start == 0 else overlap_frames
+        fade_out = overlap_frames if end < length else 0
+        if end - start < max(fade_in, fade_out):
+            raise RuntimeError(f"window [{start}, {end}) is shorter than its fade ({max(fade_in, fade_out)} samples):"
+                               f" the reference's torchaudio Fade fails here (negative dimension)")
+        plan.append(Window(start, end, fade_in, fade_out))
+        start += chunk_len - overlap_frames
+    n_native = native.lib.athd_num_windows(length, chunk_len, overlap_frames)
+    if n_native != len(plan):
+        raise AssertionError(f"window count mismatch: host {len(plan)}, library {n_native}")
+    return plan
+
+
+def _stream(dev: torch.device) -> int:
+    return torch.cuda.current_stream(dev).cuda_stream
+
+
+def overlap_add(windows: torch.Tensor, length: int, chunk_len: int, overlap_frames: int, k0: int = 0,
+                k1: Optional[int] = None) -> torch.Tensor:
+    """Fade + additive overlap-add of window outputs `windows` (k1-k0, S, 2, chunk_len) into the track span of
+    windows [k0, k1) (the whole track by default) -> (S, 2, span) on the same device (athd_overlap_add)."""
+    n = native.lib.athd_num_windows(length, chunk_len, overlap_frames)
+    k1 = n if k1 is None else k1
+    S = windows.shape[1]
+    if windows.dim() != 4 or windows.shape[0] != k1 - k0 or windows.shape[2] != 2 or windows.shape[3] != chunk_len:
+        raise ValueError(f"windows must be ({k1 - k0}, S, 2, {chunk_len}), got {tuple(windows.shape)}")
+    if windows.dtype != torch.float32 or not windows.is_contiguous() or windows.device.type != "cuda":
+        raise ValueError("windows must be a contiguous float32 device tensor")
+    hop = chunk_len - overlap_frames
+    span = min((k1 - 1) * hop + chunk_len, length) - k0 * hop
+    out = torch.empty((S, 2, span), dtype=torch.float32, device=windows.device)
+    rc = native.lib.athd_overlap_add(windows.data_ptr(), length, chunk_len, overlap_frames, S, k0, k1, out.data_ptr(),
+                                     _stream(windows.device))
+    if rc != 0:
+        raise native.AthdError(f"athd_overlap_add failed ({rc})")
+    return out
+
+
+@torch.no_grad()
+def run_windows(model: AudioTextHTDemucs, mixture: torch.Tensor, plan: Sequence[Window], stems: Sequence[str],
+                chunk_len: int, k0: int = 0, k1: Optional[int] = None, max_batch: int = 64) -> torch.Tensor:
+    """Model outputs of windows [k0, k1) of `plan` for every stem -> (k1-k0, S, 2, chunk_len); full windows are
+    batched `max_batch` at a time (encode once, decode once per stem), a short last window runs on its own."""
+    k1 = len(plan) if k1 is None else k1
+    dev = mixture.device
+    S = len(stems)
+    win = torch.zeros((k1 - k0, S, 2, chunk_len), dtype=torch.float32, device=dev)
+    full = [k for k in range(k0, k1) if plan[k].end - plan[k].start == chunk_len]
+    if full and full != list(range(k0, k0 + len(full))):
+        raise AssertionError("full windows must form a prefix of the plan")
+    for b0 in range(0, len(full), max_batch):
+        ks = full[b0:b0 + max_batch]
+        batch = torch.stack([mixture[:, plan[k].start:plan[k].end] for k in ks]).contiguous()
+        model.forward_prompts(batch, list(stems), out=win[ks[0] - k0:ks[-1] - k0 + 1])
+    for k in range(k0 + len(full), k1):
+        w = plan[k]
+        o = model.forward_prompts(mixture[:, w.start:w.end].unsqueeze(0).contiguous(), list(stems))
+        win[k - k0, :, :, :w.end - w.start] = o[0]
+    return win
+
+
+@torch.no_grad()
+def separate_track(model: AudioTextHTDemucs, mixture: torch.Tensor, stems: Sequence[str] = STEMS,
+                   sample_rate: int = 44100, segment_seconds: float = 6.0, overlap: float = 0.1,
+                   max_batch: int = 64) -> torch.Tensor:
+    """`test_inference.py:91-141`: mixture (2, L) (or (1, 2, L)) on the model's device -> final (S, 2, L)."""
+    if mixture.dim() == 3:
+        mixture = mixture[0]
+    if mixture.dim() != 2 or mixture.shape[0] != 2:
+        raise ValueError(f"expected a (2, L) stereo mixture, got {tuple(mixture.shape)}")
+    mixture = mixture.float().contiguous()
+    length = mixture.shape[-1]
+    chunk_len = int(sample_rate * segment_seconds)
+    overlap_frames = int(overlap * sample_rate)
+    plan = window_plan(length, sample_rate, segment_seconds, overlap)
+    win = run_windows(model, mixture, plan, stems, chunk_len, max_batch=max_batch)
+    return overlap_add(win, length, chunk_len, overlap_frames)
+
+
+def sdr_loss(estimated: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
+    """`src/loss.py:9-30`: -mean over rows (dim 0) of clamp(10 log10((|t|^2 + 1e-8) / (|t - e|^2 + 1e-8)), -30, 30);
+    a device scalar.  Sums are accumulated in fp64 on the device (athd_sdr)."""
+    if estimated.shape[0] != target.shape[0] or estimated.numel() != target.numel():
+        raise ValueError("estimated and target must have the same rows and size")
+    rows = estimated.shape[0]
+    est = estimated.reshape(rows, -1).float().contiguous()
+    tgt = target.reshape(rows, -1).float().contiguous()
+    scratch = torch.empty(2 * rows, dtype=torch.float64, device=est.device)
+    out = torch.empty(1, dtype=torch.float32, device=est.device)
+    rc = native.lib.athd_sdr(est.data_ptr(), tgt.data_ptr(), rows, est.shape[1], scratch.data_ptr(), out.data_ptr(),
+                             _stream(est.device))
+    if rc != 0:
+        raise native.AthdError(f"athd_sdr failed ({rc})")
+    return -out[0]
+
+
+@torch.no_grad()
+def test_inference(model: AudioTextHTDemucs, mixture: torch.Tensor, references: Optional[torch.Tensor] = None,
+                   stems: Sequence[str] = STEMS, sample_rate: int = 44100, segment_seconds: float = 6.0,
+                   overlap: float = 0.1):
+    """`test_inference.py:43-155` on an in-memory track: mixture (2, L); references (S, 2, L) true stems (optional).
+    Returns (final (S, 2, L), {stem: SDR dB}) with SDR = -sdr_loss(estimate, reference) per stem (`:147-155`)."""
+    final = separate_track(model, mixture, stems, sample_rate, segment_seconds, overlap)
+    scores = {s: -30.0 for s in stems}
+    if references is not None:
+        for i, s in enumerate(stems[:4]):
+            scores[s] = float(-sdr_loss(final[i], references[i]).item())
+    return final, scores

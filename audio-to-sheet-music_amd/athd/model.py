@@ -152,14 +152,18 @@ class AudioTextHTDemucs:
     __call__ = forward
 
     @torch.no_grad()
-    def forward_prompts(self, wav: torch.Tensor, prompts: List[str]) -> torch.Tensor:
-        """Encode once, decode once per prompt: (B,2,T) -> (B,P,2,T)."""
+    def forward_prompts(self, wav: torch.Tensor, prompts: List[str], out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Encode once, decode once per prompt: (B,2,T) -> (B,P,2,T) (written into `out` when given)."""
         wav = self._check_wav(wav)
         B, _, T = wav.shape
         ctx = self._ensure_ctx()
         table = self.embedder.rows(list(prompts), len(prompts)).to(self.device).contiguous()
         P = table.shape[0]
-        out = torch.empty((B, P, 2, T), dtype=torch.float32, device=self.device)
+        if out is None:
+            out = torch.empty((B, P, 2, T), dtype=torch.float32, device=self.device)
+        elif (tuple(out.shape) != (B, P, 2, T) or out.dtype != torch.float32 or out.device != self.device
+              or not out.is_contiguous()):
+            raise ValueError(f"out must be a contiguous float32 {(B, P, 2, T)} tensor on {self.device}")
         nbytes = ctx.workspace_bytes(B, T, P)
         ws = self._workspace(nbytes)
         stream = torch.cuda.current_stream(self.device).cuda_stream

@@ -34,6 +34,13 @@ lib.athd_forward.restype = _c.c_int
 lib.athd_forward_prompts.argtypes = [_c.c_void_p, _c.c_void_p, _c.c_int64, _c.c_int64, _c.c_void_p, _c.c_int,
                                      _c.c_void_p, _c.c_void_p, _c.c_size_t, _c.c_void_p]
 lib.athd_forward_prompts.restype = _c.c_int
+lib.athd_num_windows.argtypes = [_c.c_int64, _c.c_int64, _c.c_int64]
+lib.athd_num_windows.restype = _c.c_int64
+lib.athd_overlap_add.argtypes = [_c.c_void_p, _c.c_int64, _c.c_int64, _c.c_int64, _c.c_int, _c.c_int64, _c.c_int64,
+                                 _c.c_void_p, _c.c_void_p]
+lib.athd_overlap_add.restype = _c.c_int
+lib.athd_sdr.argtypes = [_c.c_void_p, _c.c_void_p, _c.c_int64, _c.c_int64, _c.c_void_p, _c.c_void_p, _c.c_void_p]
+lib.athd_sdr.restype = _c.c_int
 lib.athd_profile_start.argtypes = [_c.c_void_p, _c.c_char_p]
 lib.athd_profile_start.restype = _c.c_int
 lib.athd_profile_stop.argtypes = [_c.c_void_p]
@@ -49,7 +56,8 @@ lib.athd_destroy.argtypes = [_c.c_void_p]
 lib.athd_destroy.restype = None
 
 EXPORTED = ["athd_version", "athd_create", "athd_set_weight", "athd_num_required_keys", "athd_required_key",
-            "athd_finalize", "athd_workspace_bytes", "athd_forward", "athd_forward_prompts", "athd_profile_start",
+            "athd_finalize", "athd_workspace_bytes", "athd_forward", "athd_forward_prompts", "athd_num_windows",
+            "athd_overlap_add", "athd_sdr", "athd_profile_start",
             "athd_profile_stop", "athd_profile_count", "athd_profile_get", "athd_last_error", "athd_destroy"]
 
 F32, BF16 = 0, 1

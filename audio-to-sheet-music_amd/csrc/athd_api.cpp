@@ -347,6 +347,24 @@ int athd_finalize(athd_ctx* c) {
     return ATHD_OK;
 }
 
+int64_t athd_num_windows(int64_t length, int64_t chunk_len, int64_t overlap) {
+    if (length <= 0 || chunk_len <= 0 || overlap < 0 || overlap >= chunk_len) return 0;
+    const int64_t hop = chunk_len - overlap;
+    return (length + hop - 1) / hop;
+}
+
+int athd_overlap_add(const float* windows, int64_t length, int64_t chunk_len, int64_t overlap, int n_stems,
+                     int64_t k0, int64_t k1, float* out, void* stream) {
+    const int rc = ola_launch(windows, length, chunk_len, overlap, n_stems, k0, k1, out, (hipStream_t)stream);
+    return rc == 0 ? ATHD_OK : (rc == -1 ? ATHD_EINVAL : ATHD_EHIP);
+}
+
+int athd_sdr(const float* est, const float* target, int64_t rows, int64_t n, double* scratch, float* out,
+             void* stream) {
+    const int rc = sdr_launch(est, target, rows, n, scratch, out, (hipStream_t)stream);
+    return rc == 0 ? ATHD_OK : (rc == -1 ? ATHD_EINVAL : ATHD_EHIP);
+}
+
 int athd_profile_start(athd_ctx* c, const char* kernel) {
     if (!c) return ATHD_EINVAL;
     delete c->prof;

@@ -68,4 +68,9 @@ int dconv_small_launch(float* x, float* h, int64_t nb, int64_t L, int C, int dil
 void pos2d_launch(float* out, int Fr, int T1, int C, hipStream_t s);   // out[(f*T1+t)][C]
 void pos1d_launch(float* out, int T2, int C, hipStream_t s);           // out[t][C]
 
+// track.hip: window overlap-add of test_inference.py:92-141 and sdr_loss (src/loss.py:9-30)
+int ola_launch(const float* win, int64_t L, int64_t chunk, int64_t overlap, int S, int64_t k0, int64_t k1, float* out,
+               hipStream_t s);
+int sdr_launch(const float* est, const float* tgt, int64_t rows, int64_t n, double* sums, float* out, hipStream_t s);
+
 }  // namespace athd

@@ -73,6 +73,25 @@ int athd_forward(athd_ctx* ctx, const float* wav, int64_t B, int64_t T, const fl
 int athd_forward_prompts(athd_ctx* ctx, const float* wav, int64_t B, int64_t T, const float* text_table, int P,
                          float* out, void* workspace, size_t workspace_bytes, void* stream);
 
+/* ---- Track level: the window loop of test_inference.py:92-141 and sdr_loss (src/loss.py:9-30) ----
+ * Windows: start_k = k*hop with hop = chunk_len - overlap, for k = 0 .. athd_num_windows()-1 (while start < length),
+ * end_k = min(start_k + chunk_len, length).  Window k is faded by torchaudio Fade(fade_in = k ? overlap : 0,
+ * fade_out = end_k < length ? overlap : 0, 'linear') and summed into the track in ascending k.  (The reference
+ * fails when a window is shorter than its fade; callers check that with the plan.) */
+int64_t athd_num_windows(int64_t length, int64_t chunk_len, int64_t overlap);
+
+/* windows: device (k1-k0, n_stems, 2, chunk_len) f32, row k-k0 = model output of window k in its first
+ * end_k - start_k samples.  out: device (n_stems, 2, end_{k1-1} - start_{k0}) f32, the track span of windows
+ * [k0, k1) (the whole track for k0 = 0, k1 = athd_num_windows()).  Enqueued on `stream`. */
+int athd_overlap_add(const float* windows, int64_t length, int64_t chunk_len, int64_t overlap, int n_stems,
+                     int64_t k0, int64_t k1, float* out, void* stream);
+
+/* SDR of src/loss.py:9-30 with the sign of test_inference.py:153: est/target device (rows, n) f32 ->
+ * *out (device f32) = mean over rows of clamp(10 log10((sum t^2 + 1e-8) / (sum (t-e)^2 + 1e-8)), -30, 30).
+ * scratch: device, 2*rows doubles.  Sums are accumulated in fp64. */
+int athd_sdr(const float* est, const float* target, int64_t rows, int64_t n, double* scratch, float* out,
+             void* stream);
+
 /* Kernel timing (measurement aid for bench.py; not part of the reference interface).  Between
  * athd_profile_start and athd_profile_stop every launch of kernel `kernel` (its rocprofv3 symbol without
  * "void athd::", the argument list and 'u' suffixes, e.g. "attn_bf16_kernel"; NULL or "" = all kernels) made
