@@ -1,18 +1,29 @@
-// DConv (demucs residual dilated-conv branch) for narrow levels (C = 48, 96; hidden
-// H = C/8 = 6, 12) on gfx950.  These layers are HBM-bound with K or N far below an MFMA tile, so they run as
-// VALU kernels, one thread per position, weights staged in LDS (broadcast reads):
-//   c3:     h[p][j] = b[j] + sum_{tap,c} W[j][tap*C+c] x[p+(tap-1)dil][c]     + GroupNorm stats of h per group
-//   c1stat: y[p][n] = b[n] + sum_j W[n][j] h[p][j]  (2C outputs)               -> GroupNorm stats of y per group
-//   c1app:  x[p][c] += scale[c] * GLU(GN(y))[c]                                 (recomputes y: K = H is tiny)
-// A "group" is the GroupNorm(1) sample: nb index of [nb][L][C] (freq rows (b,f) along time, or time samples).
+// DConv (demucs residual dilated-conv branch) for the narrow levels (C = 48, 96; hidden
+// H = C/8 = 6, 12).  These layers are HBM-bound with K or N far below an MFMA tile, so they run as VALU kernels.
+// x is [nb][L][C] in f32 (parity mode) or bf16 (throughput mode); h is [nb][L][H] f32.  One layer = 3 passes
+// (each GroupNorm needs complete statistics before it can be applied):
+//   c3:     h = b + W3 * x[t - dil], x[t], x[t + dil]          + GroupNorm statistics of h per group
+//   c1stat: y = b1 + W1 * GELU(GN(h))   (2C outputs, never stored)  -> GroupNorm statistics of y per group
+//   c1app:  x += scale * GLU(GN(y))     (y recomputed: K = H is tiny)
+// A "group" is the GroupNorm(1) sample: one nb row of L positions (freq rows (b,f) along time, or time samples).
+// Access pattern: c3 stages its x tile (+ dilation halo) in LDS with 16-B coalesced loads; c1app maps a lane to
+// (position, 8-channel chunk) so x is read and written with consecutive 16-B (bf16) / 32-B (f32) chunks.
 #include "common.h"
 #include "prof.h"
 #include "kernels.h"
 
 namespace athd {
 
-// Block-level {sum, sumsq} per group: blocks cover 256 consecutive positions, so with L >= 256 a block spans at
-// most two groups (first group g0 of the block and g0 + 1).  Shorter rows fall back to per-thread atomics.
+template <typename TS> struct XS;
+template <> struct XS<float> {
+    static ATHD_DEV float ld(const float* p, int64_t i) { return p[i]; }
+};
+template <> struct XS<bf16_t> {
+    static ATHD_DEV float ld(const bf16_t* p, int64_t i) { return bf2f(p[i]); }
+};
+
+// Block-level {sum, sumsq} per group.  Blocks cover <= 256 consecutive positions, so with L >= 256 a block spans
+// at most two groups (g0 and g0 + 1).  Shorter rows fall back to per-thread atomics.
 ATHD_DEV void group_stats_add(double* __restrict__ st, int64_t p0, int64_t p, bool valid, int64_t L, float s1, float s2,
                               double* sh) {
     if (L < 256) {
@@ -38,43 +49,63 @@ ATHD_DEV void group_stats_add(double* __restrict__ st, int64_t p0, int64_t p, bo
     }
 }
 
-template <int C>
-__global__ __launch_bounds__(256) void dconv_c3_kernel(const float* __restrict__ x, int64_t nb, int64_t L, int dil,
+ATHD_DEV void gn_mr(const double* st, int64_t g, double cnt, float& mean, float& rstd) {
+    const double mm = st[2 * g] / cnt;
+    double var = st[2 * g + 1] / cnt - mm * mm;
+    if (var < 0) var = 0;
+    mean = (float)mm;
+    rstd = (float)(1.0 / sqrt(var + 1e-5));
+}
+
+// ---- c3: TILE positions per block, TPP = 256 / TILE threads per position, each computing H / TPP outputs
+template <int C, typename TS>
+__global__ __launch_bounds__(256) void dconv_c3_kernel(const TS* __restrict__ x, int64_t nb, int64_t L, int dil,
                                                        const float* __restrict__ W, const float* __restrict__ bias,
                                                        float* __restrict__ h, double* __restrict__ st) {
-    constexpr int H = C / 8, K = 3 * C;
+    constexpr int H = C / 8, K = 3 * C, HALO = 2;
+    constexpr int TILE = sizeof(TS) == 2 ? 256 : 128;
+    constexpr int TPP = 256 / TILE, HJ = H / TPP;
+    constexpr int ROWS = TILE + 2 * HALO;
+    constexpr int EPC = 16 / sizeof(TS);                    // elements per 16-B chunk
+    constexpr int CPR = C / EPC;                             // chunks per row
+    __shared__ __attribute__((aligned(16))) TS xs[ROWS * C];
     __shared__ float wl[H * K];
     __shared__ double sh[16];
-    for (int i = threadIdx.x; i < H * K; i += 256) wl[i] = W[i];
-    __syncthreads();
     const int64_t P = nb * L;
-    const int64_t p0 = (int64_t)blockIdx.x * 256;
-    const int64_t p = p0 + threadIdx.x;
+    const int64_t p0 = (int64_t)blockIdx.x * TILE;
+    for (int i = threadIdx.x; i < H * K; i += 256) wl[i] = W[i];
+    for (int i = threadIdx.x; i < ROWS * CPR; i += 256) {
+        const int r = i / CPR, ch = i - r * CPR;
+        const int64_t pp = p0 - HALO + r;
+        uint4 v = make_uint4(0u, 0u, 0u, 0u);
+        if (pp >= 0 && pp < P) v = *reinterpret_cast<const uint4*>(x + pp * C + ch * EPC);
+        *reinterpret_cast<uint4*>(&xs[r * C + ch * EPC]) = v;
+    }
+    __syncthreads();
+    const int lp = threadIdx.x / TPP, sub = threadIdx.x % TPP;
+    const int64_t p = p0 + lp;
     const bool valid = p < P;
     float s1 = 0.f, s2 = 0.f;
     if (valid) {
-        const int64_t g = p / L, t = p - g * L;
-        float acc[H];
+        const int64_t t = p % L;
+        float acc[HJ];
 #pragma unroll
-        for (int j = 0; j < H; ++j) acc[j] = bias[j];
+        for (int j = 0; j < HJ; ++j) acc[j] = bias[sub * HJ + j];
 #pragma unroll
         for (int tap = 0; tap < 3; ++tap) {
             const int64_t tt = t + (tap - 1) * dil;
-            if (tt < 0 || tt >= L) continue;
-            const float4* xr = reinterpret_cast<const float4*>(x + (g * L + tt) * C);
+            if (tt < 0 || tt >= L) continue;                 // zero padding of the group row
+            const TS* xr = &xs[(lp + HALO + (tap - 1) * dil) * C];
 #pragma unroll 4
-            for (int c4 = 0; c4 < C / 4; ++c4) {
-                const float4 v = xr[c4];
+            for (int c = 0; c < C; ++c) {
+                const float v = XS<TS>::ld(xr, c);
 #pragma unroll
-                for (int j = 0; j < H; ++j) {
-                    const float* wr = &wl[j * K + tap * C + 4 * c4];
-                    acc[j] += wr[0] * v.x + wr[1] * v.y + wr[2] * v.z + wr[3] * v.w;
-                }
+                for (int j = 0; j < HJ; ++j) acc[j] += wl[(sub * HJ + j) * K + tap * C + c] * v;
             }
         }
-        float* hr = h + p * H;
+        float* hr = h + p * H + sub * HJ;
 #pragma unroll
-        for (int j = 0; j < H; ++j) {
+        for (int j = 0; j < HJ; ++j) {
             hr[j] = acc[j];
             s1 += acc[j];
             s2 += acc[j] * acc[j];
@@ -83,104 +114,156 @@ __global__ __launch_bounds__(256) void dconv_c3_kernel(const float* __restrict__
     group_stats_add(st, p0, p, valid, L, s1, s2, sh);
 }
 
-template <int C, bool APPLY>
-__global__ __launch_bounds__(256) void dconv_c1_kernel(float* __restrict__ x, const float* __restrict__ h, int64_t nb,
-                                                       int64_t L, const float* __restrict__ W,
-                                                       const float* __restrict__ bias, double* __restrict__ st,
-                                                       const float* __restrict__ gw, const float* __restrict__ gb,
-                                                       const float* __restrict__ scale) {
+// GELU(GroupNorm(h)) of one position (the first GroupNorm of the layer, fused into both 1x1 passes)
+template <int H, bool FAST>
+ATHD_DEV void load_hg(const float* __restrict__ h, int64_t p, float mean, float rstd, const float* g1w, const float* g1b,
+                      float* hv) {
+#pragma unroll
+    for (int j = 0; j < H; ++j) hv[j] = gelu<FAST>((h[p * H + j] - mean) * rstd * g1w[j] + g1b[j]);
+}
+
+// ---- c1stat: one thread per position; y (2C channels) only feeds the GroupNorm statistics
+template <int C, bool FAST>
+__global__ __launch_bounds__(256) void dconv_c1_stats_kernel(const float* __restrict__ h, int64_t nb, int64_t L,
+                                                             const double* __restrict__ st_h,
+                                                             const float* __restrict__ g1w, const float* __restrict__ g1b,
+                                                             const float* __restrict__ W, const float* __restrict__ bias,
+                                                             double* __restrict__ st_y) {
     constexpr int H = C / 8, N = 2 * C;
     __shared__ float wl[N * H];
-    __shared__ float bl[N], gwl[N], gbl[N], scl[C];
+    __shared__ float bl[N], gw[H], gb[H];
     __shared__ double sh[16];
     for (int i = threadIdx.x; i < N * H; i += 256) wl[i] = W[i];
-    for (int i = threadIdx.x; i < N; i += 256) {
-        bl[i] = bias[i];
-        if (APPLY) { gwl[i] = gw[i]; gbl[i] = gb[i]; }
-    }
-    if (APPLY) for (int i = threadIdx.x; i < C; i += 256) scl[i] = scale[i];
+    for (int i = threadIdx.x; i < N; i += 256) bl[i] = bias[i];
+    if (threadIdx.x < H) { gw[threadIdx.x] = g1w[threadIdx.x]; gb[threadIdx.x] = g1b[threadIdx.x]; }
     __syncthreads();
     const int64_t P = nb * L;
     const int64_t p0 = (int64_t)blockIdx.x * 256;
     const int64_t p = p0 + threadIdx.x;
     const bool valid = p < P;
-    float hv[H];
+    float s1 = 0.f, s2 = 0.f;
     if (valid) {
-#pragma unroll
-        for (int j = 0; j < H; ++j) hv[j] = h[p * H + j];
-    }
-    if (!APPLY) {
-        float s1 = 0.f, s2 = 0.f;
-        if (valid) {
+        float mean, rstd;
+        gn_mr(st_h, p / L, (double)L * H, mean, rstd);
+        float hv[H];
+        load_hg<H, FAST>(h, p, mean, rstd, gw, gb, hv);
 #pragma unroll 4
-            for (int n = 0; n < N; ++n) {
-                float y = bl[n];
+        for (int n = 0; n < N; ++n) {
+            float y = bl[n];
 #pragma unroll
-                for (int j = 0; j < H; ++j) y += wl[n * H + j] * hv[j];
-                s1 += y;
-                s2 += y * y;
-            }
+            for (int j = 0; j < H; ++j) y += wl[n * H + j] * hv[j];
+            s1 += y;
+            s2 += y * y;
         }
-        group_stats_add(st, p0, p, valid, L, s1, s2, sh);
+    }
+    group_stats_add(st_y, p0, p, valid, L, s1, s2, sh);
+}
+
+// ---- c1app: one thread per (position, 8-channel chunk): x[p][c..c+8) += scale * GLU(GN(y))
+template <int C, typename TS, bool FAST>
+__global__ __launch_bounds__(256) void dconv_c1_apply_kernel(TS* __restrict__ x, const float* __restrict__ h, int64_t nb,
+                                                             int64_t L, const double* __restrict__ st_h,
+                                                             const float* __restrict__ g1w, const float* __restrict__ g1b,
+                                                             const float* __restrict__ W, const float* __restrict__ bias,
+                                                             const double* __restrict__ st_y,
+                                                             const float* __restrict__ g2w, const float* __restrict__ g2b,
+                                                             const float* __restrict__ scale) {
+    constexpr int H = C / 8, N = 2 * C, CV = C / 8;
+    __shared__ float wl[N * H];
+    __shared__ float bl[N], gw2[N], gb2[N], scl[C], gw[H], gb[H];
+    for (int i = threadIdx.x; i < N * H; i += 256) wl[i] = W[i];
+    for (int i = threadIdx.x; i < N; i += 256) { bl[i] = bias[i]; gw2[i] = g2w[i]; gb2[i] = g2b[i]; }
+    for (int i = threadIdx.x; i < C; i += 256) scl[i] = scale[i];
+    if (threadIdx.x < H) { gw[threadIdx.x] = g1w[threadIdx.x]; gb[threadIdx.x] = g1b[threadIdx.x]; }
+    __syncthreads();
+    const int64_t P = nb * L;
+    const int64_t gi = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (gi >= P * CV) return;
+    const int64_t p = gi / CV;
+    const int c0 = (int)(gi - p * CV) * 8;
+    const int64_t g = p / L;
+    float m1, r1, m2, r2;
+    gn_mr(st_h, g, (double)L * H, m1, r1);
+    gn_mr(st_y, g, (double)L * N, m2, r2);
+    float hv[H];
+    load_hg<H, FAST>(h, p, m1, r1, gw, gb, hv);
+    float o[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const int c = c0 + q;
+        float a = bl[c], gt = bl[C + c];
+#pragma unroll
+        for (int j = 0; j < H; ++j) {
+            a += wl[c * H + j] * hv[j];
+            gt += wl[(C + c) * H + j] * hv[j];
+        }
+        a = (a - m2) * r2 * gw2[c] + gb2[c];
+        gt = (gt - m2) * r2 * gw2[C + c] + gb2[C + c];
+        o[q] = scl[c] * (a * sigmoidf_(gt));
+    }
+    TS* xp = x + p * C + c0;
+    if constexpr (sizeof(TS) == 2) {
+        uint4 v = *reinterpret_cast<const uint4*>(xp);
+        bf16_t* e = reinterpret_cast<bf16_t*>(&v);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) e[q] = f2bf(bf2f(e[q]) + o[q]);
+        *reinterpret_cast<uint4*>(xp) = v;
     } else {
-        if (!valid) return;
-        const int64_t g = p / L;
-        const double cnt = (double)L * N;
-        const double mm = st[2 * g] / cnt;
-        double var = st[2 * g + 1] / cnt - mm * mm;
-        if (var < 0) var = 0;
-        const float mean = (float)mm, rstd = (float)(1.0 / sqrt(var + 1e-5));
-        float4* xr = reinterpret_cast<float4*>(x + p * C);
-#pragma unroll 2
-        for (int c4 = 0; c4 < C / 4; ++c4) {
-            float4 xv = xr[c4];
-            float o[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int c = 4 * c4 + q;
-                float a = bl[c], gt = bl[C + c];
-#pragma unroll
-                for (int j = 0; j < H; ++j) {
-                    a += wl[c * H + j] * hv[j];
-                    gt += wl[(C + c) * H + j] * hv[j];
-                }
-                a = (a - mean) * rstd * gwl[c] + gbl[c];
-                gt = (gt - mean) * rstd * gwl[C + c] + gbl[C + c];
-                o[q] = scl[c] * (a * sigmoidf_(gt));
-            }
-            xv.x += o[0]; xv.y += o[1]; xv.z += o[2]; xv.w += o[3];
-            xr[c4] = xv;
-        }
+        float4 a = reinterpret_cast<const float4*>(xp)[0], b = reinterpret_cast<const float4*>(xp)[1];
+        a.x += o[0]; a.y += o[1]; a.z += o[2]; a.w += o[3];
+        b.x += o[4]; b.y += o[5]; b.z += o[6]; b.w += o[7];
+        reinterpret_cast<float4*>(xp)[0] = a;
+        reinterpret_cast<float4*>(xp)[1] = b;
     }
 }
 
-int dconv_small_launch(float* x, float* h, int64_t nb, int64_t L, int C, int dil, const float* w3, const float* b3,
-                       const float* g1w, const float* g1b, const float* w1, const float* b1, const float* g2w,
-                       const float* g2b, const float* scale, double* st_h, double* st_y, hipStream_t s, bool fast) {
+template <int C, typename TS, bool FAST>
+static void dconv_small_t(void* x, float* h, int64_t nb, int64_t L, int dil, const float* w3, const float* b3,
+                          const float* g1w, const float* g1b, const float* w1, const float* b1, const float* g2w,
+                          const float* g2b, const float* scale, double* st_h, double* st_y, hipStream_t s) {
+    constexpr int H = C / 8, TILE = sizeof(TS) == 2 ? 256 : 128;
     const int64_t P = nb * L;
-    const dim3 grid((unsigned)((P + 255) / 256));
-    const int H = C / 8;
     const double px = (double)P;
-    if (C != 48 && C != 96) return -2;
+    const double xb = (double)sizeof(TS);
+    const char* tn = sizeof(TS) == 2 ? "bf16" : "f32";
     {
         KScope ks(s);
-        if (ks.on()) ks.begin(klabel("dconv_c3_kernel<%d>", C), 2.0 * px * H * 3 * C, px * (C + H) * 4);
-        if (C == 48) hipLaunchKernelGGL((dconv_c3_kernel<48>), grid, dim3(256), 0, s, x, nb, L, dil, w3, b3, h, st_h);
-        else hipLaunchKernelGGL((dconv_c3_kernel<96>), grid, dim3(256), 0, s, x, nb, L, dil, w3, b3, h, st_h);
-    }
-    gn_gelu_launch(h, (int)nb, L * H, H, st_h, g1w, g1b, s, fast);
-    {
-        KScope ks(s);
-        if (ks.on()) ks.begin(klabel("dconv_c1_kernel<%d,false>", C), 2.0 * px * 2 * C * H, px * H * 4);
-        if (C == 48) hipLaunchKernelGGL((dconv_c1_kernel<48, false>), grid, dim3(256), 0, s, x, h, nb, L, w1, b1, st_y, g2w, g2b, scale);
-        else hipLaunchKernelGGL((dconv_c1_kernel<96, false>), grid, dim3(256), 0, s, x, h, nb, L, w1, b1, st_y, g2w, g2b, scale);
+        if (ks.on()) ks.begin(klabel("dconv_c3_kernel<%d,%s>", C, tn), 2.0 * px * H * 3 * C, px * (C * xb + H * 4));
+        hipLaunchKernelGGL((dconv_c3_kernel<C, TS>), dim3((unsigned)((P + TILE - 1) / TILE)), dim3(256), 0, s,
+                           (const TS*)x, nb, L, dil, w3, b3, h, st_h);
     }
     {
         KScope ks(s);
-        if (ks.on()) ks.begin(klabel("dconv_c1_kernel<%d,true>", C), 2.0 * px * 2 * C * H, px * (H + 2 * C) * 4);
-        if (C == 48) hipLaunchKernelGGL((dconv_c1_kernel<48, true>), grid, dim3(256), 0, s, x, h, nb, L, w1, b1, st_y, g2w, g2b, scale);
-        else hipLaunchKernelGGL((dconv_c1_kernel<96, true>), grid, dim3(256), 0, s, x, h, nb, L, w1, b1, st_y, g2w, g2b, scale);
+        if (ks.on()) ks.begin(klabel("dconv_c1_stats_kernel<%d>", C), 2.0 * px * 2 * C * H, px * H * 4);
+        hipLaunchKernelGGL((dconv_c1_stats_kernel<C, FAST>), dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, h, nb,
+                           L, st_h, g1w, g1b, w1, b1, st_y);
     }
+    {
+        KScope ks(s);
+        if (ks.on()) ks.begin(klabel("dconv_c1_apply_kernel<%d,%s>", C, tn), 2.0 * px * 2 * C * H, px * (H * 4 + 2 * C * xb));
+        const int64_t n = P * (C / 8);
+        hipLaunchKernelGGL((dconv_c1_apply_kernel<C, TS, FAST>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
+                           (TS*)x, h, nb, L, st_h, g1w, g1b, w1, b1, st_y, g2w, g2b, scale);
+    }
+}
+
+int dconv_small_launch(void* x, int x_bf16, float* h, int64_t nb, int64_t L, int C, int dil, const float* w3,
+                       const float* b3, const float* g1w, const float* g1b, const float* w1, const float* b1,
+                       const float* g2w, const float* g2b, const float* scale, double* st_h, double* st_y, hipStream_t s,
+                       bool fast) {
+    if (dil < 1 || dil > 2) return -2;
+#define ATHD_DC(CC, TS, FA) \
+    dconv_small_t<CC, TS, FA>(x, h, nb, L, dil, w3, b3, g1w, g1b, w1, b1, g2w, g2b, scale, st_h, st_y, s)
+    if (C == 48) {
+        if (x_bf16) { if (fast) ATHD_DC(48, bf16_t, true); else ATHD_DC(48, bf16_t, false); }
+        else { if (fast) ATHD_DC(48, float, true); else ATHD_DC(48, float, false); }
+    } else if (C == 96) {
+        if (x_bf16) { if (fast) ATHD_DC(96, bf16_t, true); else ATHD_DC(96, bf16_t, false); }
+        else { if (fast) ATHD_DC(96, float, true); else ATHD_DC(96, float, false); }
+    } else {
+        return -2;
+    }
+#undef ATHD_DC
     return (int)hipGetLastError();
 }
 

@@ -47,12 +47,16 @@ Dims make_dims(int64_t B, int64_t T, int P) {
 
 struct Bufs {
     float* spec;
+    float* specT;
     double* stats;
     int64_t nstats;     // number of double pairs
     float *snorm, *tnorm_div, *tnorm_std;
-    float* saved[4];
-    float* saved_t[4];
-    float *ybuf, *hbuf;
+    // encoder activations: f32 in parity mode, bf16 in throughput mode (Bufs::ea bytes per element)
+    void* saved[4];
+    void* saved_t[4];
+    void* ybuf;
+    float* hbuf;
+    int ea = 4;
     float *X, *XT;
     void *H[4], *QKV, *O, *F1;
     float *pos2d, *pos1d, *x_enc, *xt_enc;
@@ -75,19 +79,21 @@ size_t plan(Arena& ar, const Dims& d, Bufs& b, bool actbf) {
     b.nstats = ns;
     b.stats = ar.take<double>(2 * ns);
     b.spec = ar.take<float>(B * 2048 * Ts * 4);
+    b.specT = ar.take<float>(B * 2048 * Ts * 4);
     b.snorm = ar.take<float>(2 * B);
     b.tnorm_div = ar.take<float>(2 * B);
     b.tnorm_std = ar.take<float>(2 * B);
     int64_t ymax = 0, hmax = 0;
     for (int i = 0; i < 4; ++i) {
         const int64_t C = ENC_CH[i];
-        b.saved[i] = ar.take<float>(B * d.F[i + 1] * Ts * C);
-        b.saved_t[i] = ar.take<float>(B * d.L[i + 1] * C);
+        b.saved[i] = act(B * d.F[i + 1] * Ts * C);
+        b.saved_t[i] = act(B * d.L[i + 1] * C);
         const int64_t rows = std::max(B * d.F[i + 1] * Ts, B * d.L[i + 1]);
         ymax = std::max(ymax, rows * C);
         hmax = std::max(hmax, rows * (C / 8));
     }
-    b.ybuf = ar.take<float>(ymax);
+    b.ybuf = act(ymax);
+    b.ea = (int)ab;
     b.hbuf = ar.take<float>(hmax);
     b.X = ar.take<float>(B * d.Nf * 512);
     b.XT = ar.take<float>(B * d.Nt * 512);
@@ -123,6 +129,9 @@ size_t plan(Arena& ar, const Dims& d, Bufs& b, bool actbf) {
     b.frames = ar.take<float>(NI * Ts * 2 * 4096);
     return ar.off;
 }
+
+// element offset into an encoder activation buffer (f32 or bf16 storage)
+inline void* eoff(void* p, int64_t n, int ea) { return (char*)p + n * ea; }
 
 struct Run {
     athd_ctx* c;
@@ -164,41 +173,49 @@ struct Run {
         g.ldo = w.N;
         return g;
     }
-    void gemm(const GemmDesc& g, const char* w) { check(gemm_launch(g, mode, s), w); }
+    void gemm(const GemmDesc& g, const char* w) {
+        KSite site(w);
+        check(gemm_launch(g, mode, s), w);
+    }
 };
 
 // One encoder level's DConv (2 residual layers) on x viewed as [nb][L][C] (freq: nb = B*F rows along time).
 // Per layer: h = conv3(x) (+stats) -> GN+GELU in place -> 1x1 conv twice: pass 1 only accumulates the GroupNorm
 // statistics of its 2C outputs, pass 2 recomputes them (K = C/8 is tiny) and applies GN -> GLU -> LayerScale
 // -> residual in the epilogue, writing x in place.  The 2C-channel intermediate never touches HBM.
-void dconv(Run& r, const EncW& e, const Bufs& b, float* x, int64_t nb, int64_t L) {
+void dconv(Run& r, const EncW& e, const Bufs& b, void* x, int64_t nb, int64_t L) {
+    const int ab = r.actbf ? 1 : 0;
     const int C = e.cout, Hh = C / 8;
     for (int dd = 0; dd < 2; ++dd) {
         const int dil = 1 << dd;
         double* st_h = r.stats(nb);
         double* st_y = r.stats(nb);
         if (C <= 96) {   // narrow levels: HBM-bound VALU kernels (dconv.hip)
-            r.check(dconv_small_launch(x, b.hbuf, nb, L, C, dil, e.dc.w3f[dd], e.dc.c3[dd].bias, e.dc.g1w[dd],
+            KSite site(dd == 0 ? "dconv0" : "dconv1");
+            r.check(dconv_small_launch(x, ab, b.hbuf, nb, L, C, dil, e.dc.w3f[dd], e.dc.c3[dd].bias, e.dc.g1w[dd],
                                        e.dc.g1b[dd], e.dc.w1f[dd], e.dc.b1f[dd], e.dc.g2wf[dd], e.dc.g2bf[dd],
                                        e.dc.scale[dd], st_h, st_y, r.s, r.actbf), "dconv_small");
             continue;
         }
         GemmDesc g;
-        g.A = x; g.nb = (int)nb; g.H_in = (int)L; g.W = 1; g.C_in = C; g.a_ld = C;
+        g.A = x; g.a_bf16 = ab; g.nb = (int)nb; g.H_in = (int)L; g.W = 1; g.C_in = C; g.a_ld = C;
         g.ntaps = 3; g.in_stride = 1; g.in_off = -dil; g.dil = dil; g.H_out = (int)L;
         g.Wp = e.dc.c3[dd].w; g.N = Hh; g.K = e.dc.c3[dd].K; g.Kp = e.dc.c3[dd].Kp; g.bias = e.dc.c3[dd].bias;
         g.C = b.hbuf; g.H_out_total = (int)L; g.ldo = Hh; g.stats = st_h;
         r.gemm(g, "dconv.conv3");
-        gn_gelu_launch(b.hbuf, (int)nb, L * Hh, Hh, st_h, e.dc.g1w[dd], e.dc.g1b[dd], r.s, r.actbf);
+        {
+            KSite site("dconv.gn_gelu");
+            gn_gelu_launch(b.hbuf, (int)nb, L * Hh, Hh, st_h, e.dc.g1w[dd], e.dc.g1b[dd], r.s, r.actbf);
+        }
         GemmDesc g2;
         g2.A = b.hbuf; g2.nb = (int)nb; g2.H_in = (int)L; g2.W = 1; g2.C_in = Hh; g2.a_ld = Hh; g2.H_out = (int)L;
         g2.Wp = e.dc.c1[dd].w; g2.N = 2 * C; g2.K = Hh; g2.Kp = e.dc.c1[dd].Kp; g2.bias = e.dc.c1[dd].bias;
-        g2.C = x; g2.H_out_total = (int)L; g2.ldo = C;
+        g2.C = x; g2.c_bf16 = ab; g2.H_out_total = (int)L; g2.ldo = C;
         GemmDesc g1 = g2;
         g1.stats = st_y; g1.store = 0;
         r.gemm(g1, "dconv.conv1x1.stats");
         g2.act = ACT_GLU; g2.gn_stats = st_y; g2.gn_count = L * 2 * C; g2.gn_w = e.dc.g2w[dd]; g2.gn_b = e.dc.g2b[dd];
-        g2.res = x; g2.res_scale = e.dc.scale[dd];
+        g2.res = x; g2.res_bf16 = ab; g2.res_scale = e.dc.scale[dd];
         r.gemm(g2, "dconv.conv1x1.apply");
     }
 }
@@ -223,7 +240,7 @@ void encode(Run& r, const Dims& d, const Bufs& b, const float* wav) {
         pp.ext_left = epl;
         pp.Lx = d.T + epl + epr;
     }
-    stft_launch(wav, (int)B, d.T, pp, (int)Ts, c->tw, c->win, b.spec, r.s);
+    stft_launch(wav, (int)B, d.T, pp, (int)Ts, c->tw, c->win, b.spec, b.specT, r.s);
     double* st_spec = r.stats(B);
     double* st_wav = r.stats(B);
     stats_launch(b.spec, (int)B, 2048LL * Ts * 4, st_spec, r.s);
@@ -232,56 +249,63 @@ void encode(Run& r, const Dims& d, const Bufs& b, const float* wav) {
     input_norm_params_launch(st_wav, (int)B, 2 * d.T, b.tnorm_div, b.tnorm_std, r.s);
 
     // ---- encoders (ATHTDemucs_v2.py:197-217; HEncLayer + DConv) ----
+    const int eab = r.actbf ? 1 : 0;       // encoder activations in bf16 (throughput mode)
+    static const char* const kFenc[4] = {"fenc0", "fenc1", "fenc2", "fenc3"};
+    static const char* const kTenc[4] = {"tenc0", "tenc1", "tenc2", "tenc3"};
     for (int i = 0; i < 4; ++i) {
+        KStage stage(kFenc[i]);
         // freq branch: conv (8,1)/(4,1) along freq rows
         const EncW& e = c->fenc[i];
         const int C = e.cout;
         const int Fi = d.F[i], Fo = d.F[i + 1];
         GemmDesc g;
         g.A = i == 0 ? (const void*)b.spec : (const void*)b.saved[i - 1];
+        g.a_bf16 = i == 0 ? 0 : eab;
         g.nb = (int)B; g.H_in = Fi; g.W = (int)Ts; g.C_in = e.cin; g.a_ld = e.cin;
         g.ntaps = 8; g.in_stride = 4; g.in_off = -2; g.dil = 1; g.H_out = Fo;
         g.a_norm = i == 0 ? b.snorm : nullptr;
         g.Wp = e.conv.w; g.N = C; g.K = e.conv.K; g.Kp = e.conv.Kp; g.bias = e.conv.bias;
-        g.C = b.ybuf; g.H_out_total = Fo; g.ldo = C; g.act = ACT_GELU;
+        g.C = b.ybuf; g.c_bf16 = eab; g.H_out_total = Fo; g.ldo = C; g.act = ACT_GELU;
         r.gemm(g, "fenc.conv");
         dconv(r, e, b, b.ybuf, B * Fo, Ts);
         GemmDesc gr;
-        gr.A = b.ybuf; gr.nb = (int)B; gr.H_in = Fo; gr.W = (int)Ts; gr.C_in = C; gr.a_ld = C; gr.H_out = Fo;
+        gr.A = b.ybuf; gr.a_bf16 = eab; gr.nb = (int)B; gr.H_in = Fo; gr.W = (int)Ts; gr.C_in = C; gr.a_ld = C; gr.H_out = Fo;
         gr.Wp = e.rewrite.w; gr.N = 2 * C; gr.K = C; gr.Kp = e.rewrite.Kp; gr.bias = e.rewrite.bias;
-        gr.C = b.saved[i]; gr.H_out_total = Fo; gr.ldo = C; gr.act = ACT_GLU;
+        gr.C = b.saved[i]; gr.c_bf16 = eab; gr.H_out_total = Fo; gr.ldo = C; gr.act = ACT_GLU;
         gr.row_add = i == 0 ? c->femb : nullptr;    // + freq_emb_scale * freq_emb(frs) (ATHTDemucs_v2.py:212-215)
         r.gemm(gr, "fenc.rewrite");
 
         // time branch: right zero-pad to a multiple of 4 is implicit (rows >= L read as 0)
+        KStage tstage(kTenc[i]);
         const EncW& et = c->tenc[i];
         const int64_t Li = d.L[i], Lo = d.L[i + 1];
         GemmDesc gt;
         if (i == 0) {
             gt.A = wav; gt.a_ld = 1; gt.a_cs = d.T; gt.a_bs = 2 * d.T; gt.a_norm = b.tnorm_div;
         } else {
-            gt.A = b.saved_t[i - 1]; gt.a_ld = et.cin;
+            gt.A = b.saved_t[i - 1]; gt.a_bf16 = eab; gt.a_ld = et.cin;
         }
         gt.nb = (int)B; gt.H_in = (int)Li; gt.W = 1; gt.C_in = et.cin;
         gt.ntaps = 8; gt.in_stride = 4; gt.in_off = -2; gt.dil = 1; gt.H_out = (int)Lo;
         gt.Wp = et.conv.w; gt.N = C; gt.K = et.conv.K; gt.Kp = et.conv.Kp; gt.bias = et.conv.bias;
-        gt.C = b.ybuf; gt.H_out_total = (int)Lo; gt.ldo = C; gt.act = ACT_GELU;
+        gt.C = b.ybuf; gt.c_bf16 = eab; gt.H_out_total = (int)Lo; gt.ldo = C; gt.act = ACT_GELU;
         r.gemm(gt, "tenc.conv");
         dconv(r, et, b, b.ybuf, B, Lo);
         GemmDesc grt;
-        grt.A = b.ybuf; grt.nb = (int)B; grt.H_in = (int)Lo; grt.W = 1; grt.C_in = C; grt.a_ld = C; grt.H_out = (int)Lo;
+        grt.A = b.ybuf; grt.a_bf16 = eab; grt.nb = (int)B; grt.H_in = (int)Lo; grt.W = 1; grt.C_in = C; grt.a_ld = C; grt.H_out = (int)Lo;
         grt.Wp = et.rewrite.w; grt.N = 2 * C; grt.K = C; grt.Kp = et.rewrite.Kp; grt.bias = et.rewrite.bias;
-        grt.C = b.saved_t[i]; grt.H_out_total = (int)Lo; grt.ldo = C; grt.act = ACT_GLU;
+        grt.C = b.saved_t[i]; grt.c_bf16 = eab; grt.H_out_total = (int)Lo; grt.ldo = C; grt.act = ACT_GLU;
         r.gemm(grt, "tenc.rewrite");
     }
 
     // ---- cross-transformer (ATHTDemucs_v2.py:219-234) ----
+    KStage xstage("transformer");
     const int ab = r.actbf ? 1 : 0;
     {
-        GemmDesc g = r.lin(c->up, b.saved[3], 0, (int)B, d.Nf, 384);
+        GemmDesc g = r.lin(c->up, b.saved[3], ab, (int)B, d.Nf, 384);
         g.C = b.X;
         r.gemm(g, "upsampler");
-        GemmDesc gt = r.lin(c->up_t, b.saved_t[3], 0, (int)B, d.Nt, 384);
+        GemmDesc gt = r.lin(c->up_t, b.saved_t[3], ab, (int)B, d.Nt, 384);
         gt.C = b.XT;
         r.gemm(gt, "upsampler_t");
     }
@@ -377,7 +401,8 @@ void encode(Run& r, const Dims& d, const Bufs& b, const float* wav) {
 // keep < 0: store all rows (4*H_in rows).  keep > 0: store only rows 4u+1, 4u+2 as slots 2u, 2u+1 (the only
 // rows the following exact /4 bilinear resize reads); statistics (if st) still cover all four residues.
 void conv_t(Run& r, const DecW& w, const void* A, int a_bf16, int nb, int H_in, int W, void* out, int out_bf16,
-            double* st, int keep) {
+            double* st, int keep, const char* stage) {
+    KStage kst(stage);
     for (int pi = 0; pi < 2; ++pi) {
         GemmDesc g;
         g.A = A; g.a_bf16 = a_bf16; g.nb = nb; g.H_in = H_in; g.W = W; g.C_in = w.cin; g.a_ld = w.cin;
@@ -391,7 +416,7 @@ void conv_t(Run& r, const DecW& w, const void* A, int a_bf16, int nb, int H_in, 
             if (pi == 0) { g.o_off = 0; g.hi_row_off = 0; g.store_mask = 2; }   // residue 1 -> slot 2u
             else { g.o_off = 1; g.store_mask = 1; }                              // residue 2 -> slot 2u+1
         }
-        r.gemm(g, "conv_transpose");
+        r.gemm(g, pi == 0 ? "convt.pair01" : "convt.pair23");
     }
 }
 
@@ -406,6 +431,7 @@ void decode_chunk(Run& r, const Dims& d, const Bufs& b, int64_t s0, int64_t Bc, 
     text_vec_launch(text_per_item ? text + s0 * 512 : text, NI, P, text_per_item ? 1 : 0, c->ta_vw, c->ta_vb, c->ta_ivw,
                     c->ta_ivb, c->ta_ow, c->ta_ob, b.avec, r.s);
     auto text_attn = [&](const float* enc, int64_t ntok, float* cond) {
+        KStage kst(ntok == d.Nf ? "text_attn.freq" : "text_attn.time");
         add_rowvec_launch(enc, b.avec, NI, P, ntok, 384, b.U, r.s);
         GemmDesc g = r.lin(c->mlp0, b.U, 0, NI, ntok, 384);
         g.C = b.Hm; g.c_bf16 = ab; g.act = ACT_GELU;
@@ -421,19 +447,21 @@ void decode_chunk(Run& r, const Dims& d, const Bufs& b, int64_t s0, int64_t Bc, 
     text_attn(b.xt_enc + s0 * d.Nt * 384, d.Nt, b.xt_cond);
 
     // ---- frequency decoder (ATHTDemucs_v2.py:82-104, 293-297) ----
-    float* const sv[4] = {b.saved[0] + s0 * 512 * Ts * 48, b.saved[1] + s0 * 128 * Ts * 96,
-                          b.saved[2] + s0 * 32 * Ts * 192, b.saved[3] + s0 * 8 * Ts * 384};
+    const int ea = b.ea;
+    void* const sv[4] = {eoff(b.saved[0], s0 * 512 * Ts * 48, ea), eoff(b.saved[1], s0 * 128 * Ts * 96, ea),
+                         eoff(b.saved[2], s0 * 32 * Ts * 192, ea), eoff(b.saved[3], s0 * 8 * Ts * 384, ea)};
     {
         // level 0: 8 -> 32 rows, GN+GELU (in place, fp32: every source row feeds ~Ts/32 output rows), resize to
         // Tspec rows, + 0.1 * resize(saved[3][:, :192])
         double* st = r.stats(NI);
-        conv_t(r, c->fdec[0], b.x_cond, ab, NI, 8, (int)Ts, b.G, 0, st, -1);
+        conv_t(r, c->fdec[0], b.x_cond, ab, NI, 8, (int)Ts, b.G, 0, st, -1, "fdec0");
+        KStage kst("fdec0");
         gn_gelu_launch(b.G, NI, 32 * Ts * 192, 192, st, c->fdec[0].gnw, c->fdec[0].gnb, r.s, r.actbf);
         MergeDesc m;
         m.src = b.G; m.H_src = 32; m.kept = 0; m.C = 192;
-        m.skip = sv[3]; m.H_skip = 8; m.C_skip = 384; m.P = P;
+        m.skip = sv[3]; m.skip_bf16 = ab; m.H_skip = 8; m.C_skip = 384; m.P = P;
         m.out = b.D; m.out_bf16 = ab; m.H_out = (int)Ts; m.W = (int)Ts; m.NI = NI;
-        dec_merge_launch(m, r.s);
+        r.check(dec_merge_launch(m, r.s), "dec_merge");
         // levels 1..3: Tspec -> 4 Tspec rows; the /4 bilinear resize reads only rows 4d+1, 4d+2
         const int skH[3] = {32, 128, 512};
         const int skC[3] = {192, 96, 48};
@@ -441,41 +469,45 @@ void decode_chunk(Run& r, const Dims& d, const Bufs& b, int64_t s0, int64_t Bc, 
             const DecW& w = c->fdec[i];
             const bool last = i == 3;
             double* sti = last ? nullptr : r.stats(NI);
-            conv_t(r, w, b.D, ab, NI, (int)Ts, (int)Ts, b.G, ab, sti, last ? 2 : 1);
+            static const char* const kF[4] = {"fdec0", "fdec1", "fdec2", "fdec3"};
+            conv_t(r, w, b.D, ab, NI, (int)Ts, (int)Ts, b.G, ab, sti, last ? 2 : 1, kF[i]);
+            KStage kst2(kF[i]);
             MergeDesc mm;
             mm.src = b.G; mm.src_bf16 = ab; mm.H_src = 4 * (int)Ts; mm.kept = 1; mm.C = w.cout; mm.fast_gelu = ab;
             mm.stats = sti; mm.gn_count = 4 * Ts * Ts * w.cout; mm.gn_w = w.gnw; mm.gn_b = w.gnb;
-            mm.skip = sv[3 - i]; mm.H_skip = skH[i - 1]; mm.C_skip = skC[i - 1]; mm.P = P;
+            mm.skip = sv[3 - i]; mm.skip_bf16 = ab; mm.H_skip = skH[i - 1]; mm.C_skip = skC[i - 1]; mm.P = P;
             mm.H_out = (int)Ts; mm.W = (int)Ts; mm.NI = NI;
             if (last) {
                 mm.out = b.FO; mm.proj_w = c->fout_w; mm.proj_b = c->fout_b;     // freq_out 1x1 (4 -> 2)
             } else {
                 mm.out = b.D; mm.out_bf16 = ab;
             }
-            dec_merge_launch(mm, r.s);
+            r.check(dec_merge_launch(mm, r.s), "dec_merge");
         }
     }
     // ---- mask + iSTFT frames (ATHTDemucs_v2.py:297-310) ----
-    istft_frames_launch(b.FO, NI, (int)Ts, P, b.spec + s0 * 2048 * Ts * 4, c->tw, c->win, b.frames, r.s);
+    istft_frames_launch(b.FO, NI, (int)Ts, P, b.specT + s0 * 2048 * Ts * 4, c->tw, c->win, b.frames, r.s);
 
     // ---- time decoder (ATHTDemucs_v2.py:125-139, 313-321) ----
     {
-        const float* svt[4] = {b.saved_t[0] + s0 * d.L[1] * 48, b.saved_t[1] + s0 * d.L[2] * 96,
-                               b.saved_t[2] + s0 * d.L[3] * 192, b.saved_t[3] + s0 * d.L[4] * 384};
+        const void* svt[4] = {eoff(b.saved_t[0], s0 * d.L[1] * 48, ea), eoff(b.saved_t[1], s0 * d.L[2] * 96, ea),
+                              eoff(b.saved_t[2], s0 * d.L[3] * 192, ea), eoff(b.saved_t[3], s0 * d.L[4] * 384, ea)};
         const void* A = b.xt_cond;
         int64_t Lin = d.Nt;
         for (int i = 0; i < 4; ++i) {
             const DecW& w = c->tdec[i];
             const bool last = i == 3;
             double* st = last ? nullptr : r.stats(NI);
-            conv_t(r, w, A, ab, NI, (int)Lin, 1, b.G, ab, st, -1);
+            static const char* const kT[4] = {"tdec0", "tdec1", "tdec2", "tdec3"};
+            conv_t(r, w, A, ab, NI, (int)Lin, 1, b.G, ab, st, -1, kT[i]);
+            KStage kst(kT[i]);
             const int64_t target = d.L[3 - i];       // lengths_t reversed
             MergeDesc m;
             m.src = b.G; m.src_bf16 = ab; m.H_src = (int)(4 * Lin); m.kept = 0; m.C = w.cout; m.fast_gelu = ab;
             m.stats = st; m.gn_count = 4 * Lin * w.cout; m.gn_w = w.gnw; m.gn_b = w.gnb;
-            m.skip = svt[3 - i]; m.H_skip = (int)d.L[4 - i]; m.C_skip = ENC_CH[3 - i]; m.P = P;
+            m.skip = svt[3 - i]; m.skip_bf16 = ab; m.H_skip = (int)d.L[4 - i]; m.C_skip = ENC_CH[3 - i]; m.P = P;
             m.out = b.D; m.out_bf16 = last ? 0 : ab; m.H_out = (int)target; m.W = 1; m.NI = NI;
-            dec_merge_launch(m, r.s);
+            r.check(dec_merge_launch(m, r.s), "dec_merge");
             A = b.D;
             Lin = target;
         }
@@ -501,10 +533,10 @@ void dump_all(const Dims& d, const Bufs& b, hipStream_t s) {
         {"xt_enc", b.xt_enc, B * d.Nt * 384, "B,Nt,384"},
         {"x_cond", b.x_cond, NI * d.Nf * 384, "NI,Nf,384"},
         {"xt_cond", b.xt_cond, NI * d.Nt * 384, "NI,Nt,384"},
-        {"FO", b.FO, NI * Ts * Ts * 2, "NI,Ts,Ts,2"},
+        {"FO", b.FO, NI * Ts * Ts * 2, "NI,t,row,2"},
         {"E3", b.D, NI * d.T * 4, "NI,T,4"},
     };
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < 4 && b.ea == 4; ++i) {      // encoder activations are f32 only in parity mode
         es.push_back({"saved" + std::to_string(i), b.saved[i], B * d.F[i + 1] * Ts * ENC_CH[i], "B,F,Ts,C"});
         es.push_back({"saved_t" + std::to_string(i), b.saved_t[i], B * d.L[i + 1] * ENC_CH[i], "B,L,C"});
     }
@@ -526,6 +558,7 @@ int forward_impl(athd_ctx* c, const float* wav, int64_t B, int64_t T, const floa
     if (!c) return ATHD_EINVAL;
     if (!c->finalized) return c->fail(ATHD_ESTATE, "athd_forward before athd_finalize");
     if (!wav || !text || !out || B <= 0 || T <= 0 || P <= 0) return c->fail(ATHD_EINVAL, "bad forward arguments");
+    if (P > 256) return c->fail(ATHD_EINVAL, "at most 256 prompts per athd_forward_prompts call");
     if (T > (int64_t)1 << 26) return c->fail(ATHD_EINVAL, "segment too long");
     const Dims d = make_dims(B, T, P);
     Bufs b;

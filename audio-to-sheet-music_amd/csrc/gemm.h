@@ -43,7 +43,8 @@ struct GemmDesc {
     int store_mask = 3;       //     bit0: store columns < col_split, bit1: store columns >= col_split
     // epilogue
     int act = ACT_NONE;       // ACT_GLU: packed pairs [a(16) | gate(16)] per 32 columns, output N/2 channels
-    const float* res = nullptr;       // residual (same layout as C, f32); out = res + rs[n]*v
+    const void* res = nullptr;        // residual (same layout as C; f32, or bf16 with res_bf16); out = res + rs[n]*v
+    int res_bf16 = 0;
     const float* res_scale = nullptr;
     const float* row_add = nullptr;   // out += row_add[ho][n]   (freq embedding after encoder level 0)
     double* stats = nullptr;          // per-batch {sum, sumsq} of the final output value

@@ -41,6 +41,20 @@ inline unsigned epi_flags(const GemmDesc& d) {
 template <unsigned F>
 ATHD_DEV bool on(unsigned flag) { return (F & flag) != 0; }
 
+// 4 consecutive residual values (f32 or bf16 storage)
+ATHD_DEV void ld_res4(const GemmDesc& d, int64_t off, float* r) {
+    if (d.res_bf16) {
+        const uint2 q = *reinterpret_cast<const uint2*>((const bf16_t*)d.res + off);
+        r[0] = __uint_as_float(q.x << 16);
+        r[1] = __uint_as_float(q.x & 0xFFFF0000u);
+        r[2] = __uint_as_float(q.y << 16);
+        r[3] = __uint_as_float(q.y & 0xFFFF0000u);
+    } else {
+        const float4 v = *reinterpret_cast<const float4*>((const float*)d.res + off);
+        r[0] = v.x; r[1] = v.y; r[2] = v.z; r[3] = v.w;
+    }
+}
+
 template <int TM, int TN, unsigned F, bool FASTG>
 ATHD_DEV void gemm_epilogue(const GemmDesc& d, const f32x4_t (&acc)[TM][TN], int64_t m0, int n0, int wm0, int wn0,
                             int lane, double* st_lds, int BM) {
@@ -120,8 +134,8 @@ ATHD_DEV void gemm_epilogue(const GemmDesc& d, const f32x4_t (&acc)[TM][TN], int
                         o[q] = v;
                     }
                     if (f_res) {
-                        const float4 rv = *reinterpret_cast<const float4*>(d.res + obase + oc);
-                        const float rr[4] = {rv.x, rv.y, rv.z, rv.w};
+                        float rr[4];
+                        ld_res4(d, obase + oc, rr);
 #pragma unroll
                         for (int q = 0; q < 4; ++q) o[q] = rr[q] + (d.res_scale ? d.res_scale[oc + q] : 1.f) * o[q];
                     }
@@ -150,8 +164,8 @@ ATHD_DEV void gemm_epilogue(const GemmDesc& d, const f32x4_t (&acc)[TM][TN], int
                         o[q] = v;
                     }
                     if (f_res) {
-                        const float4 rv = *reinterpret_cast<const float4*>(d.res + obase + n);
-                        const float rr[4] = {rv.x, rv.y, rv.z, rv.w};
+                        float rr[4];
+                        ld_res4(d, obase + n, rr);
 #pragma unroll
                         for (int q = 0; q < 4; ++q) o[q] = rr[q] + (d.res_scale ? d.res_scale[n + q] : 1.f) * o[q];
                     }

@@ -14,9 +14,11 @@ struct PadPlan {
 };
 
 // spectral.hip
+// spec [b][f][t][4] (encoder layout) and specT [b][t][f][4] (frame-major, for the iSTFT)
 void stft_launch(const float* wav, int nb, int64_t T, const PadPlan& pp, int Tspec, const float2* tw,
-                 const float* win, float* spec, hipStream_t s);
-void istft_frames_launch(const float* fo, int NI, int Tspec, int P, const float* spec, const float2* tw,
+                 const float* win, float* spec, float* specT, hipStream_t s);
+// fo: FO^T [item][t][row][2] (dec_merge_proj_kernel output); specT as above
+void istft_frames_launch(const float* fo, int NI, int Tspec, int P, const float* specT, const float2* tw,
                          const float* win, float* frames, hipStream_t s);
 void combine_launch(const float* frames, int NI, int Tspec, int64_t T, const float* win2, const float* xt3,
                     const float* tw_out, const float* tb_out, const float* tnorm, int P, float* out, hipStream_t s);
@@ -54,16 +56,18 @@ struct MergeDesc {
     int kept = 0;                                // src holds only rows 4d+1, 4d+2 as slots 2d, 2d+1
     int C = 0;                                   // channels of src and out
     const double* stats = nullptr; int64_t gn_count = 0; const float* gn_w = nullptr; const float* gn_b = nullptr;
-    const float* skip = nullptr; int H_skip = 0; int C_skip = 0; int P = 1;
+    const void* skip = nullptr; int skip_bf16 = 0; int H_skip = 0; int C_skip = 0; int P = 1;
     void* out = nullptr; int out_bf16 = 0; int H_out = 0; int W = 1; int NI = 1;
     const float* proj_w = nullptr; const float* proj_b = nullptr;   // optional 1x1 C(=4) -> 2 projection
     int fast_gelu = 0;                            // bf16 mode: branch-free erf
 };
-void dec_merge_launch(const MergeDesc& d, hipStream_t s);
+int dec_merge_launch(const MergeDesc& d, hipStream_t s);   // -1: P > 256 or NI % P != 0
 // dconv.hip: one DConv layer (conv3 -> GN -> GELU -> 1x1 -> GN -> GLU -> LayerScale -> residual) for C in {48, 96}
-int dconv_small_launch(float* x, float* h, int64_t nb, int64_t L, int C, int dil, const float* w3, const float* b3,
-                       const float* g1w, const float* g1b, const float* w1, const float* b1, const float* g2w,
-                       const float* g2b, const float* scale, double* st_h, double* st_y, hipStream_t s, bool fast);
+// x: [nb][L][C] f32 or bf16 (x_bf16), updated in place; h: [nb][L][C/8] f32 scratch
+int dconv_small_launch(void* x, int x_bf16, float* h, int64_t nb, int64_t L, int C, int dil, const float* w3,
+                       const float* b3, const float* g1w, const float* g1b, const float* w1, const float* b1,
+                       const float* g2w, const float* g2b, const float* scale, double* st_h, double* st_y, hipStream_t s,
+                       bool fast);
 // positional tables of the cross-transformer (computed on device with the fp32 op order of demucs)
 void pos2d_launch(float* out, int Fr, int T1, int C, hipStream_t s);   // out[(f*T1+t)][C]
 void pos1d_launch(float* out, int T2, int C, hipStream_t s);           // out[t][C]

@@ -277,82 +277,117 @@ ATHD_DEV void merge_src_v(const MergeDesc& d, int64_t item, int i, int w, int c,
     }
 }
 
+// resize_H(act(GN(src)))[ho][w][c..c+V) of one item
 template <int V>
-ATHD_DEV void merge_v(const MergeDesc& d, int64_t item, int ho, int w, int c, float mean, float rstd, float* out) {
-    float a[V], b[V];
+ATHD_DEV void merge_src_lerp(const MergeDesc& d, int64_t item, int ho, int w, int c, float mean, float rstd, float* out) {
     if (d.H_src == d.H_out) {
         merge_src_v<V>(d, item, ho, w, c, mean, rstd, out);
     } else {
+        float a[V], b[V];
         const LinIdx li = lin_index(ho, d.H_src, d.H_out);
         merge_src_v<V>(d, item, li.i0, w, c, mean, rstd, a);
         merge_src_v<V>(d, item, li.i1, w, c, mean, rstd, b);
 #pragma unroll
         for (int j = 0; j < V; ++j) out[j] = li.l0 * a[j] + li.l1 * b[j];
     }
-    const int64_t sb = item / d.P;
-    const float* sk = d.skip + sb * (int64_t)d.H_skip * d.W * d.C_skip;
+}
+
+// 0.1 * resize_H(skip[seg])[ho][w][c..c+V): shared by the P prompt items of a segment, computed once
+template <int V>
+ATHD_DEV void merge_skip_v(const MergeDesc& d, int64_t seg, int ho, int w, int c, float* sv) {
+    const int64_t sk = seg * (int64_t)d.H_skip * d.W * d.C_skip;
+    float a[V], b[V];
     if (d.H_skip == d.H_out) {
-        ldv<V>(sk, 0, (int64_t)(ho * d.W + w) * d.C_skip + c, a);
+        ldv<V>(d.skip, d.skip_bf16, sk + (int64_t)(ho * d.W + w) * d.C_skip + c, a);
 #pragma unroll
-        for (int j = 0; j < V; ++j) out[j] = out[j] + a[j] * 0.1f;
+        for (int j = 0; j < V; ++j) sv[j] = a[j] * 0.1f;
     } else {
         const LinIdx lj = lin_index(ho, d.H_skip, d.H_out);
-        ldv<V>(sk, 0, (int64_t)(lj.i0 * d.W + w) * d.C_skip + c, a);
-        ldv<V>(sk, 0, (int64_t)(lj.i1 * d.W + w) * d.C_skip + c, b);
+        ldv<V>(d.skip, d.skip_bf16, sk + (int64_t)(lj.i0 * d.W + w) * d.C_skip + c, a);
+        ldv<V>(d.skip, d.skip_bf16, sk + (int64_t)(lj.i1 * d.W + w) * d.C_skip + c, b);
 #pragma unroll
-        for (int j = 0; j < V; ++j) out[j] = out[j] + (lj.l0 * a[j] + lj.l1 * b[j]) * 0.1f;
+        for (int j = 0; j < V; ++j) sv[j] = (lj.l0 * a[j] + lj.l1 * b[j]) * 0.1f;
     }
 }
 
+constexpr int MERGE_MAXP = 256;
+
+// per-item GroupNorm (mean, rstd) of the block's segment into LDS
+ATHD_DEV void merge_gn_lds(const MergeDesc& d, int64_t seg, float* s_mean, float* s_rstd) {
+    for (int p = threadIdx.x; p < d.P; p += blockDim.x) {
+        float mean = 0.f, rstd = 1.f;
+        if (d.stats) gn_params(d.stats, seg * d.P + p, d.gn_count, mean, rstd);
+        s_mean[p] = mean;
+        s_rstd[p] = rstd;
+    }
+    __syncthreads();
+}
+
+// grid.y = segment; every thread reads the skip once and writes all P items of its segment
 template <int V>
 __global__ __launch_bounds__(256) void dec_merge_kernel(const MergeDesc d) {
-    const int64_t item = blockIdx.y;
-    float mean = 0.f, rstd = 1.f;
-    if (d.stats) gn_params(d.stats, item, d.gn_count, mean, rstd);
+    const int64_t seg = blockIdx.y;
+    __shared__ float s_mean[MERGE_MAXP], s_rstd[MERGE_MAXP];
+    merge_gn_lds(d, seg, s_mean, s_rstd);
     const int cv = d.C / V;
     const int n = d.H_out * d.W * cv;
-    const int64_t obase = item * (int64_t)d.H_out * d.W * d.C;
+    const int64_t per_item = (int64_t)d.H_out * d.W * d.C;
     for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
         const int c = (i % cv) * V;
         const int pw = i / cv;
         const int w = pw % d.W;
         const int ho = pw / d.W;
-        float v[V];
-        merge_v<V>(d, item, ho, w, c, mean, rstd, v);
-        const int64_t o = obase + (int64_t)pw * d.C + c;
-        if (d.out_bf16) {
-            bf16_t h[V];
+        float sv[V];
+        merge_skip_v<V>(d, seg, ho, w, c, sv);
+        for (int p = 0; p < d.P; ++p) {
+            const int64_t item = seg * d.P + p;
+            float v[V];
+            merge_src_lerp<V>(d, item, ho, w, c, s_mean[p], s_rstd[p], v);
 #pragma unroll
-            for (int j = 0; j < V; ++j) h[j] = f2bf(v[j]);
-            if constexpr (V == 8) *reinterpret_cast<uint4*>((bf16_t*)d.out + o) = *reinterpret_cast<uint4*>(h);
-            else *reinterpret_cast<uint2*>((bf16_t*)d.out + o) = *reinterpret_cast<uint2*>(h);
-        } else {
+            for (int j = 0; j < V; ++j) v[j] = v[j] + sv[j];
+            const int64_t o = item * per_item + (int64_t)pw * d.C + c;
+            if (d.out_bf16) {
+                bf16_t h[V];
 #pragma unroll
-            for (int j = 0; j < V; j += 4)
-                *reinterpret_cast<float4*>((float*)d.out + o + j) = make_float4(v[j], v[j + 1], v[j + 2], v[j + 3]);
+                for (int j = 0; j < V; ++j) h[j] = f2bf(v[j]);
+                if constexpr (V == 8) *reinterpret_cast<uint4*>((bf16_t*)d.out + o) = *reinterpret_cast<uint4*>(h);
+                else *reinterpret_cast<uint2*>((bf16_t*)d.out + o) = *reinterpret_cast<uint2*>(h);
+            } else {
+#pragma unroll
+                for (int j = 0; j < V; j += 4)
+                    *reinterpret_cast<float4*>((float*)d.out + o + j) = make_float4(v[j], v[j + 1], v[j + 2], v[j + 3]);
+            }
         }
     }
 }
 
+// last freq level: C = 4 merged channels -> freq_out 1x1 (4 -> 2), FO^T [item][w][ho][2] (frame-major for the iSTFT)
 __global__ __launch_bounds__(256) void dec_merge_proj_kernel(const MergeDesc d) {
-    const int64_t item = blockIdx.y;
-    float mean = 0.f, rstd = 1.f;
-    if (d.stats) gn_params(d.stats, item, d.gn_count, mean, rstd);
+    const int64_t seg = blockIdx.y;
+    __shared__ float s_mean[MERGE_MAXP], s_rstd[MERGE_MAXP];
+    merge_gn_lds(d, seg, s_mean, s_rstd);
     const int n = d.H_out * d.W;
-    float* op = (float*)d.out + item * (int64_t)n * 2;
     for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
         const int w = i % d.W;
         const int ho = i / d.W;
-        float m[4];
-        merge_v<4>(d, item, ho, w, 0, mean, rstd, m);
-        float2 o;
-        o.x = d.proj_b[0] + (d.proj_w[0] * m[0] + d.proj_w[1] * m[1] + d.proj_w[2] * m[2] + d.proj_w[3] * m[3]);
-        o.y = d.proj_b[1] + (d.proj_w[4] * m[0] + d.proj_w[5] * m[1] + d.proj_w[6] * m[2] + d.proj_w[7] * m[3]);
-        *reinterpret_cast<float2*>(op + i * 2) = o;
+        float sv[4];
+        merge_skip_v<4>(d, seg, ho, w, 0, sv);
+        for (int p = 0; p < d.P; ++p) {
+            const int64_t item = seg * d.P + p;
+            float m[4];
+            merge_src_lerp<4>(d, item, ho, w, 0, s_mean[p], s_rstd[p], m);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) m[j] = m[j] + sv[j];
+            float2 o;
+            o.x = d.proj_b[0] + (d.proj_w[0] * m[0] + d.proj_w[1] * m[1] + d.proj_w[2] * m[2] + d.proj_w[3] * m[3]);
+            o.y = d.proj_b[1] + (d.proj_w[4] * m[0] + d.proj_w[5] * m[1] + d.proj_w[6] * m[2] + d.proj_w[7] * m[3]);
+            *reinterpret_cast<float2*>((float*)d.out + item * (int64_t)n * 2 + ((int64_t)w * d.H_out + ho) * 2) = o;
+        }
     }
 }
 
-void dec_merge_launch(const MergeDesc& d, hipStream_t s) {
+int dec_merge_launch(const MergeDesc& d, hipStream_t s) {
+    if (d.P < 1 || d.P > MERGE_MAXP || d.NI % d.P != 0) return -1;
     const int V = (d.C % 8 == 0) ? 8 : 4;    // C is 192/96/48 (8) or 4
     const int64_t n = (int64_t)d.H_out * d.W * (d.proj_w ? 1 : d.C / V);
     int blocks = (int)((n + 255) / 256);
@@ -364,13 +399,15 @@ void dec_merge_launch(const MergeDesc& d, hipStream_t s) {
         const double src_rows = std::min<double>(d.kept ? d.H_src / 2 : d.H_src, 2.0 * d.H_out);
         const double skip_rows = std::min<double>(d.H_skip, 2.0 * d.H_out);
         const double by = (double)d.NI * src_rows * d.W * d.C * (d.src_bf16 ? 2 : 4) +
-                          (double)(d.NI / d.P) * skip_rows * d.W * d.C_skip * 4 +
+                          (double)(d.NI / d.P) * skip_rows * d.W * d.C_skip * (d.skip_bf16 ? 2 : 4) +
                           (double)d.NI * d.H_out * d.W * (d.proj_w ? 2 * 4 : d.C * (d.out_bf16 ? 2 : 4));
         ks.begin(d.proj_w ? "dec_merge_proj_kernel" : (V == 8 ? "dec_merge_kernel<8>" : "dec_merge_kernel<4>"), 0.0, by);
     }
-    if (d.proj_w) hipLaunchKernelGGL(dec_merge_proj_kernel, dim3(blocks, d.NI), dim3(256), 0, s, d);
-    else if (V == 8) hipLaunchKernelGGL(dec_merge_kernel<8>, dim3(blocks, d.NI), dim3(256), 0, s, d);
-    else hipLaunchKernelGGL(dec_merge_kernel<4>, dim3(blocks, d.NI), dim3(256), 0, s, d);
+    const dim3 grid(blocks, d.NI / d.P);
+    if (d.proj_w) hipLaunchKernelGGL(dec_merge_proj_kernel, grid, dim3(256), 0, s, d);
+    else if (V == 8) hipLaunchKernelGGL(dec_merge_kernel<8>, grid, dim3(256), 0, s, d);
+    else hipLaunchKernelGGL(dec_merge_kernel<4>, grid, dim3(256), 0, s, d);
+    return (int)hipGetLastError();
 }
 
 // --------------------------------------------------------------------------------------------- position tables

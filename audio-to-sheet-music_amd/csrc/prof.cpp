@@ -1,14 +1,33 @@
 #include "prof.h"
 
+#include <cstdlib>
 #include <map>
 
 namespace athd {
 
 thread_local KProf* t_kprof = nullptr;
+thread_local const char* t_ksite = nullptr;
+thread_local const char* t_kstage = nullptr;
 
-void KScope::begin(const std::string& label, double flops, double bytes) {
+static bool sites_on() {
+    static const bool on = [] {
+        const char* e = std::getenv("ATHD_PROF_SITES");
+        return e && *e && *e != '0';
+    }();
+    return on;
+}
+
+void KScope::begin(const std::string& label0, double flops, double bytes) {
     KProf* p = t_kprof;
-    if (!p || (!p->only.empty() && p->only != label)) return;
+    if (!p) return;
+    std::string label = label0;
+    if (sites_on() && (t_kstage || t_ksite)) {
+        label += "@";
+        if (t_kstage) label += t_kstage;
+        if (t_kstage && t_ksite) label += ".";
+        if (t_ksite) label += t_ksite;
+    }
+    if (!p->only.empty() && p->only != label) return;
     hipEvent_t ev[2];
     for (auto& e : ev) {
         if (!p->pool.empty()) {

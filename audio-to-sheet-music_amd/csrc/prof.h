@@ -25,6 +25,18 @@ struct KProf {
 };
 
 extern thread_local KProf* t_kprof;
+extern thread_local const char* t_ksite;    // call-site tags appended as "@stage.site" when ATHD_PROF_SITES=1
+extern thread_local const char* t_kstage;
+struct KStage {                               // RAII stage tag (e.g. "fenc2", "fdec1")
+    const char* saved;
+    explicit KStage(const char* s) : saved(t_kstage) { t_kstage = s; }
+    ~KStage() { t_kstage = saved; }
+};
+struct KSite {
+    const char* saved;
+    explicit KSite(const char* s) : saved(t_ksite) { t_ksite = s; }
+    ~KSite() { t_ksite = saved; }
+};
 
 class KScope {
   public:

@@ -71,7 +71,7 @@ ATHD_DEV float pad_sample(const float* __restrict__ x, int64_t p, const PadPlan&
 
 __global__ __launch_bounds__(256) void stft_kernel(const float* __restrict__ wav, int64_t T, PadPlan pp, int Tspec,
                                                    const float2* __restrict__ tw, const float* __restrict__ win,
-                                                   float* __restrict__ spec) {
+                                                   float* __restrict__ spec, float* __restrict__ specT) {
     __shared__ cpx bufA[NFFT];
     __shared__ cpx bufB[NFFT];
     const int t = blockIdx.x;
@@ -86,6 +86,7 @@ __global__ __launch_bounds__(256) void stft_kernel(const float* __restrict__ wav
     __syncthreads();
     cpx* Z = fft4096(bufA, bufB, tw);
     float* out = spec + ((b * 2048) * Tspec + t) * 4;
+    float* outT = specT + (b * Tspec + t) * 2048LL * 4;      // frame-major copy for the iSTFT (contiguous)
     for (int k = threadIdx.x; k < 2048; k += 256) {
         cpx zk = Z[k], zn = Z[(NFFT - k) & (NFFT - 1)];
         // X_L = (zk + conj zn)/2, X_R = (zk - conj zn)/(2i); scaled by 1/64 (normalized=True)
@@ -96,19 +97,20 @@ __global__ __launch_bounds__(256) void stft_kernel(const float* __restrict__ wav
         v.z = (zk.y + zn.y) * s;
         v.w = -(zk.x - zn.x) * s;
         *reinterpret_cast<float4*>(out + (int64_t)k * Tspec * 4) = v;
+        *reinterpret_cast<float4*>(outT + (int64_t)k * 4) = v;
     }
 }
 
 void stft_launch(const float* wav, int nb, int64_t T, const PadPlan& pp, int Tspec, const float2* tw,
-                 const float* win, float* spec, hipStream_t s) {
+                 const float* win, float* spec, float* specT, hipStream_t s) {
     KScope ks(s);
-    if (ks.on()) ks.begin("stft_kernel", 0.0, (double)nb * 2 * T * 4 + (double)nb * 2048 * Tspec * 4 * 4);
-    hipLaunchKernelGGL(stft_kernel, dim3(Tspec, nb), dim3(256), 0, s, wav, T, pp, Tspec, tw, win, spec);
+    if (ks.on()) ks.begin("stft_kernel", 0.0, (double)nb * 2 * T * 4 + 2.0 * nb * 2048 * Tspec * 4 * 4);
+    hipLaunchKernelGGL(stft_kernel, dim3(Tspec, nb), dim3(256), 0, s, wav, T, pp, Tspec, tw, win, spec, specT);
 }
 
 // ---------------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void istft_frames_kernel(const float* __restrict__ fo, int Tspec, int P,
-                                                           const float* __restrict__ spec,
+                                                           const float* __restrict__ specT,
                                                            const float2* __restrict__ tw,
                                                            const float* __restrict__ win,
                                                            float* __restrict__ frames) {
@@ -117,16 +119,16 @@ __global__ __launch_bounds__(256) void istft_frames_kernel(const float* __restri
     const int t = blockIdx.x;
     const int64_t item = blockIdx.y;
     const int64_t b = item / P;
-    const float* F0 = fo + item * (int64_t)Tspec * Tspec * 2;   // [row][t][2]
-    const float* S = spec + b * 2048LL * Tspec * 4;
+    const float* F0 = fo + (item * (int64_t)Tspec + t) * Tspec * 2;   // FO^T: [item][t][row][2]
+    const float* S = specT + (b * Tspec + t) * 2048LL * 4;             // [b][t][k][4]
     for (int k = threadIdx.x; k < 2048; k += 256) {
         const LinIdx li = lin_index(k, Tspec, 2048);
-        const float* r0 = F0 + ((int64_t)li.i0 * Tspec + t) * 2;
-        const float* r1 = F0 + ((int64_t)li.i1 * Tspec + t) * 2;
+        const float* r0 = F0 + (int64_t)li.i0 * 2;
+        const float* r1 = F0 + (int64_t)li.i1 * 2;
         const float xd0 = li.l0 * r0[0] + li.l1 * r1[0];
         const float xd1 = li.l0 * r0[1] + li.l1 * r1[1];
         const float m0 = sigmoidf_(xd0), m1 = sigmoidf_(xd1);
-        const float4 z = *reinterpret_cast<const float4*>(S + ((int64_t)k * Tspec + t) * 4);
+        const float4 z = *reinterpret_cast<const float4*>(S + (int64_t)k * 4);
         // masked_z = (mag*mask) * (z / (mag + 1e-8)); ch0: z_L with mag = Re z_L; ch1: z_R with mag = Im z_L
         const float ms0 = z.x * m0, ms1 = z.y * m1;
         const float d0 = z.x + 1e-8f, d1 = z.y + 1e-8f;

@@ -77,6 +77,7 @@ def main():
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dump-kernels", default=None, help="write the warmup step's per-kernel profile (JSON)")
     ap.add_argument("--kernel", default=None, help="roofline kernel (default: largest summed time in warmup)")
     args = ap.parse_args()
 
@@ -115,6 +116,11 @@ def main():
     dominant = args.kernel
     if args.warmup > 0:
         allk = model.profile_stop()
+        if args.dump_kernels and rank == 0:
+            for r in allk:
+                r["tflops"] = r["flops"] / (r["ms"] * 1e-3) / 1e12 if r["ms"] else 0.0
+                r["gbs"] = r["bytes"] / (r["ms"] * 1e-3) / 1e9 if r["ms"] else 0.0
+            json.dump(sorted(allk, key=lambda r: -r["ms"]), open(args.dump_kernels, "w"), indent=1)
         if dominant is None:
             dominant = max(allk, key=lambda r: r["ms"])["kernel"]
     if dominant is None:
@@ -181,6 +187,7 @@ def main():
         "stems_per_s": round(4 * value, 3),
         "roofline": roofline,
         "step_essential_tflops": round(step_tf, 2),
+        "workspace_gb": round(model._ws.numel() / 1e9, 2) if model._ws is not None else None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         rec["cpu_baseline"] = cpu_baseline(sd, table)

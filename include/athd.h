@@ -68,7 +68,7 @@ size_t athd_workspace_bytes(athd_ctx* ctx, int64_t B, int64_t T, int P);
 int athd_forward(athd_ctx* ctx, const float* wav, int64_t B, int64_t T, const float* text_emb, float* out,
                  void* workspace, size_t workspace_bytes, void* stream);
 
-/* Encode once, decode once per prompt: wav (B,2,T), text_table (P,512) -> out (B,P,2,T); equal to P calls of
+/* Encode once, decode once per prompt (1 <= P <= 256): wav (B,2,T), text_table (P,512) -> out (B,P,2,T); equal to P calls of
  * athd_forward because the encoder and cross-transformer do not see the prompt (ATHTDemucs_v2.py:278-283). */
 int athd_forward_prompts(athd_ctx* ctx, const float* wav, int64_t B, int64_t T, const float* text_table, int P,
                          float* out, void* workspace, size_t workspace_bytes, void* stream);
