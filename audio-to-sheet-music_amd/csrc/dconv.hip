@@ -7,7 +7,10 @@
 //   c1app:  x += scale * GLU(GN(y))     (y recomputed: K = H is tiny)
 // A "group" is the GroupNorm(1) sample: one nb row of L positions (freq rows (b,f) along time, or time samples).
 // Access pattern: c3 stages its x tile (+ dilation halo) in LDS with 16-B coalesced loads; c1app maps a lane to
-// (position, 8-channel chunk) so x is read and written with consecutive 16-B (bf16) / 32-B (f32) chunks.
+// (position, 32-B chunk of x), so x is read and written in consecutive 32-B chunks.  Per-group GroupNorm
+// parameters are finalised once per block into LDS.
+#include <algorithm>
+
 #include "common.h"
 #include "prof.h"
 #include "kernels.h"
@@ -122,6 +125,22 @@ ATHD_DEV void load_hg(const float* __restrict__ h, int64_t p, float mean, float 
     for (int j = 0; j < H; ++j) hv[j] = gelu<FAST>((h[p * H + j] - mean) * rstd * g1w[j] + g1b[j]);
 }
 
+// GroupNorm (mean, rstd) of the groups [g_first, g_first + n) a block touches, into LDS (n <= GN_TAB); the caller
+// synchronises.  Blocks touching more groups (very short rows) compute per thread.
+constexpr int GN_TAB = 8;
+ATHD_DEV void gn_table(const double* st, double cnt, int64_t g_first, int64_t n, float* tm, float* tr) {
+    if (n <= GN_TAB && (int64_t)threadIdx.x < n) gn_mr(st, g_first + threadIdx.x, cnt, tm[threadIdx.x], tr[threadIdx.x]);
+}
+ATHD_DEV void gn_lookup(const double* st, double cnt, int64_t g, int64_t g_first, int64_t n, const float* tm,
+                        const float* tr, float& mean, float& rstd) {
+    if (n <= GN_TAB) {
+        mean = tm[g - g_first];
+        rstd = tr[g - g_first];
+    } else {
+        gn_mr(st, g, cnt, mean, rstd);
+    }
+}
+
 // ---- c1stat: one thread per position; y (2C channels) only feeds the GroupNorm statistics
 template <int C, bool FAST>
 __global__ __launch_bounds__(256) void dconv_c1_stats_kernel(const float* __restrict__ h, int64_t nb, int64_t L,
@@ -131,20 +150,22 @@ __global__ __launch_bounds__(256) void dconv_c1_stats_kernel(const float* __rest
                                                              double* __restrict__ st_y) {
     constexpr int H = C / 8, N = 2 * C;
     __shared__ float wl[N * H];
-    __shared__ float bl[N], gw[H], gb[H];
+    __shared__ float bl[N], gw[H], gb[H], tm[GN_TAB], tr[GN_TAB];
     __shared__ double sh[16];
+    const int64_t P = nb * L;
+    const int64_t p0 = (int64_t)blockIdx.x * 256;
+    const int64_t gf = p0 / L, ng = (std::min<int64_t>(p0 + 255, P - 1)) / L - gf + 1;
     for (int i = threadIdx.x; i < N * H; i += 256) wl[i] = W[i];
     for (int i = threadIdx.x; i < N; i += 256) bl[i] = bias[i];
     if (threadIdx.x < H) { gw[threadIdx.x] = g1w[threadIdx.x]; gb[threadIdx.x] = g1b[threadIdx.x]; }
+    gn_table(st_h, (double)L * H, gf, ng, tm, tr);
     __syncthreads();
-    const int64_t P = nb * L;
-    const int64_t p0 = (int64_t)blockIdx.x * 256;
     const int64_t p = p0 + threadIdx.x;
     const bool valid = p < P;
     float s1 = 0.f, s2 = 0.f;
     if (valid) {
         float mean, rstd;
-        gn_mr(st_h, p / L, (double)L * H, mean, rstd);
+        gn_lookup(st_h, (double)L * H, p / L, gf, ng, tm, tr, mean, rstd);
         float hv[H];
         load_hg<H, FAST>(h, p, mean, rstd, gw, gb, hv);
 #pragma unroll 4
@@ -159,7 +180,7 @@ __global__ __launch_bounds__(256) void dconv_c1_stats_kernel(const float* __rest
     group_stats_add(st_y, p0, p, valid, L, s1, s2, sh);
 }
 
-// ---- c1app: one thread per (position, 8-channel chunk): x[p][c..c+8) += scale * GLU(GN(y))
+// ---- c1app: one thread per (position, 32-B chunk of x = CPT channels): x[p][c..c+CPT) += scale * GLU(GN(y))
 template <int C, typename TS, bool FAST>
 __global__ __launch_bounds__(256) void dconv_c1_apply_kernel(TS* __restrict__ x, const float* __restrict__ h, int64_t nb,
                                                              int64_t L, const double* __restrict__ st_h,
@@ -168,28 +189,35 @@ __global__ __launch_bounds__(256) void dconv_c1_apply_kernel(TS* __restrict__ x,
                                                              const double* __restrict__ st_y,
                                                              const float* __restrict__ g2w, const float* __restrict__ g2b,
                                                              const float* __restrict__ scale) {
-    constexpr int H = C / 8, N = 2 * C, CV = C / 8;
+    constexpr int H = C / 8, N = 2 * C;
+    constexpr int CPT = 32 / sizeof(TS), CV = C / CPT;
     __shared__ float wl[N * H];
     __shared__ float bl[N], gw2[N], gb2[N], scl[C], gw[H], gb[H];
+    __shared__ float tm1[GN_TAB], tr1[GN_TAB], tm2[GN_TAB], tr2[GN_TAB];
+    const int64_t P = nb * L;
+    const int64_t q0 = (int64_t)blockIdx.x * 256;
+    const int64_t pf = q0 / CV, pl = std::min<int64_t>((q0 + 255) / CV, P - 1);
+    const int64_t gf = pf / L, ng = pl / L - gf + 1;
     for (int i = threadIdx.x; i < N * H; i += 256) wl[i] = W[i];
     for (int i = threadIdx.x; i < N; i += 256) { bl[i] = bias[i]; gw2[i] = g2w[i]; gb2[i] = g2b[i]; }
     for (int i = threadIdx.x; i < C; i += 256) scl[i] = scale[i];
     if (threadIdx.x < H) { gw[threadIdx.x] = g1w[threadIdx.x]; gb[threadIdx.x] = g1b[threadIdx.x]; }
+    gn_table(st_h, (double)L * H, gf, ng, tm1, tr1);
+    gn_table(st_y, (double)L * N, gf, ng, tm2, tr2);
     __syncthreads();
-    const int64_t P = nb * L;
-    const int64_t gi = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t gi = q0 + threadIdx.x;
     if (gi >= P * CV) return;
     const int64_t p = gi / CV;
-    const int c0 = (int)(gi - p * CV) * 8;
+    const int c0 = (int)(gi - p * CV) * CPT;
     const int64_t g = p / L;
     float m1, r1, m2, r2;
-    gn_mr(st_h, g, (double)L * H, m1, r1);
-    gn_mr(st_y, g, (double)L * N, m2, r2);
+    gn_lookup(st_h, (double)L * H, g, gf, ng, tm1, tr1, m1, r1);
+    gn_lookup(st_y, (double)L * N, g, gf, ng, tm2, tr2, m2, r2);
     float hv[H];
     load_hg<H, FAST>(h, p, m1, r1, gw, gb, hv);
-    float o[8];
+    float o[CPT];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
+    for (int q = 0; q < CPT; ++q) {
         const int c = c0 + q;
         float a = bl[c], gt = bl[C + c];
 #pragma unroll
@@ -201,20 +229,19 @@ __global__ __launch_bounds__(256) void dconv_c1_apply_kernel(TS* __restrict__ x,
         gt = (gt - m2) * r2 * gw2[C + c] + gb2[C + c];
         o[q] = scl[c] * (a * sigmoidf_(gt));
     }
-    TS* xp = x + p * C + c0;
+    uint4* xp = reinterpret_cast<uint4*>(x + p * C + c0);
+    uint4 v[2] = {xp[0], xp[1]};
     if constexpr (sizeof(TS) == 2) {
-        uint4 v = *reinterpret_cast<const uint4*>(xp);
-        bf16_t* e = reinterpret_cast<bf16_t*>(&v);
+        bf16_t* e = reinterpret_cast<bf16_t*>(v);
 #pragma unroll
-        for (int q = 0; q < 8; ++q) e[q] = f2bf(bf2f(e[q]) + o[q]);
-        *reinterpret_cast<uint4*>(xp) = v;
+        for (int q = 0; q < CPT; ++q) e[q] = f2bf(bf2f(e[q]) + o[q]);
     } else {
-        float4 a = reinterpret_cast<const float4*>(xp)[0], b = reinterpret_cast<const float4*>(xp)[1];
-        a.x += o[0]; a.y += o[1]; a.z += o[2]; a.w += o[3];
-        b.x += o[4]; b.y += o[5]; b.z += o[6]; b.w += o[7];
-        reinterpret_cast<float4*>(xp)[0] = a;
-        reinterpret_cast<float4*>(xp)[1] = b;
+        float* e = reinterpret_cast<float*>(v);
+#pragma unroll
+        for (int q = 0; q < CPT; ++q) e[q] += o[q];
     }
+    xp[0] = v[0];
+    xp[1] = v[1];
 }
 
 template <int C, typename TS, bool FAST>
@@ -241,7 +268,7 @@ static void dconv_small_t(void* x, float* h, int64_t nb, int64_t L, int dil, con
     {
         KScope ks(s);
         if (ks.on()) ks.begin(klabel("dconv_c1_apply_kernel<%d,%s>", C, tn), 2.0 * px * 2 * C * H, px * (H * 4 + 2 * C * xb));
-        const int64_t n = P * (C / 8);
+        const int64_t n = P * (C / (32 / (int)sizeof(TS)));
         hipLaunchKernelGGL((dconv_c1_apply_kernel<C, TS, FAST>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
                            (TS*)x, h, nb, L, st_h, g1w, g1b, w1, b1, st_y, g2w, g2b, scale);
     }

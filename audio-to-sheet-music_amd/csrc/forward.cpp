@@ -48,6 +48,7 @@ Dims make_dims(int64_t B, int64_t T, int P) {
 struct Bufs {
     float* spec;
     float* specT;
+    float* wavT;
     double* stats;
     int64_t nstats;     // number of double pairs
     float *snorm, *tnorm_div, *tnorm_std;
@@ -80,6 +81,7 @@ size_t plan(Arena& ar, const Dims& d, Bufs& b, bool actbf) {
     b.stats = ar.take<double>(2 * ns);
     b.spec = ar.take<float>(B * 2048 * Ts * 4);
     b.specT = ar.take<float>(B * 2048 * Ts * 4);
+    b.wavT = ar.take<float>(B * d.T * 2);
     b.snorm = ar.take<float>(2 * B);
     b.tnorm_div = ar.take<float>(2 * B);
     b.tnorm_std = ar.take<float>(2 * B);
@@ -241,6 +243,7 @@ void encode(Run& r, const Dims& d, const Bufs& b, const float* wav) {
         pp.Lx = d.T + epl + epr;
     }
     stft_launch(wav, (int)B, d.T, pp, (int)Ts, c->tw, c->win, b.spec, b.specT, r.s);
+    wav_interleave_launch(wav, (int)B, d.T, b.wavT, r.s);
     double* st_spec = r.stats(B);
     double* st_wav = r.stats(B);
     stats_launch(b.spec, (int)B, 2048LL * Ts * 4, st_spec, r.s);
@@ -259,9 +262,12 @@ void encode(Run& r, const Dims& d, const Bufs& b, const float* wav) {
         const int C = e.cout;
         const int Fi = d.F[i], Fo = d.F[i + 1];
         GemmDesc g;
-        g.A = i == 0 ? (const void*)b.spec : (const void*)b.saved[i - 1];
+        g.A = i == 0 ? (const void*)b.specT : (const void*)b.saved[i - 1];
         g.a_bf16 = i == 0 ? 0 : eab;
         g.nb = (int)B; g.H_in = Fi; g.W = (int)Ts; g.C_in = e.cin; g.a_ld = e.cin;
+        if (i == 0) {   // frame-major spectrogram: the 8 freq taps x 4 channels of a row are 128 contiguous bytes
+            g.a_ld = 2048 * 4; g.a_hs = 4; g.a_bs = Ts * 2048 * 4;
+        }
         g.ntaps = 8; g.in_stride = 4; g.in_off = -2; g.dil = 1; g.H_out = Fo;
         g.a_norm = i == 0 ? b.snorm : nullptr;
         g.Wp = e.conv.w; g.N = C; g.K = e.conv.K; g.Kp = e.conv.Kp; g.bias = e.conv.bias;
@@ -281,7 +287,7 @@ void encode(Run& r, const Dims& d, const Bufs& b, const float* wav) {
         const int64_t Li = d.L[i], Lo = d.L[i + 1];
         GemmDesc gt;
         if (i == 0) {
-            gt.A = wav; gt.a_ld = 1; gt.a_cs = d.T; gt.a_bs = 2 * d.T; gt.a_norm = b.tnorm_div;
+            gt.A = b.wavT; gt.a_ld = 2; gt.a_hs = 2; gt.a_bs = 2 * d.T; gt.a_norm = b.tnorm_div;   // (B, T, 2)
         } else {
             gt.A = b.saved_t[i - 1]; gt.a_bf16 = eab; gt.a_ld = et.cin;
         }

@@ -22,6 +22,8 @@ struct GemmDesc {
     int a_ld = 0;             // elements between consecutive positions (>= C_in)
     int64_t a_cs = 1;         // elements between channels (1 = channels-last; the raw (B,2,T) waveform uses T)
     int64_t a_bs = -1;        // elements between batches (-1: H_in*W*a_ld)
+    int64_t a_hs = -1;        // elements between consecutive input rows h (-1: W*a_ld).  a_hs == C_in with dil == 1
+                              // makes the whole (tap, ci) K row contiguous ("flat K", used when C_in < 8)
     int ntaps = 1, in_stride = 1, in_off = 0, dil = 1;
     int H_out = 1;            // output rows computed per batch
     const float* a_norm = nullptr;    // optional per-batch {sub, div} on in-bounds A: (a - sub[b]) / div[b]

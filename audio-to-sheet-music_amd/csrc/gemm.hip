@@ -47,7 +47,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmDesc d) {
     const int64_t m0 = (int64_t)blockIdx.x * BM;
     const int n0 = blockIdx.y * BN;
     const int64_t a_bs = d.a_bs >= 0 ? d.a_bs : (int64_t)d.H_in * d.W * d.a_ld;
-    const int64_t rowpitch = (int64_t)d.W * d.a_ld;
+    const int64_t rowpitch = d.a_hs >= 0 ? d.a_hs : (int64_t)d.W * d.a_ld;
 
     // ---- per-thread A rows (fixed across k) ----
     const int kg = tid & 3;

@@ -39,7 +39,7 @@ __global__ __launch_bounds__(256) void gemm2_kernel(const GemmDesc d) {
     const int64_t m0 = (int64_t)blockIdx.x * BM;
     const int n0 = blockIdx.y * BN;
     const int64_t a_bs = d.a_bs >= 0 ? d.a_bs : (int64_t)d.H_in * d.W * d.a_ld;
-    const int64_t rowpitch = (int64_t)d.W * d.a_ld;
+    const int64_t rowpitch = d.a_hs >= 0 ? d.a_hs : (int64_t)d.W * d.a_ld;
     const int lrow = lane >> 3;                                // row within an 8-row instruction
     const int chunk = (lane & 7) ^ lrow;                       // global 16-B chunk this lane fetches
 
@@ -71,8 +71,9 @@ __global__ __launch_bounds__(256) void gemm2_kernel(const GemmDesc d) {
     const char* zero = reinterpret_cast<const char*>(g_zero_page);
     const int nk = d.Kp / 64;
 
+    const bool flat = d.C_in < 8;                             // (gemm2_supported: fp32 A, a_hs == C_in, dil 1)
     float4 ra[AQ][2];   // fp32-A staging
-    bool rv[AQ];        // staged element in bounds (normalisation applies to in-bounds values only)
+    unsigned rv[AQ];    // per-element in-bounds mask (normalisation applies to in-bounds values only; padding stays 0)
     (void)ra;
     (void)rv;
 
@@ -88,8 +89,31 @@ __global__ __launch_bounds__(256) void gemm2_kernel(const GemmDesc d) {
             if constexpr (A_BF16) {
                 const char* src = ok ? (const char*)d.A + off * 2 : zero;
                 __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(sA + (wave + 4 * q) * 1024), 16, 0, 0);
+            } else if (flat) {
+                // flat K (C_in < 8, taps contiguous): the 8 elements span taps tap .. tap + (ci + 7) / C_in
+                const int row_l = row + (ci + 7) / d.C_in * d.dil;
+                const bool ok_l = a_ok[q] && kok && row_l >= 0 && row_l < d.H_in;
+                if (ok && ok_l && k_cur + 8 <= d.K) {
+                    rv[q] = 0xFFu;
+                    const float4* p = reinterpret_cast<const float4*>((const float*)d.A + off);
+                    ra[q][0] = p[0];
+                    ra[q][1] = p[1];
+                } else {
+                    float v[8];
+                    unsigned m = 0u;
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        const int rj = row + (ci + j) / d.C_in * d.dil;
+                        const bool okj = a_ok[q] && k_cur + j < d.K && rj >= 0 && rj < d.H_in;
+                        v[j] = okj ? ((const float*)d.A)[off + j] : 0.f;
+                        m |= okj ? (1u << j) : 0u;
+                    }
+                    rv[q] = m;
+                    ra[q][0] = make_float4(v[0], v[1], v[2], v[3]);
+                    ra[q][1] = make_float4(v[4], v[5], v[6], v[7]);
+                }
             } else {
-                rv[q] = ok;
+                rv[q] = ok ? 0xFFu : 0u;
                 if (ok) {
                     const float4* p = reinterpret_cast<const float4*>((const float*)d.A + off);
                     ra[q][0] = p[0];
@@ -119,7 +143,7 @@ __global__ __launch_bounds__(256) void gemm2_kernel(const GemmDesc d) {
                 if (d.a_norm && rv[q]) {
                     const float sub = d.a_norm[2 * a_b[q]], dv = d.a_norm[2 * a_b[q] + 1];
 #pragma unroll
-                    for (int j = 0; j < 8; ++j) v[j] = (v[j] - sub) / dv;
+                    for (int j = 0; j < 8; ++j) v[j] = ((rv[q] >> j) & 1u) ? (v[j] - sub) / dv : 0.f;
                 }
                 bf16_t h[8];
 #pragma unroll
@@ -169,7 +193,10 @@ __global__ __launch_bounds__(256) void gemm2_kernel(const GemmDesc d) {
 }
 
 bool gemm2_supported(const GemmDesc& d) {
-    if (d.C_in % 8 != 0 || d.a_ld % 8 != 0 || d.a_cs != 1 || d.Kp % 64 != 0 || d.N < 48) return false;
+    const bool flat = d.C_in < 8 && 8 % d.C_in == 0 && !d.a_bf16 && d.a_hs == d.C_in && d.dil == 1;
+    if ((d.C_in % 8 != 0 && !flat) || d.a_ld % (flat ? d.C_in : 8) != 0 || d.a_cs != 1 || d.Kp % 64 != 0 || d.N < 48)
+        return false;
+    if (flat && (d.a_bs % 4 != 0 || d.a_ld % 4 != 0)) return false;      // 16-B aligned chunk starts
     if (d.a_bf16 && d.a_norm) return false;
     if (d.act == ACT_GLU && d.N % 32 != 0) return false;
     return true;

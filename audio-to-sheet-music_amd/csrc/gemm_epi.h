@@ -27,7 +27,7 @@ inline unsigned epi_flags(const GemmDesc& d) {
     if (d.gn_stats) f |= F_GN;
     if (d.row_add) f |= F_ROWADD;
     if (d.col_split) f |= F_SPLIT;
-    if (d.c_bf16) f |= F_CBF16;
+    if (d.c_bf16 && d.store) f |= F_CBF16;     // the output dtype is irrelevant when nothing is stored
     if (!d.store) f |= F_NOSTORE;
     return f;
 }
@@ -36,7 +36,8 @@ inline unsigned epi_flags(const GemmDesc& d) {
 #define ATHD_EPI_LIST(X)                                                                                         \
     X(0u) X(F_CBF16) X(F_GELU) X(F_GELU | F_CBF16) X(F_RES) X(F_RES | F_STATS) X(F_GLU) X(F_GLU | F_ROWADD)    \
     X(F_STATS | F_NOSTORE) X(F_GN | F_GLU | F_RES) X(F_STATS) X(F_SPLIT | F_STATS) X(F_SPLIT)                  \
-    X(F_SPLIT | F_STATS | F_CBF16) X(F_SPLIT | F_CBF16)
+    X(F_SPLIT | F_STATS | F_CBF16) X(F_SPLIT | F_CBF16) X(F_GLU | F_CBF16) X(F_GLU | F_ROWADD | F_CBF16)         \
+    X(F_GN | F_GLU | F_RES | F_CBF16)
 
 template <unsigned F>
 ATHD_DEV bool on(unsigned flag) { return (F & flag) != 0; }

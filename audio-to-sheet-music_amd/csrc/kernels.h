@@ -68,6 +68,8 @@ int dconv_small_launch(void* x, int x_bf16, float* h, int64_t nb, int64_t L, int
                        const float* b3, const float* g1w, const float* g1b, const float* w1, const float* b1,
                        const float* g2w, const float* g2b, const float* scale, double* st_h, double* st_y, hipStream_t s,
                        bool fast);
+// (B, 2, T) -> (B, T, 2)
+void wav_interleave_launch(const float* wav, int nb, int64_t T, float* out, hipStream_t s);
 // positional tables of the cross-transformer (computed on device with the fp32 op order of demucs)
 void pos2d_launch(float* out, int Fr, int T1, int C, hipStream_t s);   // out[(f*T1+t)][C]
 void pos1d_launch(float* out, int T2, int C, hipStream_t s);           // out[t][C]

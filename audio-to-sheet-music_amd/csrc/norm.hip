@@ -410,6 +410,23 @@ int dec_merge_launch(const MergeDesc& d, hipStream_t s) {
     return (int)hipGetLastError();
 }
 
+// --------------------------------------------------------------------------------------------- waveform layout
+// (B, 2, T) -> (B, T, 2): the time level-0 conv then reads its 8 taps x 2 channels as one contiguous K row
+__global__ __launch_bounds__(256) void wav_interleave_kernel(const float* __restrict__ wav, int64_t T,
+                                                             float* __restrict__ out) {
+    const int64_t b = blockIdx.y;
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t >= T) return;
+    const float* x = wav + b * 2 * T;
+    *reinterpret_cast<float2*>(out + (b * T + t) * 2) = make_float2(x[t], x[T + t]);
+}
+
+void wav_interleave_launch(const float* wav, int nb, int64_t T, float* out, hipStream_t s) {
+    KScope ks(s);
+    if (ks.on()) ks.begin("wav_interleave_kernel", 0.0, 2.0 * nb * 2 * T * 4);
+    hipLaunchKernelGGL(wav_interleave_kernel, dim3((unsigned)((T + 255) / 256), nb), dim3(256), 0, s, wav, T, out);
+}
+
 // --------------------------------------------------------------------------------------------- position tables
 __global__ void pos2d_kernel(float* out, int Fr, int T1, int C) {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
