@@ -73,8 +73,8 @@ class AudioTextHTDemucs:
         device = torch.device(device)
         if device.type != "cuda":
             raise RuntimeError("athd runs on a HIP device only (there is no CPU path)")
-        if device.index is None:
-            device = torch.device("cuda", torch.cuda.current_device())
+        if device.index is None:     # torch's current device (0 until torch.cuda is initialised; no init here)
+            device = torch.device("cuda", torch.cuda.current_device() if torch.cuda.is_initialized() else 0)
         if self.device != device:
             self._ctx = None
         self.device = device

@@ -22,6 +22,13 @@ ATHD_DEV void wait_vm() {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
+// XCD-aware tile order (cdna_hip_programming.md T1): workgroup i runs on XCD i % 8, so hand each XCD a contiguous
+// range of M tiles (bijective for any tile count) - neighbouring tiles share input rows (conv taps) in that L2.
+ATHD_DEV int xcd_remap(int i, int n) {
+    const int q = n / 8, r = n % 8, x = i % 8;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i / 8;
+}
+
 template <int BM, int BN, int WM, int WN, int STAGES, unsigned F>
 __global__ __launch_bounds__(WM * WN * 64) void gemm3_kernel(const GemmDesc d) {
     constexpr int NW = WM * WN;
@@ -38,7 +45,7 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm3_kernel(const GemmDesc d) {
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm0 = (wave / WN) * (BM / WM), wn0 = (wave % WN) * (BN / WN);
     const int64_t M = (int64_t)d.nb * d.H_out * d.W;
-    const int64_t m0 = (int64_t)blockIdx.x * BM;
+    const int64_t m0 = (int64_t)xcd_remap(blockIdx.x, gridDim.x) * BM;
     const int n0 = blockIdx.y * BN;
     const int64_t a_bs = d.a_bs >= 0 ? d.a_bs : (int64_t)d.H_in * d.W * d.a_ld;
     const int64_t rowpitch = d.a_hs >= 0 ? d.a_hs : (int64_t)d.W * d.a_ld;
@@ -166,11 +173,15 @@ static void launch3(const GemmDesc& d, hipStream_t s) {
     }
 }
 
-// variant: 0 = auto, 1 = 256x128 (8 waves, 3 stages), 2 = 128x128 (4 waves, 3 stages), 3 = 256x192 (8 waves, 2 st)
+// variant: 0 = auto, 1 = 256x128 (8 waves, 3 stages), 2 = 128x128 (4 waves, 3 stages), 3 = 256x192 (8 waves, 2 st),
+// 4 = 128x192 (4 waves, 2 stages: 80 KB LDS, 2 blocks/CU), 5 = 128x192 (4 waves, 3 stages), 6 = 128x96 (4 waves, 3 st)
 int gemm3_launch(const GemmDesc& d, hipStream_t s, int variant) {
     if (variant == 0) variant = (d.N % 192 == 0 && d.N % 128 != 0) ? 3 : 1;
     if (variant == 1) launch3<256, 128, 4, 2, 3>(d, s);
     else if (variant == 2) launch3<128, 128, 2, 2, 3>(d, s);
+    else if (variant == 4) launch3<128, 192, 2, 2, 2>(d, s);
+    else if (variant == 5) launch3<128, 192, 2, 2, 3>(d, s);
+    else if (variant == 6) launch3<128, 96, 2, 2, 3>(d, s);
     else launch3<256, 192, 4, 2, 2>(d, s);
     return (int)hipGetLastError();
 }

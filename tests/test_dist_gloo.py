@@ -88,13 +88,22 @@ def test_shard_range():
 
 
 def test_world2_gloo():
-    ctx = mp.get_context("fork")
+    # spawn, not fork: a child forked after the parent used torch's CPU thread pool can deadlock
+    ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
     ps = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in ps:
         p.start()
-    res = dict(q.get(timeout=120) for _ in ps)
-    for p in ps:
-        p.join(timeout=30)
+    res = {}
+    try:
+        for _ in ps:
+            r, msg = q.get(timeout=240)
+            res[r] = msg
+    finally:
+        for p in ps:
+            p.join(timeout=20)
+            if p.is_alive():
+                p.kill()
+                p.join(timeout=5)
     assert res == {0: "ok", 1: "ok"}, res

@@ -6,4 +6,4 @@ timeout -k 10 300 python tools/kbench.py attn > gpurun_out/kbench.log 2>&1
 rc=$?; grep -v amdgpu.ids gpurun_out/kbench.log | tail -12
 if [ $rc -ne 0 ]; then exit $rc; fi
 exec_rc=0
-bash ./gpu_job1.sh
+bash ./tools/gpu_job1.sh

@@ -23,6 +23,21 @@ int kb_gemm(int variant, const void* A, int a_bf16, const void* W, const float* 
     if (variant >= 30) return gemm3_launch(d, (hipStream_t)stream, variant - 30);
     return gemm_launch(d, 1, (hipStream_t)stream);
 }
+// ConvT residue-pair GEMM as the decoder runs it (kept mode, pair 0): A (nb, H, W, Cin) bf16, 2 taps (rows u-1, u),
+// N = 2*Cout columns split at Cout, only the high half stored into slot 2u of a (nb, 2H, W, Cout) bf16 output,
+// GroupNorm statistics per nb.
+int kb_convt(int variant, const void* A, const void* W, const float* bias, void* C, double* stats, int nb, int H,
+             int Wd, int Cin, int Cout, int Kp, void* stream) {
+    GemmDesc d;
+    d.A = A; d.a_bf16 = 1; d.nb = nb; d.H_in = H; d.W = Wd; d.C_in = Cin; d.a_ld = Cin;
+    d.ntaps = 2; d.in_stride = 1; d.in_off = -1; d.dil = 1; d.H_out = H;
+    d.Wp = W; d.N = 2 * Cout; d.K = 2 * Cin; d.Kp = Kp; d.bias = bias;
+    d.C = C; d.c_bf16 = 1; d.ldo = Cout; d.stats = stats; d.col_split = Cout;
+    d.H_out_total = 2 * H; d.o_stride = 2; d.o_off = 0; d.hi_row_off = 0; d.store_mask = 2;
+    if (variant == 2) return gemm2_launch(d, (hipStream_t)stream);
+    if (variant >= 30) return gemm3_launch(d, (hipStream_t)stream, variant - 30);
+    return gemm_launch(d, 1, (hipStream_t)stream);
+}
 int kb_attn(const void* qkv, int nb, int N, void* out, void* stream) {
     AttnDesc a;
     a.nb = nb; a.Nq = N; a.Nk = N; a.heads = 8; a.scale = 0.125f;

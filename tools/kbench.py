@@ -50,6 +50,32 @@ def gemm_case(M, N, K, act=0):
     print(f"GEMM M={M} N={N} K={K} act={act}: " + "  ".join(f"{k}: {v[0]:8.1f}us {v[1]:7.1f}TF err={v[2]:.1e}" for k, v in res.items()), flush=True)
 
 
+def convt_case(nb, H, Wd, Cin, Cout, variants):
+    dev = "cuda"
+    A = (torch.randn(nb, H, Wd, Cin, device=dev) * 0.5).to(torch.bfloat16)
+    K = 2 * Cin
+    Kp = (K + 63) // 64 * 64
+    W = torch.zeros(2 * Cout, Kp, device=dev, dtype=torch.bfloat16)
+    W[:, :K] = (torch.randn(2 * Cout, K, device=dev) * 0.05).to(torch.bfloat16)
+    bias = torch.randn(2 * Cout, device=dev) * 0.1
+    C = torch.zeros(nb, 2 * H, Wd, Cout, device=dev, dtype=torch.bfloat16)
+    st = torch.zeros(2 * nb, device=dev, dtype=torch.float64)
+    s = torch.cuda.current_stream().cuda_stream
+    flops = 2.0 * nb * H * Wd * 2 * Cout * K
+    # reference for row-slot 2u: columns >= Cout of [A[u-1] | A[u]] @ W^T + b
+    Ap = torch.cat([torch.zeros_like(A[:, :1]), A], dim=1)                    # row -1 = 0
+    X = torch.cat([Ap[:, :-1], Ap[:, 1:]], dim=-1).float()                    # (nb, H, Wd, 2Cin)
+    ref = (X @ W[:, :K].float().t() + bias)[..., Cout:]
+    out = []
+    for v in variants:
+        f = lambda: lib.kb_convt(v, vp(A.data_ptr()), vp(W.data_ptr()), vp(bias.data_ptr()), vp(C.data_ptr()),
+                                 vp(st.data_ptr()), nb, H, Wd, Cin, Cout, Kp, vp(s))
+        us = timeit(f)
+        err = (C[:, 0::2].float() - ref).abs().max().item() / (ref.abs().max().item() + 1e-9)
+        out.append(f"v{v}: {us:8.1f}us {flops / us / 1e6:6.1f}TF err={err:.1e}")
+    print(f"CONVT nb={nb} H={H} W={Wd} Cin={Cin} Cout={Cout}: " + "  ".join(out), flush=True)
+
+
 def attn_case(B, N):
     qkv = (torch.randn(B, N, 1536, device="cuda")).to(torch.bfloat16)
     out = torch.empty(B, N, 512, device="cuda", dtype=torch.bfloat16)
@@ -75,6 +101,11 @@ if __name__ == "__main__":
     torch.manual_seed(0)
     if "tr" in sys.argv[1:]:
         tr_probe()
+    if "convt" in sys.argv[1:]:
+        convt_case(64, 259, 259, 192, 96, (2, 33, 34, 35))
+        convt_case(64, 259, 259, 96, 48, (2, 34, 35, 36))
+        convt_case(64, 1034, 1, 384, 192, (2, 33, 34, 35))
+        sys.exit(0)
     if "attn" in sys.argv[1:]:
         attn_case(4, 200)
         attn_case(64, 2072)
