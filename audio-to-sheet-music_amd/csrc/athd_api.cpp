@@ -313,6 +313,15 @@ int athd_finalize(athd_ctx* c) {
                 }
                 dw.pair[pi] = c->up_gemm(pk, 2 * dw.cout, 2 * dw.cin, bb);
             }
+            if (br == 0 && i == 1) {                  // [k*cout + co][ci] for the re-associated level 1
+                std::vector<float> tk((size_t)8 * dw.cout * dw.cin);
+                for (int k = 0; k < 8; ++k)
+                    for (int co = 0; co < dw.cout; ++co)
+                        for (int ci = 0; ci < dw.cin; ++ci)
+                            tk[((size_t)k * dw.cout + co) * dw.cin + ci] = w[((size_t)ci * dw.cout + co) * 8 + k];
+                dw.taps = c->up_gemm(tk, 8 * dw.cout, dw.cin, {});
+                dw.bias = c->up_f32(b);
+            }
             if (i < 3) {
                 dw.gnw = c->up_key(p + ".1.weight");
                 dw.gnb = c->up_key(p + ".1.bias");

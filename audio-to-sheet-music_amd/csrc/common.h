@@ -73,6 +73,15 @@ ATHD_DEV LinIdx lin_index(int dst, int in_size, int out_size) {
     return r;
 }
 
+// GroupNorm(1) (mean, 1/sqrt(var + 1e-5)) of batch b from fp64 {sum, sumsq} over `count` elements
+ATHD_DEV void gn_params(const double* st, int64_t b, int64_t count, float& mean, float& rstd) {
+    const double m = st[2 * b] / (double)count;
+    double var = st[2 * b + 1] / (double)count - m * m;
+    if (var < 0) var = 0;
+    mean = (float)m;
+    rstd = (float)(1.0 / sqrt(var + 1e-5));
+}
+
 #define HIP_CHECK_RET(x)                                                       \
     do {                                                                       \
         hipError_t e_ = (x);                                                   \

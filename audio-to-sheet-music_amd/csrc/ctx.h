@@ -46,6 +46,8 @@ struct TLayerW {
 struct DecW {
     int cin = 0, cout = 0;
     GemmW pair[2];          // ConvTranspose residue pairs {0,1} (taps u-1,u) and {2,3} (taps u,u+1), N = 2*cout
+    GemmW taps;             // freq level 1 only: every tap as its own column block, N = 8*cout, K = cin (fdec_lr.hip)
+    float* bias = nullptr;  // freq level 1 only: ConvT bias [cout]
     float *gnw = nullptr, *gnb = nullptr;
 };
 

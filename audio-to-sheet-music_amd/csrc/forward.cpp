@@ -66,6 +66,7 @@ struct Bufs {
     float *U, *Yb, *x_cond, *xt_cond;
     void* Hm;
     float *G, *D, *FO, *frames;
+    void *Z, *Zs;       // freq level 1 re-associated (fdec_lr.hip): per-tap products of the 32 / 8 source rows
 };
 
 size_t plan(Arena& ar, const Dims& d, Bufs& b, bool actbf) {
@@ -127,6 +128,8 @@ size_t plan(Arena& ar, const Dims& d, Bufs& b, bool actbf) {
     dm = std::max(dm, d.L[1] * 48);
     dm = std::max(dm, d.T * 4);
     b.D = ar.take<float>(NI * dm);
+    b.Z = act(NI * 32 * Ts * 8 * DEC_CH[2]);
+    b.Zs = act(d.Bc * 8 * Ts * 8 * DEC_CH[2]);
     b.FO = ar.take<float>(NI * Ts * Ts * 2);
     b.frames = ar.take<float>(NI * Ts * 2 * 4096);
     return ar.off;
@@ -463,15 +466,31 @@ void decode_chunk(Run& r, const Dims& d, const Bufs& b, int64_t s0, int64_t Bc, 
         conv_t(r, c->fdec[0], b.x_cond, ab, NI, 8, (int)Ts, b.G, 0, st, -1, "fdec0");
         KStage kst("fdec0");
         gn_gelu_launch(b.G, NI, 32 * Ts * 192, 192, st, c->fdec[0].gnw, c->fdec[0].gnb, r.s, r.actbf);
-        MergeDesc m;
-        m.src = b.G; m.H_src = 32; m.kept = 0; m.C = 192;
-        m.skip = sv[3]; m.skip_bf16 = ab; m.H_skip = 8; m.C_skip = 384; m.P = P;
-        m.out = b.D; m.out_bf16 = ab; m.H_out = (int)Ts; m.W = (int)Ts; m.NI = NI;
-        r.check(dec_merge_launch(m, r.s), "dec_merge");
+        // level 1 from the 32-row S = GELU(GN(ConvT0)) without materialising the resized 259-row input
+        // (fdec_lr.hip): Z = S @ [W_0 .. W_7], Zs = skip3[:, :192] @ [W_0 .. W_7], then stats + merge passes
+        KStage kst1("fdec1");
+        const DecW& w1 = c->fdec[1];
+        GemmDesc gz;
+        gz.A = b.G; gz.a_bf16 = 0; gz.nb = NI; gz.H_in = 32; gz.W = (int)Ts; gz.C_in = w1.cin; gz.a_ld = w1.cin;
+        gz.H_out = 32; gz.Wp = w1.taps.w; gz.N = w1.taps.N; gz.K = w1.taps.K; gz.Kp = w1.taps.Kp;
+        gz.C = b.Z; gz.c_bf16 = ab; gz.H_out_total = 32; gz.ldo = w1.taps.N;
+        r.gemm(gz, "fdec1.z");
+        GemmDesc gs = gz;
+        gs.A = sv[3]; gs.a_bf16 = ab; gs.nb = (int)Bc; gs.H_in = 8; gs.H_out = 8; gs.H_out_total = 8; gs.a_ld = 384;
+        gs.C = b.Zs;
+        r.gemm(gs, "fdec1.zs");
+        LowRankDesc lr;
+        lr.Z = b.Z; lr.Zs = b.Zs; lr.z_bf16 = ab; lr.Hs = 32; lr.Hk = 8; lr.Hd = (int)Ts; lr.W = (int)Ts;
+        lr.Co = w1.cout; lr.P = P; lr.NI = NI; lr.bias = w1.bias; lr.stats = r.stats(NI);
+        lr.gn_w = w1.gnw; lr.gn_b = w1.gnb; lr.fast_gelu = ab;
+        lr.skip = sv[2]; lr.skip_bf16 = ab; lr.H_skip = 32; lr.C_skip = 192;
+        lr.out = b.D; lr.out_bf16 = ab;
+        r.check(fdec_lr_stats_launch(lr, r.s), "fdec_lr_stats");
+        r.check(fdec_lr_merge_launch(lr, r.s), "fdec_lr_merge");
         // levels 1..3: Tspec -> 4 Tspec rows; the /4 bilinear resize reads only rows 4d+1, 4d+2
         const int skH[3] = {32, 128, 512};
         const int skC[3] = {192, 96, 48};
-        for (int i = 1; i < 4; ++i) {
+        for (int i = 2; i < 4; ++i) {
             const DecW& w = c->fdec[i];
             const bool last = i == 3;
             double* sti = last ? nullptr : r.stats(NI);

@@ -62,6 +62,19 @@ struct MergeDesc {
     int fast_gelu = 0;                            // bf16 mode: branch-free erf
 };
 int dec_merge_launch(const MergeDesc& d, hipStream_t s);   // -1: P > 256 or NI % P != 0
+// fdec_lr.hip: FreqDecoder level 1 from the 32-row level-0 output (re-associated ConvT; see fdec_lr.hip).
+// Z [NI][Hs][W][8*Co] = W_k S[j] per tap k; Zs [NI/P][Hk][W][8*Co] = W_k skip3[m]; skip [NI/P][H_skip][W][C_skip].
+struct LowRankDesc {
+    const void* Z = nullptr; const void* Zs = nullptr; int z_bf16 = 0;
+    int Hs = 32, Hk = 8, Hd = 0, W = 0, Co = 0, P = 1, NI = 0;
+    const float* bias = nullptr;                  // ConvT bias [Co]
+    double* stats = nullptr;                      // per item {sum, sumsq} over the 4*Hd ConvT rows
+    const float* gn_w = nullptr; const float* gn_b = nullptr; int fast_gelu = 0;
+    const void* skip = nullptr; int skip_bf16 = 0; int H_skip = 0; int C_skip = 0;
+    void* out = nullptr; int out_bf16 = 0;        // [NI][Hd][W][Co]
+};
+int fdec_lr_stats_launch(const LowRankDesc& d, hipStream_t s);
+int fdec_lr_merge_launch(const LowRankDesc& d, hipStream_t s);
 // dconv.hip: one DConv layer (conv3 -> GN -> GELU -> 1x1 -> GN -> GLU -> LayerScale -> residual) for C in {48, 96}
 // x: [nb][L][C] f32 or bf16 (x_bf16), updated in place; h: [nb][L][C/8] f32 scratch
 int dconv_small_launch(void* x, int x_bf16, float* h, int64_t nb, int64_t L, int C, int dil, const float* w3,

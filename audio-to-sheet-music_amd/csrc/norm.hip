@@ -54,13 +54,6 @@ void input_norm_params_launch(const double* stats, int nb, int64_t n, float* mea
     hipLaunchKernelGGL(input_norm_params_kernel, dim3((nb + 63) / 64), dim3(64), 0, s, stats, nb, n, mean_div, mean_std);
 }
 
-ATHD_DEV void gn_params(const double* st, int64_t b, int64_t count, float& mean, float& rstd) {
-    const double m = st[2 * b] / (double)count;
-    double var = st[2 * b + 1] / (double)count - m * m;
-    if (var < 0) var = 0;
-    mean = (float)m;
-    rstd = (float)(1.0 / sqrt(var + 1e-5));
-}
 
 // --------------------------------------------------------------------------------------------- GroupNorm users
 template <bool FAST>

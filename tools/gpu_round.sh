@@ -7,7 +7,7 @@ mkdir -p $O
 export TMPDIR=/tmp
 step() { echo "== $1"; }
 step pytest
-timeout -k 10 900 python -m pytest tests -m gpu -q -rA -p no:cacheprovider > $O/pytest_gpu.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -rA -p no:cacheprovider --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1
 rc=$?; grep -E "passed|failed" $O/pytest_gpu.log | tail -2
 if [ $rc -gt 1 ]; then tail -30 $O/pytest_gpu.log; exit $rc; fi
 step bench
