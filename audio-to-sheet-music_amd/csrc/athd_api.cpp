@@ -214,6 +214,11 @@ int athd_finalize(athd_ctx* c) {
                         for (int ci = 0; ci < C; ++ci)
                             for (int t = 0; t < 3; ++t) t3[((size_t)j * 3 + t) * C + ci] = w3[((size_t)j * C + ci) * 3 + t];
                     e.dc.w3f[d] = c->up_f32(t3);
+                    if (c->mode == 1) {
+                        std::vector<float> t16((size_t)16 * 3 * C, 0.f);
+                        std::copy(t3.begin(), t3.end(), t16.begin());
+                        e.dc.c3p[d] = c->up_gemm(t16, 16, 3 * C, {});
+                    }
                     e.dc.w1f[d] = c->up_key(q + ".3.weight");        // [2C][H][1] == [2C][H]
                     e.dc.b1f[d] = c->up_key(q + ".3.bias");
                     e.dc.g2wf[d] = c->up_key(q + ".4.weight");

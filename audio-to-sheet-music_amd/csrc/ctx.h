@@ -24,6 +24,7 @@ struct GemmW {
 
 struct DConvW {
     GemmW c3[2], c1[2];
+    GemmW c3p[2];           // bf16 mode, C <= 96: conv3 with its C/8 rows zero-padded to 16 (fenc_row.hip MFMA tile)
     float *g1w[2], *g1b[2], *g2w[2], *g2b[2], *scale[2];
     // natural-order fp32 copies for the VALU kernels of the narrow levels (C <= 96): conv3 [H][3C] (tap-major k),
     // 1x1 [2C][H], its bias and GroupNorm affine

@@ -7,8 +7,10 @@
 //   T_u[k]   = W_k D0[u] = lerp(Z_k[i0(u)], Z_k[i1(u)]) + 0.1 * lerp(Zs_k[p0(u)], Zs_k[p1(u)])
 //   Y[4u+r]  = b + T_u[r+2] + (r < 2 ? T_{u-1}[r+6] : T_{u+1}[r-2])            (k = o + 2 - 4u)
 // This is the same arithmetic re-associated: 8x fewer MACs than the ConvT on Hd rows, and D0 never exists.
-// Two passes, both sweeping u in order per (item, w, 4 channels) with the Z rows the resize touches held in
-// registers (a row changes every ~Hd/32 steps):
+// Two passes, both sweeping u in order per (item, w, channel pair) with the Z rows the resize touches held in
+// registers (a row changes every ~Hd/32 steps) and the per-step resize indices read from an LDS table.  Both
+// passes are VALU-bound: the arithmetic runs on packed fp32 pairs (v_pk_fma_f32), the bias and the skip row
+// base are folded into one per-row-change base so a step costs two packed FMAs per tap:
 //   fdec_lr_stats_kernel: GroupNorm(1) {sum, sumsq} over all 4*Hd ConvT rows;
 //   fdec_lr_merge_kernel: rows 4d+1, 4d+2 (the only rows the exact /4 bilinear resize reads) -> GN -> GELU ->
 //                         lerp -> + 0.1 * resize_H(skip2) -> D1 [item][d][w][Co].
@@ -22,46 +24,106 @@ namespace athd {
 
 namespace {
 
-template <typename ZT>
-ATHD_DEV void ld4(const ZT* p, float* v) {
-    if constexpr (sizeof(ZT) == 2) {
-        const uint2 q = *reinterpret_cast<const uint2*>(p);
-        const bf16_t* h = reinterpret_cast<const bf16_t*>(&q);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] = bf2f(h[j]);
+typedef float f2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf2_t __attribute__((ext_vector_type(2)));
+
+ATHD_DEV f2 splat(float v) { return (f2){v, v}; }
+ATHD_DEV f2 pfma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+
+template <typename T>
+ATHD_DEV f2 ld2(const T* p) {
+    if constexpr (sizeof(T) == 2) {
+        const uint32_t q = *reinterpret_cast<const uint32_t*>(p);
+        return (f2){__uint_as_float(q << 16), __uint_as_float(q & 0xFFFF0000u)};
     } else {
-        const float4 a = *reinterpret_cast<const float4*>(p);
-        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+        return *reinterpret_cast<const f2*>(p);
     }
+}
+
+// GELU with the branch-free erf of common.h::erf_fast on a packed pair (bf16 mode), or exact erf (f32 mode)
+template <bool FAST>
+ATHD_DEV f2 gelu2(f2 x) {
+    if constexpr (!FAST) {
+        return (f2){gelu_erf(x.x), gelu_erf(x.y)};
+    } else {
+        const f2 u = x * splat(0.70710678118654752440f);
+        const f2 ax = (f2){fabsf(u.x), fabsf(u.y)};
+        const f2 den = pfma(splat(0.3275911f), ax, splat(1.0f));
+        const f2 t = (f2){__builtin_amdgcn_rcpf(den.x), __builtin_amdgcn_rcpf(den.y)};
+        f2 p = pfma(splat(1.061405429f), t, splat(-1.453152027f));
+        p = pfma(p, t, splat(1.421413741f));
+        p = pfma(p, t, splat(-0.284496736f));
+        p = pfma(p, t, splat(0.254829592f));
+        p = p * t;
+        const f2 q = ax * (ax * splat(-1.4426950408889634f));
+        const f2 e = (f2){__builtin_amdgcn_exp2f(q.x), __builtin_amdgcn_exp2f(q.y)};
+        const f2 em = pfma(-p, e, splat(1.0f));
+        const f2 erf = (f2){copysignf(em.x, u.x), copysignf(em.y, u.y)};
+        const f2 h = x * splat(0.5f);
+        return pfma(h, erf, h);
+    }
+}
+
+// Per-step resize indices of lin_index(v, in, Hd), tabulated once per block in LDS for v < LR_TAB.
+constexpr int LR_TAB = 1024;
+struct LrTab {
+    int ij;     // i0 | i1 << 16
+    float l1;
+};
+ATHD_DEV void lr_fill(LrTab* t, int n, int in, int out) {
+    for (int v = threadIdx.x; v < n && v < LR_TAB; v += blockDim.x) {
+        const LinIdx li = lin_index(v, in, out);
+        t[v].ij = li.i0 | (li.i1 << 16);
+        t[v].l1 = li.l1;
+    }
+}
+struct Lerp {
+    int i0, i1;
+    float l1;
+};
+ATHD_DEV Lerp lr_get(const LrTab* t, int v, int in, int out) {
+    Lerp r;
+    if (v < LR_TAB) {
+        const LrTab e = t[v];
+        const int ij = __builtin_amdgcn_readfirstlane(e.ij);
+        r.i0 = ij & 0xFFFF;
+        r.i1 = ij >> 16;
+        r.l1 = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(e.l1)));
+    } else {
+        const LinIdx li = lin_index(v, in, out);
+        r.i0 = li.i0;
+        r.i1 = li.i1;
+        r.l1 = li.l1;
+    }
+    return r;
 }
 
 // tap index of slot t: all 8 taps (stats pass) or {0, 3, 4, 7} (merge pass: rows 4d+1, 4d+2)
 template <int NT>
 ATHD_DEV constexpr int tap_of(int t) { return NT == 8 ? t : (t == 0 ? 0 : t == 1 ? 3 : t == 2 ? 4 : 7); }
 
-// The two rows (i0, i1) a lerp reads, as r0 = scale * row[i0] and dr = scale * (row[i1] - row[i0]) per tap slot.
+// The two rows (i0, i1) one lerp reads: r0 = scale * row[i0], dr = scale * (row[i1] - row[i0]) per tap slot, so the
+// lerp is fma(l1, dr, r0) (same value as l0 * a + l1 * b up to rounding; l0 = 1 - l1).
 template <typename ZT, int NT>
 struct LerpRows {
-    float r0[NT][4], dr[NT][4];
+    f2 r0[NT], dr[NT];
     int c0 = -1, c1 = -1;
-    ATHD_DEV void update(const ZT* base, int64_t rowpitch, int Co, const LinIdx& li, float scale) {
-        if (li.i0 == c0 && li.i1 == c1) return;
+    ATHD_DEV bool update(const ZT* base, int64_t rowpitch, int Co, const Lerp& li, float scale) {
+        if (li.i0 == c0 && li.i1 == c1) return false;
         c0 = li.i0;
         c1 = li.i1;
-        float a[NT][4], b[NT][4];
+        f2 a[NT], b[NT];
 #pragma unroll
-        for (int t = 0; t < NT; ++t) ld4(base + (int64_t)li.i0 * rowpitch + tap_of<NT>(t) * Co, a[t]);
+        for (int t = 0; t < NT; ++t) a[t] = ld2(base + (int64_t)li.i0 * rowpitch + tap_of<NT>(t) * Co);
 #pragma unroll
-        for (int t = 0; t < NT; ++t) ld4(base + (int64_t)li.i1 * rowpitch + tap_of<NT>(t) * Co, b[t]);
+        for (int t = 0; t < NT; ++t) b[t] = ld2(base + (int64_t)li.i1 * rowpitch + tap_of<NT>(t) * Co);
 #pragma unroll
-        for (int t = 0; t < NT; ++t)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                r0[t][j] = a[t][j] * scale;
-                dr[t][j] = (b[t][j] - a[t][j]) * scale;
-            }
+        for (int t = 0; t < NT; ++t) {
+            r0[t] = a[t] * splat(scale);
+            dr[t] = (b[t] - a[t]) * splat(scale);
+        }
+        return true;
     }
-    ATHD_DEV float at(int t, int j, float l1) const { return fmaf(l1, dr[t][j], r0[t][j]); }
 };
 
 struct LrThread {
@@ -71,11 +133,11 @@ struct LrThread {
 
 ATHD_DEV LrThread lr_thread(const LowRankDesc& d) {
     LrThread t;
-    const int cg = d.Co / 4;
+    const int cg = d.Co / 2;
     const int q = blockIdx.x * 256 + threadIdx.x;
     t.active = q < d.W * cg;
     t.w = t.active ? q / cg : 0;
-    t.c = t.active ? (q % cg) * 4 : 0;
+    t.c = t.active ? (q % cg) * 2 : 0;
     t.item = blockIdx.y;
     t.seg = t.item / d.P;
     return t;
@@ -85,57 +147,58 @@ ATHD_DEV LrThread lr_thread(const LowRankDesc& d) {
 
 template <typename ZT>
 __global__ __launch_bounds__(256) void fdec_lr_stats_kernel(const LowRankDesc d) {
+    __shared__ LrTab tz[LR_TAB], tk[LR_TAB];
+    lr_fill(tz, d.Hd, d.Hs, d.Hd);
+    lr_fill(tk, d.Hd, d.Hk, d.Hd);
+    __syncthreads();
     const LrThread th = lr_thread(d);
     const int N8 = 8 * d.Co;
     const int64_t rp = (int64_t)d.W * N8;
     const ZT* zb = (const ZT*)d.Z + (int64_t)th.item * d.Hs * rp + (int64_t)th.w * N8 + th.c;
     const ZT* sb = (const ZT*)d.Zs + (int64_t)th.seg * d.Hk * rp + (int64_t)th.w * N8 + th.c;
-    float bias[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) bias[j] = d.bias[th.c + j];
+    const f2 bias = ld2(d.bias + th.c);
     LerpRows<ZT, 8> zr, sr;
-    float prev[4][4] = {};     // T_{v-1}[4..7]
+    f2 base[8];                // r0(Z) + r0(Zs) (+ bias on taps 2..5: every output row has exactly one of those)
+    f2 prev[4] = {};           // T_{v-1}[4..7]
     double s1 = 0.0, s2 = 0.0;
     if (th.active) {
-        for (int v = 0; v <= d.Hd; ++v) {
-            float T[8][4];
-            if (v < d.Hd) {
-                const LinIdx a = lin_index(v, d.Hs, d.Hd);
-                const LinIdx k = lin_index(v, d.Hk, d.Hd);
-                zr.update(zb, rp, d.Co, a, 1.0f);
-                sr.update(sb, rp, d.Co, k, 0.1f);
+        for (int v0 = 0; v0 <= d.Hd; v0 += 16) {
+            f2 a1 = {}, a2 = {};
+            const int v1 = min(v0 + 16, d.Hd + 1);
+            for (int v = v0; v < v1; ++v) {
+                f2 T[8];
+                if (v < d.Hd) {
+                    const Lerp a = lr_get(tz, v, d.Hs, d.Hd);
+                    const Lerp k = lr_get(tk, v, d.Hk, d.Hd);
+                    const bool cz = zr.update(zb, rp, d.Co, a, 1.0f);
+                    const bool cs = sr.update(sb, rp, d.Co, k, 0.1f);
+                    if (cz || cs) {
 #pragma unroll
-                for (int t = 0; t < 8; ++t)
+                        for (int t = 0; t < 8; ++t) base[t] = zr.r0[t] + sr.r0[t] + ((t >= 2 && t <= 5) ? bias : f2{});
+                    }
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) T[t][j] = zr.at(t, j, a.l1) + sr.at(t, j, k.l1);
-            } else {
+                    for (int t = 0; t < 8; ++t) T[t] = pfma(splat(a.l1), zr.dr[t], pfma(splat(k.l1), sr.dr[t], base[t]));
+                } else {
 #pragma unroll
-                for (int t = 0; t < 8; ++t)
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) T[t][j] = 0.f;
-            }
-            float p1 = 0.f, p2 = 0.f;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                if (v >= 1) {     // rows 4(v-1)+2, 4(v-1)+3
-                    const float y2 = bias[j] + prev[0][j] + T[0][j];
-                    const float y3 = bias[j] + prev[1][j] + T[1][j];
-                    p1 += y2 + y3;
-                    p2 += y2 * y2 + y3 * y3;
+                    for (int t = 0; t < 8; ++t) T[t] = f2{};
                 }
-                if (v < d.Hd) {   // rows 4v, 4v+1
-                    const float y0 = bias[j] + T[2][j] + prev[2][j];
-                    const float y1 = bias[j] + T[3][j] + prev[3][j];
-                    p1 += y0 + y1;
-                    p2 += y0 * y0 + y1 * y1;
+                if (v >= 1) {          // rows 4(v-1)+2, 4(v-1)+3
+                    const f2 y2 = prev[0] + T[0];
+                    const f2 y3 = prev[1] + T[1];
+                    a1 += y2 + y3;
+                    a2 = pfma(y2, y2, pfma(y3, y3, a2));
                 }
+                if (v < d.Hd) {        // rows 4v, 4v+1
+                    const f2 y0 = T[2] + prev[2];
+                    const f2 y1 = T[3] + prev[3];
+                    a1 += y0 + y1;
+                    a2 = pfma(y0, y0, pfma(y1, y1, a2));
+                }
+#pragma unroll
+                for (int t = 0; t < 4; ++t) prev[t] = T[4 + t];
             }
-            s1 += (double)p1;
-            s2 += (double)p2;
-#pragma unroll
-            for (int t = 0; t < 4; ++t)
-#pragma unroll
-                for (int j = 0; j < 4; ++j) prev[t][j] = T[4 + t][j];
+            s1 += (double)a1.x + (double)a1.y;
+            s2 += (double)a2.x + (double)a2.y;
         }
     }
     s1 = wave_sum_d(s1);
@@ -152,6 +215,11 @@ __global__ __launch_bounds__(256) void fdec_lr_stats_kernel(const LowRankDesc d)
 
 template <typename ZT, bool FAST>
 __global__ __launch_bounds__(256) void fdec_lr_merge_kernel(const LowRankDesc d) {
+    __shared__ LrTab tz[LR_TAB], tk[LR_TAB], tj[LR_TAB];
+    lr_fill(tz, d.Hd, d.Hs, d.Hd);
+    lr_fill(tk, d.Hd, d.Hk, d.Hd);
+    lr_fill(tj, d.Hd, d.H_skip, d.Hd);
+    __syncthreads();
     const LrThread th = lr_thread(d);
     if (!th.active) return;
     const int N8 = 8 * d.Co;
@@ -160,93 +228,84 @@ __global__ __launch_bounds__(256) void fdec_lr_merge_kernel(const LowRankDesc d)
     const ZT* sb = (const ZT*)d.Zs + (int64_t)th.seg * d.Hk * rp + (int64_t)th.w * N8 + th.c;
     float mean, rstd;
     gn_params(d.stats, th.item, 4LL * d.Hd * d.W * d.Co, mean, rstd);
-    float bias[4], gw[4], gb[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        bias[j] = d.bias[th.c + j];
-        gw[j] = d.gn_w[th.c + j];
-        gb[j] = d.gn_b[th.c + j];
-    }
-    // skip2 [seg][H_skip][W][C_skip], channels [0, Co)
+    const f2 bias = ld2(d.bias + th.c);
+    const f2 gsc = ld2(d.gn_w + th.c) * splat(rstd);     // (y - mean) * rstd * w + b  as  (y - mean) * gsc + b
+    const f2 gb = ld2(d.gn_b + th.c);
+    // skip2 [seg][H_skip][W][C_skip], channels [0, Co): 0.1 * lerp, rows cached like the Z rows
     const int64_t kp = (int64_t)d.W * d.C_skip;
     const int64_t kb = (int64_t)th.seg * d.H_skip * kp + (int64_t)th.w * d.C_skip + th.c;
     int k0c = -1, k1c = -1;
-    float ka[4] = {}, kbv[4] = {};
+    f2 ka = {}, kd = {};
     const int64_t ob = (int64_t)th.item * d.Hd * d.W * d.Co + (int64_t)th.w * d.Co + th.c;
     const int64_t op = (int64_t)d.W * d.Co;
 
     LerpRows<ZT, 4> zr, sr;       // slots: taps 0, 3, 4, 7
-    float cur3[4] = {}, cur4[4] = {}, cur7[4] = {}, prev7[4] = {};
+    f2 base[4];
+    f2 cur3 = {}, cur4 = {}, cur7 = {}, prev7 = {};
     for (int v = 0; v <= d.Hd; ++v) {
-        float T[4][4];
+        f2 T[4];
         if (v < d.Hd) {
-            const LinIdx a = lin_index(v, d.Hs, d.Hd);
-            const LinIdx k = lin_index(v, d.Hk, d.Hd);
-            zr.update(zb, rp, d.Co, a, 1.0f);
-            sr.update(sb, rp, d.Co, k, 0.1f);
+            const Lerp a = lr_get(tz, v, d.Hs, d.Hd);
+            const Lerp k = lr_get(tk, v, d.Hk, d.Hd);
+            const bool cz = zr.update(zb, rp, d.Co, a, 1.0f);
+            const bool cs = sr.update(sb, rp, d.Co, k, 0.1f);
+            if (cz || cs) {
 #pragma unroll
-            for (int t = 0; t < 4; ++t)
+                for (int t = 0; t < 4; ++t) base[t] = zr.r0[t] + sr.r0[t] + ((t == 1 || t == 2) ? bias : f2{});
+            }
 #pragma unroll
-                for (int j = 0; j < 4; ++j) T[t][j] = zr.at(t, j, a.l1) + sr.at(t, j, k.l1);
+            for (int t = 0; t < 4; ++t) T[t] = pfma(splat(a.l1), zr.dr[t], pfma(splat(k.l1), sr.dr[t], base[t]));
         } else {
 #pragma unroll
-            for (int t = 0; t < 4; ++t)
-#pragma unroll
-                for (int j = 0; j < 4; ++j) T[t][j] = 0.f;
+            for (int t = 0; t < 4; ++t) T[t] = f2{};
         }
         if (v >= 1) {
-            const int dd = v - 1;     // output row: resize of ConvT rows 4dd+1 (i0) and 4dd+2 (i1)
-            const LinIdx rr = lin_index(dd, 4 * d.Hd, d.Hd);
-            const LinIdx lj = lin_index(dd, d.H_skip, d.Hd);
+            // output row dd: the exact /4 bilinear resize of the 4*Hd ConvT rows reads rows 4dd+1 and 4dd+2 with
+            // weights 0.5 / 0.5 (src = 4dd + 1.5, exact in fp32)
+            const int dd = v - 1;
+            const Lerp lj = lr_get(tj, dd, d.H_skip, d.Hd);
             if (lj.i0 != k0c || lj.i1 != k1c) {
                 k0c = lj.i0;
                 k1c = lj.i1;
+                f2 a, b;
                 if (d.skip_bf16) {
-                    ld4((const bf16_t*)d.skip + kb + (int64_t)lj.i0 * kp, ka);
-                    ld4((const bf16_t*)d.skip + kb + (int64_t)lj.i1 * kp, kbv);
+                    a = ld2((const bf16_t*)d.skip + kb + (int64_t)lj.i0 * kp);
+                    b = ld2((const bf16_t*)d.skip + kb + (int64_t)lj.i1 * kp);
                 } else {
-                    ld4((const float*)d.skip + kb + (int64_t)lj.i0 * kp, ka);
-                    ld4((const float*)d.skip + kb + (int64_t)lj.i1 * kp, kbv);
+                    a = ld2((const float*)d.skip + kb + (int64_t)lj.i0 * kp);
+                    b = ld2((const float*)d.skip + kb + (int64_t)lj.i1 * kp);
                 }
+                ka = a * splat(0.1f);
+                kd = (b - a) * splat(0.1f);
             }
-            float o[4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const float y1 = bias[j] + cur3[j] + prev7[j];
-                const float y2 = bias[j] + cur4[j] + T[0][j];
-                const float g1 = gelu<FAST>((y1 - mean) * rstd * gw[j] + gb[j]);
-                const float g2 = gelu<FAST>((y2 - mean) * rstd * gw[j] + gb[j]);
-                const float sv = (lj.l0 * ka[j] + lj.l1 * kbv[j]) * 0.1f;
-                o[j] = (rr.l0 * g1 + rr.l1 * g2) + sv;
-            }
+            const f2 y1 = cur3 + prev7;
+            const f2 y2 = cur4 + T[0];
+            const f2 g1 = gelu2<FAST>(pfma(y1 - splat(mean), gsc, gb));
+            const f2 g2 = gelu2<FAST>(pfma(y2 - splat(mean), gsc, gb));
+            const f2 o = pfma(g1 + g2, splat(0.5f), pfma(splat(lj.l1), kd, ka));
             const int64_t oi = ob + (int64_t)dd * op;
             if (d.out_bf16) {
-                bf16_t h[4];
-#pragma unroll
-                for (int j = 0; j < 4; ++j) h[j] = f2bf(o[j]);
-                *reinterpret_cast<uint2*>((bf16_t*)d.out + oi) = *reinterpret_cast<uint2*>(h);
+                const bf2_t h = __builtin_convertvector(o, bf2_t);
+                *reinterpret_cast<bf2_t*>((bf16_t*)d.out + oi) = h;
             } else {
-                *reinterpret_cast<float4*>((float*)d.out + oi) = make_float4(o[0], o[1], o[2], o[3]);
+                *reinterpret_cast<f2*>((float*)d.out + oi) = o;
             }
         }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            prev7[j] = cur7[j];
-            cur3[j] = T[1][j];
-            cur4[j] = T[2][j];
-            cur7[j] = T[3][j];
-        }
+        prev7 = cur7;
+        cur3 = T[1];
+        cur4 = T[2];
+        cur7 = T[3];
     }
 }
 
 static bool lr_ok(const LowRankDesc& d) {
-    return d.Z && d.Zs && d.bias && d.stats && d.Co % 4 == 0 && d.Hd > 0 && d.W > 0 && d.P > 0 && d.NI % d.P == 0 &&
-           d.Hs > 0 && d.Hk > 0;
+    return d.Z && d.Zs && d.bias && d.stats && d.Co % 2 == 0 && d.Hd > 0 && d.Hd < 65536 && d.W > 0 && d.P > 0 &&
+           d.NI % d.P == 0 && d.Hs > 0 && d.Hk > 0;
 }
 
 int fdec_lr_stats_launch(const LowRankDesc& d, hipStream_t s) {
     if (!lr_ok(d)) return -1;
-    const dim3 grid((unsigned)((d.W * (d.Co / 4) + 255) / 256), (unsigned)d.NI);
+    const dim3 grid((unsigned)((d.W * (d.Co / 2) + 255) / 256), (unsigned)d.NI);
     KScope ks(s);
     if (ks.on()) {
         // unique bytes: Z of every item + Zs of every segment, read once
@@ -260,8 +319,10 @@ int fdec_lr_stats_launch(const LowRankDesc& d, hipStream_t s) {
 }
 
 int fdec_lr_merge_launch(const LowRankDesc& d, hipStream_t s) {
-    if (!lr_ok(d) || !d.gn_w || !d.gn_b || !d.skip || !d.out || d.C_skip < d.Co || d.C_skip % 4 != 0) return -1;
-    const dim3 grid((unsigned)((d.W * (d.Co / 4) + 255) / 256), (unsigned)d.NI);
+    if (!lr_ok(d) || !d.gn_w || !d.gn_b || !d.skip || !d.out || d.C_skip < d.Co || d.C_skip % 2 != 0 ||
+        d.H_skip <= 0)
+        return -1;
+    const dim3 grid((unsigned)((d.W * (d.Co / 2) + 255) / 256), (unsigned)d.NI);
     KScope ks(s);
     if (ks.on()) {
         // unique bytes: half the taps of Z / Zs, the skip rows the resize touches (once per segment), the output

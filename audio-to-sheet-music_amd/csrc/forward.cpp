@@ -66,7 +66,7 @@ struct Bufs {
     float *U, *Yb, *x_cond, *xt_cond;
     void* Hm;
     float *G, *D, *FO, *frames;
-    void *Z, *Zs;       // freq level 1 re-associated (fdec_lr.hip): per-tap products of the 32 / 8 source rows
+    void *S, *Z, *Zs;   // freq level 1 re-associated (fdec_lr.hip): per-tap products of the 32 / 8 source rows
 };
 
 size_t plan(Arena& ar, const Dims& d, Bufs& b, bool actbf) {
@@ -128,6 +128,7 @@ size_t plan(Arena& ar, const Dims& d, Bufs& b, bool actbf) {
     dm = std::max(dm, d.L[1] * 48);
     dm = std::max(dm, d.T * 4);
     b.D = ar.take<float>(NI * dm);
+    b.S = act(NI * 32 * Ts * DEC_CH[1]);
     b.Z = act(NI * 32 * Ts * 8 * DEC_CH[2]);
     b.Zs = act(d.Bc * 8 * Ts * 8 * DEC_CH[2]);
     b.FO = ar.take<float>(NI * Ts * Ts * 2);
@@ -225,6 +226,9 @@ void dconv(Run& r, const EncW& e, const Bufs& b, void* x, int64_t nb, int64_t L)
     }
 }
 
+// the fused narrow freq level (fenc_row.hip) applies: bf16 mode, C in {48, 96}, T <= 272, padded conv3 packed
+bool br_fused(const EncW& e, int Ts) { return e.dc.c3p[0].w && e.dc.c3p[1].w && fenc_row_supported(e.cin, e.cout, Ts); }
+
 void encode(Run& r, const Dims& d, const Bufs& b, const float* wav) {
     athd_ctx* c = r.c;
     const int64_t B = d.B, Ts = d.Tspec;
@@ -264,6 +268,25 @@ void encode(Run& r, const Dims& d, const Bufs& b, const float* wav) {
         const EncW& e = c->fenc[i];
         const int C = e.cout;
         const int Fi = d.F[i], Fo = d.F[i + 1];
+        if (r.actbf && br_fused(e, (int)Ts)) {
+            // narrow level: conv + GELU + DConv + rewrite GLU in one kernel per (b, f) row (fenc_row.hip)
+            FencRowDesc fr;
+            fr.in = i == 0 ? (const void*)b.specT : (const void*)b.saved[i - 1];
+            fr.a_norm = i == 0 ? b.snorm : nullptr;
+            fr.B = (int)B; fr.Fin = Fi; fr.Fout = Fo; fr.T = (int)Ts;
+            fr.wc = (const uint16_t*)e.conv.w; fr.wc_ld = e.conv.Kp; fr.bc = e.conv.bias;
+            for (int dd = 0; dd < 2; ++dd) {
+                fr.w3[dd] = (const uint16_t*)e.dc.c3p[dd].w; fr.w3_ld = e.dc.c3p[dd].Kp; fr.b3[dd] = e.dc.c3[dd].bias;
+                fr.g1w[dd] = e.dc.g1w[dd]; fr.g1b[dd] = e.dc.g1b[dd];
+                fr.w1[dd] = (const uint16_t*)e.dc.c1[dd].w; fr.w1_ld = e.dc.c1[dd].Kp; fr.b1[dd] = e.dc.c1[dd].bias;
+                fr.g2w[dd] = e.dc.g2w[dd]; fr.g2b[dd] = e.dc.g2b[dd]; fr.scale[dd] = e.dc.scale[dd];
+            }
+            fr.wr = (const uint16_t*)e.rewrite.w; fr.wr_ld = e.rewrite.Kp; fr.br = e.rewrite.bias;
+            fr.row_add = i == 0 ? c->femb : nullptr;
+            fr.out = (uint16_t*)b.saved[i];
+            KSite site("fenc_row");
+            r.check(fenc_row_launch(fr, e.cin, C, r.s), "fenc_row");
+        } else {
         GemmDesc g;
         g.A = i == 0 ? (const void*)b.specT : (const void*)b.saved[i - 1];
         g.a_bf16 = i == 0 ? 0 : eab;
@@ -283,6 +306,7 @@ void encode(Run& r, const Dims& d, const Bufs& b, const float* wav) {
         gr.C = b.saved[i]; gr.c_bf16 = eab; gr.H_out_total = Fo; gr.ldo = C; gr.act = ACT_GLU;
         gr.row_add = i == 0 ? c->femb : nullptr;    // + freq_emb_scale * freq_emb(frs) (ATHTDemucs_v2.py:212-215)
         r.gemm(gr, "fenc.rewrite");
+        }
 
         // time branch: right zero-pad to a multiple of 4 is implicit (rows >= L read as 0)
         KStage tstage(kTenc[i]);
@@ -465,13 +489,15 @@ void decode_chunk(Run& r, const Dims& d, const Bufs& b, int64_t s0, int64_t Bc, 
         double* st = r.stats(NI);
         conv_t(r, c->fdec[0], b.x_cond, ab, NI, 8, (int)Ts, b.G, 0, st, -1, "fdec0");
         KStage kst("fdec0");
-        gn_gelu_launch(b.G, NI, 32 * Ts * 192, 192, st, c->fdec[0].gnw, c->fdec[0].gnb, r.s, r.actbf);
+        // S = GELU(GN(ConvT0)): in place (fp32 mode) or as a bf16 copy, the A operand of the level-1 tap GEMM
+        if (r.actbf) gn_gelu_bf16_launch(b.G, (uint16_t*)b.S, NI, 32 * Ts * 192, 192, st, c->fdec[0].gnw, c->fdec[0].gnb, r.s);
+        else gn_gelu_launch(b.G, NI, 32 * Ts * 192, 192, st, c->fdec[0].gnw, c->fdec[0].gnb, r.s, false);
         // level 1 from the 32-row S = GELU(GN(ConvT0)) without materialising the resized 259-row input
         // (fdec_lr.hip): Z = S @ [W_0 .. W_7], Zs = skip3[:, :192] @ [W_0 .. W_7], then stats + merge passes
         KStage kst1("fdec1");
         const DecW& w1 = c->fdec[1];
         GemmDesc gz;
-        gz.A = b.G; gz.a_bf16 = 0; gz.nb = NI; gz.H_in = 32; gz.W = (int)Ts; gz.C_in = w1.cin; gz.a_ld = w1.cin;
+        gz.A = r.actbf ? b.S : (const void*)b.G; gz.a_bf16 = ab; gz.nb = NI; gz.H_in = 32; gz.W = (int)Ts; gz.C_in = w1.cin; gz.a_ld = w1.cin;
         gz.H_out = 32; gz.Wp = w1.taps.w; gz.N = w1.taps.N; gz.K = w1.taps.K; gz.Kp = w1.taps.Kp;
         gz.C = b.Z; gz.c_bf16 = ab; gz.H_out_total = 32; gz.ldo = w1.taps.N;
         r.gemm(gz, "fdec1.z");

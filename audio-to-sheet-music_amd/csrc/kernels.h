@@ -32,6 +32,9 @@ void input_norm_params_launch(const double* stats, int nb, int64_t n, float* mea
 // h[nb][L*H] = GELU(GN(h)) in place (GroupNorm(1,H), stats over L*H per nb)
 void gn_gelu_launch(float* h, int nb, int64_t per_batch, int H, const double* stats, const float* w,
                     const float* b, hipStream_t s, bool fast);
+// out[nb][per_batch] (bf16) = GELU_fast(GN(h)); per_batch % 8 == 0, H % 8 == 0
+void gn_gelu_bf16_launch(const float* h, uint16_t* out, int nb, int64_t per_batch, int H, const double* stats,
+                         const float* w, const float* b, hipStream_t s);
 // x[nb][N][C] = GN(x) in place
 void gn_apply_launch(float* x, int nb, int64_t N, int C, const double* stats, const float* w, const float* b,
                      hipStream_t s);
@@ -75,6 +78,26 @@ struct LowRankDesc {
 };
 int fdec_lr_stats_launch(const LowRankDesc& d, hipStream_t s);
 int fdec_lr_merge_launch(const LowRankDesc& d, hipStream_t s);
+// fenc_row.hip: a whole narrow frequency-encoder level (conv + GELU + DConv + rewrite GLU) per (b, f) row, bf16 mode
+constexpr int FR_MT_MAX = 17;        // T <= 272 positions (16-position tiles)
+struct FencRowDesc {
+    const void* in = nullptr;          // level 0: specT f32 [B][T][Fin][4]; level 1: bf16 [B][Fin][T][Cin]
+    const float* a_norm = nullptr;     // level 0: per batch {sub, div}
+    int B = 0, Fin = 0, Fout = 0, T = 0;
+    const uint16_t* wc = nullptr; int wc_ld = 0; const float* bc = nullptr;        // conv [C][8 Cin]
+    const uint16_t* w3[2] = {nullptr, nullptr}; int w3_ld = 0;                    // conv3 [16][3C] (rows >= C/8 zero)
+    const float* b3[2] = {nullptr, nullptr};
+    const float* g1w[2] = {nullptr, nullptr}; const float* g1b[2] = {nullptr, nullptr};
+    const uint16_t* w1[2] = {nullptr, nullptr}; int w1_ld = 0;                    // 1x1 [2C][C/8] GLU-interleaved
+    const float* b1[2] = {nullptr, nullptr};
+    const float* g2w[2] = {nullptr, nullptr}; const float* g2b[2] = {nullptr, nullptr};   // packed order
+    const float* scale[2] = {nullptr, nullptr};
+    const uint16_t* wr = nullptr; int wr_ld = 0; const float* br = nullptr;      // rewrite [2C][C] GLU-interleaved
+    const float* row_add = nullptr;    // level 0: freq embedding [Fout][C]
+    uint16_t* out = nullptr;           // [B][Fout][T][C] bf16
+};
+bool fenc_row_supported(int cin, int c, int T);
+int fenc_row_launch(const FencRowDesc& d, int cin, int c, hipStream_t s);
 // dconv.hip: one DConv layer (conv3 -> GN -> GELU -> 1x1 -> GN -> GLU -> LayerScale -> residual) for C in {48, 96}
 // x: [nb][L][C] f32 or bf16 (x_bf16), updated in place; h: [nb][L][C/8] f32 scratch
 int dconv_small_launch(void* x, int x_bf16, float* h, int64_t nb, int64_t L, int C, int dil, const float* w3,

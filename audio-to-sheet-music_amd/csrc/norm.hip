@@ -71,6 +71,37 @@ __global__ __launch_bounds__(256) void gn_gelu_kernel(float* __restrict__ h, int
     }
 }
 
+// bf16-mode variant writing a separate bf16 copy (the fp32 input stays intact): 8 elements per thread
+__global__ __launch_bounds__(256) void gn_gelu_bf16_kernel(const float* __restrict__ h, bf16_t* __restrict__ out,
+                                                           int64_t per_batch, int H, const double* __restrict__ st,
+                                                           const float* __restrict__ w, const float* __restrict__ bb) {
+    const int64_t b = blockIdx.y;
+    float mean, rstd;
+    gn_params(st, b, per_batch, mean, rstd);
+    const float* p = h + b * per_batch;
+    bf16_t* o = out + b * per_batch;
+    const int n8 = (int)(per_batch / 8);
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < n8; i += gridDim.x * 256) {
+        const float4 u = *reinterpret_cast<const float4*>(p + 8 * (int64_t)i);
+        const float4 v = *reinterpret_cast<const float4*>(p + 8 * (int64_t)i + 4);
+        const float x[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
+        const int c0 = (8 * i) % H;
+        bf16_t r[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) r[j] = f2bf(gelu_fast((x[j] - mean) * rstd * w[c0 + j] + bb[c0 + j]));
+        *reinterpret_cast<uint4*>(o + 8 * (int64_t)i) = *reinterpret_cast<const uint4*>(r);
+    }
+}
+
+void gn_gelu_bf16_launch(const float* h, bf16_t* out, int nb, int64_t per_batch, int H, const double* stats,
+                         const float* w, const float* b, hipStream_t s) {
+    int blocks = (int)((per_batch / 8 + 255) / 256);
+    if (blocks > 1024) blocks = 1024;
+    KScope ks(s);
+    if (ks.on()) ks.begin("gn_gelu_bf16_kernel", 0.0, (double)nb * per_batch * (4 + 2));
+    hipLaunchKernelGGL(gn_gelu_bf16_kernel, dim3(blocks, nb), dim3(256), 0, s, h, out, per_batch, H, stats, w, b);
+}
+
 void gn_gelu_launch(float* h, int nb, int64_t per_batch, int H, const double* stats, const float* w, const float* b,
                     hipStream_t s, bool fast) {
     int blocks = (int)((per_batch + 255) / 256);
