@@ -318,6 +318,23 @@ int athd_finalize(athd_ctx* c) {
                 }
                 dw.pair[pi] = c->up_gemm(pk, 2 * dw.cout, 2 * dw.cin, bb);
             }
+            if (i == 2) {                             // one GEMM for all four residues (zero blocks where a
+                const int co4 = 4 * dw.cout, K3 = 3 * dw.cin;   // residue does not read that row)
+                std::vector<float> q((size_t)co4 * K3, 0.f);
+                std::vector<float> qb(co4);
+                for (int r = 0; r < 4; ++r) {
+                    const int ta = RES_OFF[r] + 1;    // K column block of row u + RES_OFF[r]
+                    for (int co = 0; co < dw.cout; ++co) {
+                        const size_t row = (size_t)(r * dw.cout + co) * K3;
+                        for (int ci = 0; ci < dw.cin; ++ci) {
+                            q[row + (size_t)ta * dw.cin + ci] = w[((size_t)ci * dw.cout + co) * 8 + RES_K0[r]];
+                            q[row + (size_t)(ta + 1) * dw.cin + ci] = w[((size_t)ci * dw.cout + co) * 8 + RES_K1[r]];
+                        }
+                        qb[r * dw.cout + co] = b[co];
+                    }
+                }
+                dw.quad = c->up_gemm(q, co4, K3, qb);
+            }
             if (br == 0 && i == 1) {                  // [k*cout + co][ci] for the re-associated level 1
                 std::vector<float> tk((size_t)8 * dw.cout * dw.cin);
                 for (int k = 0; k < 8; ++k)
@@ -337,6 +354,42 @@ int athd_finalize(athd_ctx* c) {
     c->fout_b = c->up_key("freq_out.bias");
     c->tout_w = c->up_key("time_out.weight");
     c->tout_b = c->up_key("time_out.bias");
+    // ---- last decoder levels folded with their 1x1 output projections (dec_last.hip), in double ----
+    for (int br = 0; br < 2; ++br) {
+        const std::string p = std::string(br == 0 ? "freq_decoder" : "time_decoder") + ".layers.3.0.";
+        const auto& w = c->W(p + "weight").v;      // [48][4][8]
+        const auto& b = c->W(p + "bias").v;        // [4]
+        const auto& P = c->W(br == 0 ? "freq_out.weight" : "time_out.weight").v;   // [2][4]
+        const auto& pb = c->W(br == 0 ? "freq_out.bias" : "time_out.bias").v;      // [2]
+        const int cin = DEC_CH[3], co = DEC_CH[4];
+        auto pw = [&](int j, int ci, int k) {     // (P W_k)[j][ci]
+            double a = 0.0;
+            for (int cc = 0; cc < co; ++cc) a += (double)P[j * co + cc] * w[((size_t)ci * co + cc) * 8 + k];
+            return a;
+        };
+        double pbias[2];
+        for (int j = 0; j < 2; ++j) {
+            pbias[j] = 0.0;
+            for (int cc = 0; cc < co; ++cc) pbias[j] += (double)P[j * co + cc] * b[cc];
+        }
+        std::vector<float> f;
+        if (br == 0) {   // Am = P W7 / 2, A0 = P (W3 + W4) / 2, Ap = P W0 / 2; P b + pb; 0.1 P
+            for (int m = 0; m < 3; ++m)
+                for (int j = 0; j < 2; ++j)
+                    for (int ci = 0; ci < cin; ++ci)
+                        f.push_back((float)(0.5 * (m == 0 ? pw(j, ci, 7) : m == 1 ? pw(j, ci, 3) + pw(j, ci, 4) : pw(j, ci, 0))));
+            for (int j = 0; j < 2; ++j) f.push_back((float)(pbias[j] + pb[j]));
+        } else {         // Q_k = P W_k; P b; tb; 0.1 P
+            for (int k = 0; k < 8; ++k)
+                for (int j = 0; j < 2; ++j)
+                    for (int ci = 0; ci < cin; ++ci) f.push_back((float)pw(j, ci, k));
+            for (int j = 0; j < 2; ++j) f.push_back((float)pbias[j]);
+            for (int j = 0; j < 2; ++j) f.push_back(pb[j]);
+        }
+        for (int j = 0; j < 2; ++j)
+            for (int cc = 0; cc < co; ++cc) f.push_back((float)(0.1 * P[j * co + cc]));
+        (br == 0 ? c->flast : c->tlast) = c->up_f32(f);
+    }
     // ---- FFT twiddles and the periodic Hann window (torch.hann_window(4096)) ----
     {
         std::vector<float2> tw(4096);

@@ -47,6 +47,7 @@ struct TLayerW {
 struct DecW {
     int cin = 0, cout = 0;
     GemmW pair[2];          // ConvTranspose residue pairs {0,1} (taps u-1,u) and {2,3} (taps u,u+1), N = 2*cout
+    GemmW quad;             // levels 2: all four residues in one GEMM, rows [rho * cout + co], K = [row u-1 | u | u+1]
     GemmW taps;             // freq level 1 only: every tap as its own column block, N = 8*cout, K = cin (fdec_lr.hip)
     float* bias = nullptr;  // freq level 1 only: ConvT bias [cout]
     float *gnw = nullptr, *gnb = nullptr;
@@ -106,6 +107,8 @@ struct athd_ctx {
     GemmW mlp0, mlp2;
     DecW fdec[4], tdec[4];
     float *fout_w, *fout_b, *tout_w, *tout_b;
+    float* flast = nullptr;          // folded last freq level + freq_out (dec_last.hip)
+    float* tlast = nullptr;          // folded last time level + time_out
     float2* tw = nullptr;
     float* win = nullptr;
     float* win2 = nullptr;

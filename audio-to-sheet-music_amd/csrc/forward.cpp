@@ -120,13 +120,12 @@ size_t plan(Arena& ar, const Dims& d, Bufs& b, bool actbf) {
     g = std::max(g, 4 * d.Nt * 192);
     g = std::max(g, 4 * d.L[3] * 96);
     g = std::max(g, 4 * d.L[2] * 48);
-    g = std::max(g, 4 * d.L[1] * 4);
+    g = std::max(g, d.T * 2);                  // tdec_last output xt2 [NI][T][2]
     b.G = ar.take<float>(NI * g);
     int64_t dm = Ts * Ts * 192;
     dm = std::max(dm, d.L[3] * 192);
     dm = std::max(dm, d.L[2] * 96);
     dm = std::max(dm, d.L[1] * 48);
-    dm = std::max(dm, d.T * 4);
     b.D = ar.take<float>(NI * dm);
     b.S = act(NI * 32 * Ts * DEC_CH[1]);
     b.Z = act(NI * 32 * Ts * 8 * DEC_CH[2]);
@@ -436,6 +435,21 @@ void encode(Run& r, const Dims& d, const Bufs& b, const float* wav) {
 void conv_t(Run& r, const DecW& w, const void* A, int a_bf16, int nb, int H_in, int W, void* out, int out_bf16,
             double* st, int keep, const char* stage) {
     KStage kst(stage);
+    if (w.quad.w) {
+        // all four residues in one GEMM (N = 4 cout, K = rows u-1 | u | u+1): the input is read once
+        GemmDesc g;
+        g.A = A; g.a_bf16 = a_bf16; g.nb = nb; g.H_in = H_in; g.W = W; g.C_in = w.cin; g.a_ld = w.cin;
+        g.ntaps = 3; g.in_stride = 1; g.in_off = -1; g.dil = 1; g.H_out = H_in;
+        g.Wp = w.quad.w; g.N = w.quad.N; g.K = w.quad.K; g.Kp = w.quad.Kp; g.bias = w.quad.bias;
+        g.C = out; g.c_bf16 = out_bf16; g.ldo = w.cout; g.stats = st; g.col_split = w.cout; g.hi_row_off = 1;
+        if (keep < 0) {
+            g.H_out_total = 4 * H_in; g.o_stride = 4; g.o_off = 0; g.store_mask = 15;
+        } else {                                    // residues 1, 2 -> slots 2u, 2u+1; 0 and 3 feed the statistics
+            g.H_out_total = 2 * H_in; g.o_stride = 2; g.o_off = -1; g.store_mask = 6;
+        }
+        r.gemm(g, "convt.quad");
+        return;
+    }
     for (int pi = 0; pi < 2; ++pi) {
         GemmDesc g;
         g.A = A; g.a_bf16 = a_bf16; g.nb = nb; g.H_in = H_in; g.W = W; g.C_in = w.cin; g.a_ld = w.cin;
@@ -516,24 +530,28 @@ void decode_chunk(Run& r, const Dims& d, const Bufs& b, int64_t s0, int64_t Bc, 
         // levels 1..3: Tspec -> 4 Tspec rows; the /4 bilinear resize reads only rows 4d+1, 4d+2
         const int skH[3] = {32, 128, 512};
         const int skC[3] = {192, 96, 48};
-        for (int i = 2; i < 4; ++i) {
+        {
+            const int i = 2;
             const DecW& w = c->fdec[i];
-            const bool last = i == 3;
-            double* sti = last ? nullptr : r.stats(NI);
-            static const char* const kF[4] = {"fdec0", "fdec1", "fdec2", "fdec3"};
-            conv_t(r, w, b.D, ab, NI, (int)Ts, (int)Ts, b.G, ab, sti, last ? 2 : 1, kF[i]);
-            KStage kst2(kF[i]);
+            double* sti = r.stats(NI);
+            conv_t(r, w, b.D, ab, NI, (int)Ts, (int)Ts, b.G, ab, sti, 1, "fdec2");
+            KStage kst2("fdec2");
             MergeDesc mm;
             mm.src = b.G; mm.src_bf16 = ab; mm.H_src = 4 * (int)Ts; mm.kept = 1; mm.C = w.cout; mm.fast_gelu = ab;
             mm.stats = sti; mm.gn_count = 4 * Ts * Ts * w.cout; mm.gn_w = w.gnw; mm.gn_b = w.gnb;
             mm.skip = sv[3 - i]; mm.skip_bf16 = ab; mm.H_skip = skH[i - 1]; mm.C_skip = skC[i - 1]; mm.P = P;
             mm.H_out = (int)Ts; mm.W = (int)Ts; mm.NI = NI;
-            if (last) {
-                mm.out = b.FO; mm.proj_w = c->fout_w; mm.proj_b = c->fout_b;     // freq_out 1x1 (4 -> 2)
-            } else {
-                mm.out = b.D; mm.out_bf16 = ab;
-            }
+            mm.out = b.D; mm.out_bf16 = ab;
             r.check(dec_merge_launch(mm, r.s), "dec_merge");
+        }
+        {
+            // level 3 + resize + skip + freq_out 1x1 (4 -> 2) as one pass over the 48-channel input (dec_last.hip)
+            KStage kst3("fdec3");
+            DecLastDesc dl;
+            dl.in = b.D; dl.in_bf16 = ab; dl.NI = NI; dl.P = P; dl.H = (int)Ts; dl.W = (int)Ts;
+            dl.fold = c->flast; dl.skip = sv[0]; dl.skip_bf16 = ab; dl.H_skip = skH[2]; dl.C_skip = skC[2];
+            dl.out = b.FO;
+            r.check(fdec_last_launch(dl, r.s), "fdec_last");
         }
     }
     // ---- mask + iSTFT frames (ATHTDemucs_v2.py:297-310) ----
@@ -545,7 +563,7 @@ void decode_chunk(Run& r, const Dims& d, const Bufs& b, int64_t s0, int64_t Bc, 
                               eoff(b.saved_t[2], s0 * d.L[3] * 192, ea), eoff(b.saved_t[3], s0 * d.L[4] * 384, ea)};
         const void* A = b.xt_cond;
         int64_t Lin = d.Nt;
-        for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < 3; ++i) {
             const DecW& w = c->tdec[i];
             const bool last = i == 3;
             double* st = last ? nullptr : r.stats(NI);
@@ -562,10 +580,16 @@ void decode_chunk(Run& r, const Dims& d, const Bufs& b, int64_t s0, int64_t Bc, 
             A = b.D;
             Lin = target;
         }
+        // level 3 + resize + skip + time_out 1x1 (4 -> 2) as one pass over the 48-channel input (dec_last.hip)
+        KStage kst("tdec3");
+        DecLastDesc dl;
+        dl.in = b.D; dl.in_bf16 = ab; dl.NI = NI; dl.P = P; dl.H = (int)Lin; dl.T = d.T;
+        dl.fold = c->tlast; dl.skip = svt[0]; dl.skip_bf16 = ab; dl.H_skip = (int)d.L[1]; dl.C_skip = ENC_CH[0];
+        dl.out = b.G;
+        r.check(tdec_last_launch(dl, r.s), "tdec_last");
     }
-    // ---- iSTFT overlap-add + time_out + denorm + branch sum (ATHTDemucs_v2.py:310-324) ----
-    combine_launch(b.frames, NI, (int)Ts, d.T, c->win2, b.D, c->tout_w, c->tout_b, b.tnorm_std + 2 * s0, P,
-                   out + s0 * P * 2 * d.T, r.s);
+    // ---- iSTFT overlap-add + denorm + branch sum (ATHTDemucs_v2.py:310-324) ----
+    combine_launch(b.frames, NI, (int)Ts, d.T, c->win2, b.G, b.tnorm_std + 2 * s0, P, out + s0 * P * 2 * d.T, r.s);
 }
 
 // Debug aid: ATHD_DUMP=<dir> makes the forward synchronise at the end and write the main intermediates of the
@@ -585,7 +609,7 @@ void dump_all(const Dims& d, const Bufs& b, hipStream_t s) {
         {"x_cond", b.x_cond, NI * d.Nf * 384, "NI,Nf,384"},
         {"xt_cond", b.xt_cond, NI * d.Nt * 384, "NI,Nt,384"},
         {"FO", b.FO, NI * Ts * Ts * 2, "NI,t,row,2"},
-        {"E3", b.D, NI * d.T * 4, "NI,T,4"},
+        {"XT2", b.G, NI * d.T * 2, "NI,T,2"},
     };
     for (int i = 0; i < 4 && b.ea == 4; ++i) {      // encoder activations are f32 only in parity mode
         es.push_back({"saved" + std::to_string(i), b.saved[i], B * d.F[i + 1] * Ts * ENC_CH[i], "B,F,Ts,C"});

@@ -40,9 +40,9 @@ struct GemmDesc {
     int col_off = 0;
     int64_t c_bs = -1;        // elements between output batches (-1: H_out_total*W*ldo)
     int store = 1;            // 0: compute statistics only
-    int col_split = 0;        // >0: columns >= col_split go to output row + hi_row_off, column n - col_split
-    int hi_row_off = 1;       //     (two ConvTranspose residue classes computed by one GEMM)
-    int store_mask = 3;       //     bit0: store columns < col_split, bit1: store columns >= col_split
+    int col_split = 0;        // >0: column group g = n / col_split goes to output row + g * hi_row_off, column
+    int hi_row_off = 1;       //     n - g * col_split (ConvTranspose residue classes computed by one GEMM)
+    int store_mask = 3;       //     bit g: store column group g
     // epilogue
     int act = ACT_NONE;       // ACT_GLU: packed pairs [a(16) | gate(16)] per 32 columns, output N/2 channels
     const void* res = nullptr;        // residual (same layout as C; f32, or bf16 with res_bf16); out = res + rs[n]*v

@@ -86,9 +86,11 @@ ATHD_DEV void gemm_epilogue(const GemmDesc& d, const f32x4_t (&acc)[TM][TN], int
 
     // per-column constants (hoisted out of the row loop): columns n = nb_j + {0..3}
     float4 bj[TN];
+    int grp[TN];     // ConvT residue group of the lane's 4 columns (col_split % 4 == 0: a 4-group never straddles)
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
         const int nb = n0 + wn0 + 16 * j + 4 * fg;
+        grp[j] = f_split ? nb / d.col_split : 0;
         bj[j] = (d.bias && nb + 3 < d.N) ? *reinterpret_cast<const float4*>(d.bias + nb) : make_float4(0.f, 0.f, 0.f, 0.f);
         if (d.bias && nb < d.N && nb + 3 >= d.N) {   // ragged N (N % 4 != 0 never occurs; keep it exact anyway)
             float t[4] = {0.f, 0.f, 0.f, 0.f};
@@ -105,7 +107,9 @@ ATHD_DEV void gemm_epilogue(const GemmDesc& d, const f32x4_t (&acc)[TM][TN], int
             const uint32_t t = m / (uint32_t)d.W;
             const uint32_t ho = t % (uint32_t)d.H_out;
             const uint32_t b = t / (uint32_t)d.H_out;
-            const int64_t obase = (int64_t)b * c_bs + ((int64_t)(ho * d.o_stride + d.o_off) * d.W + w) * d.ldo + d.col_off;
+            // signed row arithmetic: o_off may be negative (its row is then masked out by store_mask / hi_row_off)
+            const int64_t orow = (int64_t)(int)ho * d.o_stride + d.o_off;
+            const int64_t obase = (int64_t)b * c_bs + (orow * d.W + w) * d.ldo + d.col_off;
             float gm = 0.f, gr = 1.f;
             if (f_gn) {
                 const double mm = d.gn_stats[2 * b] / (double)d.gn_count;
@@ -181,9 +185,8 @@ ATHD_DEV void gemm_epilogue(const GemmDesc& d, const f32x4_t (&acc)[TM][TN], int
                         int64_t off = obase + n;
                         bool st = true;
                         if (f_split) {
-                            const bool hi = n >= d.col_split;       // col_split % 4 == 0: a 4-group never straddles
-                            st = (d.store_mask >> (hi ? 1 : 0)) & 1;
-                            if (hi) off += hi_off;
+                            st = (d.store_mask >> grp[j]) & 1;
+                            off += grp[j] * hi_off;
                         }
                         if (st) {
                             if (f_cbf) {

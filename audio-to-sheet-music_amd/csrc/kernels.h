@@ -20,8 +20,9 @@ void stft_launch(const float* wav, int nb, int64_t T, const PadPlan& pp, int Tsp
 // fo: FO^T [item][t][row][2] (dec_merge_proj_kernel output); specT as above
 void istft_frames_launch(const float* fo, int NI, int Tspec, int P, const float* specT, const float2* tw,
                          const float* win, float* frames, hipStream_t s);
-void combine_launch(const float* frames, int NI, int Tspec, int64_t T, const float* win2, const float* xt3,
-                    const float* tw_out, const float* tb_out, const float* tnorm, int P, float* out, hipStream_t s);
+// out[item][c][n] = OLA(frames)/env + xt2[item][n][c] * stdt[b] + meant[b]   (xt2: tdec_last_launch output)
+void combine_launch(const float* frames, int NI, int Tspec, int64_t T, const float* win2, const float* xt2,
+                    const float* tnorm, int P, float* out, hipStream_t s);
 
 // norm.hip
 // per-batch {sum, sumsq} (double) of x[b][0..n)
@@ -98,6 +99,21 @@ struct FencRowDesc {
 };
 bool fenc_row_supported(int cin, int c, int T);
 int fenc_row_launch(const FencRowDesc& d, int cin, int c, hipStream_t s);
+// dec_last.hip: last decoder level (ConvT 48 -> 4 + resize + 0.1 skip + 1x1 projection to 2, folded) of either branch.
+//   freq: in [NI][H][W][48] -> out FO^T [NI][W][H][2] (H = W = Tspec); fold = [Am | A0 | Ap] (3 x [2][48]), P b + pb (2),
+//         0.1 P (8); skip [NI/P][H_skip][W][C_skip] (channels 0..3 used)
+//   time: in [NI][H][48] (H = Lin) -> out xt2 [NI][T][2] = time_out(...) incl. bias; fold = Q_k (8 x [2][48]), P b (2),
+//         tb (2), 0.1 P (8); skip [NI/P][H_skip][C_skip]
+struct DecLastDesc {
+    const void* in = nullptr; int in_bf16 = 0;
+    int NI = 0, P = 1, H = 0, W = 1;
+    int64_t T = 0;
+    const float* fold = nullptr;
+    const void* skip = nullptr; int skip_bf16 = 0; int H_skip = 0; int C_skip = 0;
+    float* out = nullptr;
+};
+int fdec_last_launch(const DecLastDesc& d, hipStream_t s);
+int tdec_last_launch(const DecLastDesc& d, hipStream_t s);
 // dconv.hip: one DConv layer (conv3 -> GN -> GELU -> 1x1 -> GN -> GLU -> LayerScale -> residual) for C in {48, 96}
 // x: [nb][L][C] f32 or bf16 (x_bf16), updated in place; h: [nb][L][C/8] f32 scratch
 int dconv_small_launch(void* x, int x_bf16, float* h, int64_t nb, int64_t L, int C, int dil, const float* w3,

@@ -164,11 +164,10 @@ void istft_frames_launch(const float* fo, int NI, int Tspec, int P, const float*
     hipLaunchKernelGGL(istft_frames_kernel, dim3(Tspec, NI), dim3(256), 0, s, fo, Tspec, P, spec, tw, win, frames);
 }
 
-// out[item][c][n] = OLA(frames)/env + (time_out(xt3[item][n][:]) * stdt[b] + meant[b])
+// out[item][c][n] = OLA(frames)/env + xt2[item][n][c] * stdt[b] + meant[b]   (ATHTDemucs_v2.py:310-324; xt2 is
+// time_out of the time decoder, dec_last.hip)
 __global__ __launch_bounds__(256) void combine_kernel(const float* __restrict__ frames, int Tspec, int64_t T,
-                                                      const float* __restrict__ win2,
-                                                      const float* __restrict__ xt3, const float* __restrict__ tw_out,
-                                                      const float* __restrict__ tb_out,
+                                                      const float* __restrict__ win2, const float* __restrict__ xt2,
                                                       const float* __restrict__ tnorm, int P,
                                                       float* __restrict__ out) {
     const int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -177,7 +176,7 @@ __global__ __launch_bounds__(256) void combine_kernel(const float* __restrict__ 
     const int64_t b = item / P;
     const int64_t q = n + 3584;                      // OLA index: 1536 (_ispec slice) + 2048 (istft centre)
     const int nfr = Tspec + 4;
-    int f_lo = (int)((q - NFFT + HOP) / HOP);        // first frame f' with 1024 f' + 4096 > q
+    int f_lo;                                        // first frame f' with 1024 f' + 4096 > q
     if (q - NFFT + 1 <= 0) f_lo = 0;
     else f_lo = (int)((q - NFFT + 1 + HOP - 1) / HOP);
     int f_hi = (int)(q / HOP);
@@ -193,21 +192,19 @@ __global__ __launch_bounds__(256) void combine_kernel(const float* __restrict__ 
             y1 += fr[NFFT + j];
         }
     }
-    const float4 x3 = *reinterpret_cast<const float4*>(xt3 + (item * T + n) * 4);
+    const float2 x2 = *reinterpret_cast<const float2*>(xt2 + (item * T + n) * 2);
     const float mean = tnorm[2 * b], stdv = tnorm[2 * b + 1];
-    float t0 = tb_out[0] + tw_out[0] * x3.x + tw_out[1] * x3.y + tw_out[2] * x3.z + tw_out[3] * x3.w;
-    float t1 = tb_out[1] + tw_out[4] * x3.x + tw_out[5] * x3.y + tw_out[6] * x3.z + tw_out[7] * x3.w;
-    out[(item * 2 + 0) * T + n] = y0 / env + (t0 * stdv + mean);
-    out[(item * 2 + 1) * T + n] = y1 / env + (t1 * stdv + mean);
+    out[(item * 2 + 0) * T + n] = y0 / env + (x2.x * stdv + mean);
+    out[(item * 2 + 1) * T + n] = y1 / env + (x2.y * stdv + mean);
 }
 
-void combine_launch(const float* frames, int NI, int Tspec, int64_t T, const float* win2, const float* xt3,
-                    const float* tw_out, const float* tb_out, const float* tnorm, int P, float* out, hipStream_t s) {
+void combine_launch(const float* frames, int NI, int Tspec, int64_t T, const float* win2, const float* xt2,
+                    const float* tnorm, int P, float* out, hipStream_t s) {
     dim3 grid((unsigned)((T + 255) / 256), NI);
     KScope ks(s);
     if (ks.on())
-        ks.begin("combine_kernel", 0.0, (double)NI * Tspec * 2 * 4096 * 4 + (double)NI * T * 4 * 4 + (double)NI * 2 * T * 4);
-    hipLaunchKernelGGL(combine_kernel, grid, dim3(256), 0, s, frames, Tspec, T, win2, xt3, tw_out, tb_out, tnorm, P, out);
+        ks.begin("combine_kernel", 0.0, (double)NI * Tspec * 2 * 4096 * 4 + (double)NI * T * 2 * 4 + (double)NI * 2 * T * 4);
+    hipLaunchKernelGGL(combine_kernel, grid, dim3(256), 0, s, frames, Tspec, T, win2, xt2, tnorm, P, out);
 }
 
 }  // namespace athd

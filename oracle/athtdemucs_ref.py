@@ -177,6 +177,8 @@ class AudioTextHTDemucsRef:
         xt_dec = F.conv1d(xt_dec, *self.time_out)
         if xt_dec.shape[-1] != original_length:
             xt_dec = F.interpolate(xt_dec, size=original_length, mode="linear", align_corners=False)
+        if capture is not None:
+            capture["xt_out"] = xt_dec
         xt_dec = xt_dec * stdt + meant
         if capture is not None:
             capture.update(x_cond=x_cond, xt_cond=xt_cond, mask=mask, freq_wav=freq_wav, xt_dec=xt_dec)

@@ -163,7 +163,7 @@ def test_intermediates_f32(models, oracle_model, text_table):
     cmp("x_cond", cap["x_cond"].permute(0, 2, 3, 1).numpy(), dump["x_cond"])
     cmp("xt_cond", cap["xt_cond"].permute(0, 2, 1).numpy(), dump["xt_cond"])
     cmp("FO", cap["x_fo"].permute(0, 3, 2, 1).numpy(), dump["FO"])          # FO^T [item][t][row][2]
-    cmp("E3", cap["xt_dec3"].permute(0, 2, 1).numpy(), dump["E3"])
+    cmp("XT2", cap["xt_out"].permute(0, 2, 1).numpy(), dump["XT2"])      # time_out(time decoder) [item][n][2]
     _report("intermediates_f32", res)
     bad = {k: v for k, v in res.items() if v["sdr_db"] < F32_SDR_DB}
     assert not bad, bad
