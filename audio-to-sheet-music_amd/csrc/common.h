@@ -4,6 +4,7 @@
 #include <stdint.h>
 
 #define ATHD_DEV __device__ __forceinline__
+#define ATHD_HD __host__ __device__ __forceinline__
 
 typedef __attribute__((ext_vector_type(8))) short bf16x8_t;   // 8 bf16 = one MFMA 16x16x32 operand fragment
 typedef __attribute__((ext_vector_type(4))) float f32x4_t;    // 16x16 accumulator fragment
@@ -56,7 +57,7 @@ ATHD_DEV float wave_max(float v) {
 // PyTorch-faithful fp32 source index for linear/bilinear resize with align_corners=False and no explicit scale
 // (ATen UpSample.h area_pixel_compute_scale / area_pixel_compute_source_index / guard_index_and_lambda).
 struct LinIdx { int i0, i1; float l0, l1; };
-ATHD_DEV LinIdx lin_index(int dst, int in_size, int out_size) {
+ATHD_HD LinIdx lin_index(int dst, int in_size, int out_size) {
     LinIdx r;
     if (in_size == out_size) { r.i0 = r.i1 = dst; r.l0 = 1.f; r.l1 = 0.f; return r; }
     float scale = (float)in_size / (float)out_size;

@@ -18,6 +18,8 @@
 #include "kernels.h"
 #include "prof.h"
 
+#include <algorithm>
+
 namespace athd {
 
 namespace {
@@ -251,6 +253,341 @@ __global__ __launch_bounds__(256) void tdec_last_generic_kernel(const DecLastDes
     o.x = (li.l0 * a0 + li.l1 * b0) + cb[2] + (S[0] * s[0] + S[1] * s[1] + S[2] * s[2] + S[3] * s[3]);
     o.y = (li.l0 * a1 + li.l1 * b1) + cb[3] + (S[4] * s[0] + S[5] * s[1] + S[6] * s[2] + S[7] * s[3]);
     *reinterpret_cast<float2*>(d.out + (item * (int64_t)d.T + n) * 2) = o;
+}
+
+// ------------------------------------------------------------------------------------------ fused level-2 merge
+// dec_tail: the level-2 merge of both branches (ATHTDemucs_v2.py:88-103 / :126-138 with i = 2: GroupNorm -> GELU of
+// the ConvT output, resize, + 0.1 * resize(skip[:, :48])) computed in front of the folded last level, so the merged
+// 48-channel level-2 output never goes to HBM: per output row the kernel reads the ConvT rows the resize touches and
+// the skip rows, and writes 2 floats.  Same fp32 expression order as dec_merge_kernel (norm.hip) for each value.
+
+namespace {
+// Uniform read-only tables (folded weights, GroupNorm affine) read through the constant address space: the compiler
+// cannot prove a generic pointer unclobbered by the kernel's own stores and would otherwise use vector loads and
+// hold ~300 weights in VGPRs.
+typedef const __attribute__((address_space(4))) float cfloat;
+ATHD_DEV cfloat* cview(const float* p) { return (cfloat*)p; }
+// a zero the compiler cannot see through: table addresses offset by it cannot be hoisted above the point it is made,
+// which bounds how many uniform weights are live in scalar registers at once
+ATHD_DEV int opaque_zero() {
+    int z;
+    asm volatile("s_mov_b32 %0, 0" : "=s"(z));
+    return z;
+}
+
+// 8 channels (bf16 or f32) -> f32
+ATHD_DEV void ld8(const void* p, int bf, int64_t off, float* v) {
+    if (bf) {
+        const uint4 q = *reinterpret_cast<const uint4*>((const bf16_t*)p + off);
+        const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            v[2 * e] = __uint_as_float(w[e] << 16);
+            v[2 * e + 1] = __uint_as_float(w[e] & 0xFFFF0000u);
+        }
+    } else {
+        const float4 a = *reinterpret_cast<const float4*>((const float*)p + off);
+        const float4 b = *reinterpret_cast<const float4*>((const float*)p + off + 4);
+        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+    }
+}
+
+template <bool FAST>
+ATHD_DEV float gn_act(float y, float mean, float rstd, float w, float b) {
+    return gelu<FAST>((y - mean) * rstd * w + b);
+}
+}  // namespace
+
+// Raw loads of one lane's 12-channel slice (channels 12 cg .. 12 cg + 11) of the four rows an x row needs: the two
+// ConvT rows the resize reads and the two level-2 skip rows.
+template <bool BF> struct Slice12;
+template <> struct Slice12<true> {
+    uint2 v[4][3];
+    ATHD_DEV void load(int r, const void* p, int64_t off) {
+#pragma unroll
+        for (int i = 0; i < 3; ++i) v[r][i] = *reinterpret_cast<const uint2*>((const bf16_t*)p + off + 4 * i);
+    }
+    ATHD_DEV float get(int r, int j) const {
+        const uint2 q = v[r][j >> 2];
+        const uint32_t w = (j & 2) ? q.y : q.x;
+        return (j & 1) ? __uint_as_float(w & 0xFFFF0000u) : __uint_as_float(w << 16);
+    }
+};
+template <> struct Slice12<false> {
+    float4 v[4][3];
+    ATHD_DEV void load(int r, const void* p, int64_t off) {
+#pragma unroll
+        for (int i = 0; i < 3; ++i) v[r][i] = *reinterpret_cast<const float4*>((const float*)p + off + 4 * i);
+    }
+    ATHD_DEV float get(int r, int j) const {
+        const float4 q = v[r][j >> 2];
+        return (j & 3) == 0 ? q.x : (j & 3) == 1 ? q.y : (j & 3) == 2 ? q.z : q.w;
+    }
+};
+
+// freq: one wave = (item, d-chunk of FL_DC rows, 16 consecutive w).  Lane l: position w = 16 wt + (l & 15), channel
+// group cg = l >> 4.  Per row u the lane forms x[u] at its 12 channels (0.5 act(y[4u+1]) + 0.5 act(y[4u+2]) + skip,
+// dec_merge_kernel's fp32 expression order) and the 6 projections [Am; A0; Ap] x[u] come out of 12 exact-f32
+// v_mfma_f32_16x16x4_f32 (A = the folded weights, rows 0..5, K permuted to channel 12 cg + step; B = x): the row
+// reduction over channels happens in the matrix core and the weights are 12 per-lane constants.
+template <bool BF>
+__global__ __launch_bounds__(256) void fdec_tail_kernel(const DecLastDesc d) {
+    const int64_t item = blockIdx.y;
+    const int64_t seg = item / d.P;
+    const int H = d.H, W = d.W;
+    const int lane = threadIdx.x & 63;
+    const int nwt = (W + 15) / 16;
+    const int nch = (H + FL_DC - 1) / FL_DC;
+    const int wv = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (wv >= nch * nwt) return;                       // wave-uniform
+    const int wt = wv % nwt, c = wv / nwt;
+    const int p = lane & 15, cg = lane >> 4;
+    const int w = wt * 16 + p;
+    const bool wok = w < W;
+    const int wc = wok ? w : W - 1;                    // clamped: the spare lanes compute a duplicate, never stored
+    const int d0 = c * FL_DC;
+    const int d1 = min(H, d0 + FL_DC);
+    float mean, rstd;
+    gn_params(d.stats, item, d.gn_count, mean, rstd);
+    const int ch0 = 12 * cg;
+    float wA[12], gw[12], gb[12];
+#pragma unroll
+    for (int s = 0; s < 12; ++s) {
+        wA[s] = p < 6 ? d.fold[p * DL_C + ch0 + s] : 0.f;
+        gw[s] = d.gn_w[ch0 + s];
+        gb[s] = d.gn_b[ch0 + s];
+    }
+    const float* F = d.fold;
+    const float* cst = F + 6 * DL_C;
+    const float* S = F + 6 * DL_C + 2;
+    const int64_t g_item = item * (int64_t)(2 * H) * W * DL_C + (int64_t)wc * DL_C + ch0;
+    const int64_t sk2 = seg * (int64_t)d.H_skip2 * W * d.C_skip2 + (int64_t)wc * d.C_skip2 + ch0;
+    const int64_t sk = seg * d.H_skip * W * d.C_skip;
+    float* fo = d.out + (item * W + wc) * (int64_t)H * 2;
+
+    auto load = [&](int u, Slice12<BF>& r) {
+        const LinIdx lj = lin_index(u, d.H_skip2, H);
+        const int64_t o0 = g_item + (int64_t)(2 * u) * W * DL_C;   // kept slots 2u, 2u+1 = rows 4u+1, 4u+2
+        r.load(0, d.g, o0);
+        r.load(1, d.g, o0 + (int64_t)W * DL_C);
+        r.load(2, d.skip2, sk2 + (int64_t)lj.i0 * W * d.C_skip2);
+        r.load(3, d.skip2, sk2 + (int64_t)lj.i1 * W * d.C_skip2);
+    };
+    // [Am0 Am1 A00 A01] x[u] (lanes cg = 0) and [Ap0 Ap1 0 0] x[u] (lanes cg = 1)
+    auto proj = [&](int u, const Slice12<BF>& r) {
+        const LinIdx li = lin_index(u, 4 * H, H);
+        const LinIdx lj = lin_index(u, d.H_skip2, H);
+        f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < 12; ++s) {
+            const float va = gn_act<BF>(r.get(0, s), mean, rstd, gw[s], gb[s]);
+            const float vb = gn_act<BF>(r.get(1, s), mean, rstd, gw[s], gb[s]);
+            const float sv = (lj.l0 * r.get(2, s) + lj.l1 * r.get(3, s)) * 0.1f;
+            const float x = (li.l0 * va + li.l1 * vb) + sv;
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wA[s], x, acc, 0, 0, 0);
+        }
+        return acc;
+    };
+
+    Slice12<BF> cur, nxt;
+    float cr0 = 0.f, cr1 = 0.f;                // Am x[u-1]: carry into row u
+    if (d0 > 0) {
+        load(d0 - 1, cur);
+        const f32x4_t a = proj(d0 - 1, cur);
+        cr0 = a[0];
+        cr1 = a[1];
+    }
+    load(d0, cur);
+    float pe0 = 0.f, pe1 = 0.f;                // pending FO[u-1] without its Ap x[u] term
+#pragma unroll 1
+    for (int u = d0; u < d1; ++u) {
+        if (u + 1 < H) load(u + 1, nxt);       // prefetch (also the halo row d1)
+        const f32x4_t a = proj(u, cur);
+        const float ap0 = __shfl(a[0], p + 16, 64), ap1 = __shfl(a[1], p + 16, 64);
+        if (cg == 0) {
+            const LinIdx lj = lin_index(u, d.H_skip, H);
+            float sa[4], sb[4], s4[4];
+            ld_skip4(d.skip, BF, sk + ((int64_t)lj.i0 * W + wc) * d.C_skip, sa);
+            ld_skip4(d.skip, BF, sk + ((int64_t)lj.i1 * W + wc) * d.C_skip, sb);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) s4[q] = lj.l0 * sa[q] + lj.l1 * sb[q];
+            if (u > d0 && wok) *reinterpret_cast<float2*>(fo + 2 * (u - 1)) = make_float2(pe0 + ap0, pe1 + ap1);
+            pe0 = cst[0] + (S[0] * s4[0] + S[1] * s4[1] + S[2] * s4[2] + S[3] * s4[3]) + cr0 + a[2];
+            pe1 = cst[1] + (S[4] * s4[0] + S[5] * s4[1] + S[6] * s4[2] + S[7] * s4[3]) + cr1 + a[3];
+            cr0 = a[0];
+            cr1 = a[1];
+        }
+        cur = nxt;
+    }
+    float q0 = 0.f, q1 = 0.f;
+    if (d1 < H) {                              // halo: Ap x[d1] (loaded by the last iteration)
+        const f32x4_t a = proj(d1, cur);
+        q0 = __shfl(a[0], p + 16, 64);
+        q1 = __shfl(a[1], p + 16, 64);
+    }
+    if (cg == 0 && wok) *reinterpret_cast<float2*>(fo + 2 * (d1 - 1)) = make_float2(pe0 + q0, pe1 + q1);
+}
+
+// time (4 H == T): block = (item, TL_IN output rows + 1 halo row each side), row r <-> u = TL_IN bx - 1 + r.
+//   phase 1: GroupNorm + GELU of the block's span of ConvT rows (<= TT_ROWS) into LDS (fp32);
+//   phase 2: wave w, pass k: rows r = 64 k + 16 w + (l & 15); the lane forms x[u] at channels 12 cg .. 12 cg + 11
+//            (resize of the LDS rows + 0.1 resize(skip2)) and 12 v_mfma_f32_16x16x4_f32 give the 16 tap products
+//            z[u] = [Q_0; ..; Q_7] x[u] (row 2k + j = tap k, channel j) - lane (p, cg) ends with taps 2cg, 2cg + 1;
+//   phase 3: z rows through LDS; thread r writes the 4 output samples 4u .. 4u + 3 of its row (x 2 channels).
+constexpr int TT_ROWS = 264;
+constexpr int TT_LD = 50;        // LDS row pitch in floats (3 blocks per CU)
+
+ATHD_HD int tt_span(int bx, int Lin, int Hg, int& r0) {
+    const int ua = bx * TL_IN - 1 < 0 ? 0 : bx * TL_IN - 1;
+    const int ub = bx * TL_IN + TL_IN < Lin - 1 ? bx * TL_IN + TL_IN : Lin - 1;
+    r0 = lin_index(ua, Hg, Lin).i0;
+    return lin_index(ub, Hg, Lin).i1 - r0 + 1;
+}
+
+template <bool BF>
+__global__ __launch_bounds__(TL_NT) void tdec_tail_kernel(const DecLastDesc d) {
+    __shared__ __attribute__((aligned(16))) float gs[TT_ROWS * TT_LD];
+    float* zb = gs;                              // phase 3: z rows [TL_NT][16], over the dead phase-1 tile
+    const int64_t item = blockIdx.y;
+    const int64_t seg = item / d.P;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int Lin = d.H;
+    float mean, rstd;
+    gn_params(d.stats, item, d.gn_count, mean, rstd);
+    int r0;
+    const int nr = tt_span(blockIdx.x, Lin, d.Hg, r0);
+    const int64_t gb = (item * d.Hg + r0) * (int64_t)DL_C;
+    for (int i = tid; i < nr * (DL_C / 8); i += TL_NT) {
+        const int rr = i / (DL_C / 8), q = i % (DL_C / 8);
+        float a[8];
+        ld8(d.g, BF, gb + (int64_t)rr * DL_C + 8 * q, a);
+        float2* dst = reinterpret_cast<float2*>(gs + rr * TT_LD + 8 * q);
+#pragma unroll
+        for (int j = 0; j < 8; j += 2)
+            dst[j / 2] = make_float2(gn_act<BF>(a[j], mean, rstd, d.gn_w[8 * q + j], d.gn_b[8 * q + j]),
+                                     gn_act<BF>(a[j + 1], mean, rstd, d.gn_w[8 * q + j + 1], d.gn_b[8 * q + j + 1]));
+    }
+    __syncthreads();
+    const int p = lane & 15, cg = lane >> 4, ch0 = 12 * cg;
+    float wA[12];
+#pragma unroll
+    for (int s = 0; s < 12; ++s) wA[s] = d.fold[p * DL_C + ch0 + s];     // Q [8][2][48]: row p = 2 k + j
+    f32x4_t z[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int r = 64 * k + 16 * wave + p;
+        const int u = blockIdx.x * TL_IN - 1 + r;
+        float x[12];
+#pragma unroll
+        for (int s = 0; s < 12; ++s) x[s] = 0.f;      // x = 0 outside [0, Lin): zero taps
+        if (u >= 0 && u < Lin) {
+            const LinIdx li = lin_index(u, d.Hg, Lin);
+            const LinIdx lj = lin_index(u, d.H_skip2, Lin);
+            Slice12<BF> sl;
+            sl.load(2, d.skip2, (seg * d.H_skip2 + lj.i0) * (int64_t)d.C_skip2 + ch0);
+            sl.load(3, d.skip2, (seg * d.H_skip2 + lj.i1) * (int64_t)d.C_skip2 + ch0);
+            const float* ga = gs + (li.i0 - r0) * TT_LD + ch0;
+            const float* gq = gs + (li.i1 - r0) * TT_LD + ch0;
+#pragma unroll
+            for (int s = 0; s < 12; ++s) {
+                const float sv = (lj.l0 * sl.get(2, s) + lj.l1 * sl.get(3, s)) * 0.1f;
+                x[s] = (li.l0 * ga[s] + li.l1 * gq[s]) + sv;
+            }
+        }
+        // the MFMAs run wave-converged (a matrix op reads every lane's operands whatever EXEC says)
+        z[k] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < 12; ++s) z[k] = __builtin_amdgcn_mfma_f32_16x16x4f32(wA[s], x[s], z[k], 0, 0, 0);
+    }
+    __syncthreads();                             // every wave is done reading the phase-1 tile
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        *reinterpret_cast<float4*>(zb + (64 * k + 16 * wave + p) * 16 + 4 * cg) = make_float4(z[k][0], z[k][1], z[k][2], z[k][3]);
+    __syncthreads();
+    const int u = blockIdx.x * TL_IN - 1 + tid;
+    if (!(tid > 0 && tid < TL_NT - 1 && u < Lin)) return;
+    const float* F = d.fold;
+    const float* cb = F + 16 * DL_C;             // P b (2), then tb (2), then 0.1 P (8)
+    const float* S = cb + 4;
+    const float c0 = cb[0] + cb[2], c1 = cb[1] + cb[3];
+    float sbv[4][2];
+    const int64_t sk = seg * d.H_skip * d.C_skip;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const LinIdx lj = lin_index(4 * u + r, d.H_skip, (int)d.T);
+        float a[4], b[4], s[4];
+        ld_skip4(d.skip, BF, sk + (int64_t)lj.i0 * d.C_skip, a);
+        ld_skip4(d.skip, BF, sk + (int64_t)lj.i1 * d.C_skip, b);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) s[q] = lj.l0 * a[q] + lj.l1 * b[q];
+        sbv[r][0] = c0 + (S[0] * s[0] + S[1] * s[1] + S[2] * s[2] + S[3] * s[3]);
+        sbv[r][1] = c1 + (S[4] * s[0] + S[5] * s[1] + S[6] * s[2] + S[7] * s[3]);
+    }
+    const float* zc = zb + tid * 16;             // taps of row u:   [z0 z1 | z2 z3 | z4 z5 | z6 z7] x 2 channels
+    const float* zl = zc - 16;                   // row u - 1 feeds rows 4u + {0, 1} through taps 6, 7
+    const float* zh = zc + 16;                   // row u + 1 feeds rows 4u + {2, 3} through taps 0, 1
+    float4 o0, o1;
+    o0.x = (zc[4] + zl[12]) + sbv[0][0];
+    o0.y = (zc[5] + zl[13]) + sbv[0][1];
+    o0.z = (zc[6] + zl[14]) + sbv[1][0];
+    o0.w = (zc[7] + zl[15]) + sbv[1][1];
+    o1.x = (zc[8] + zh[0]) + sbv[2][0];
+    o1.y = (zc[9] + zh[1]) + sbv[2][1];
+    o1.z = (zc[10] + zh[2]) + sbv[3][0];
+    o1.w = (zc[11] + zh[3]) + sbv[3][1];
+    float4* o = reinterpret_cast<float4*>(d.out + (item * (int64_t)d.T + 4 * (int64_t)u) * 2);
+    o[0] = o0;
+    o[1] = o1;
+}
+
+int fdec_tail_launch(const DecLastDesc& d, hipStream_t s) {
+    if (d.g_bf16 != d.skip2_bf16 || d.g_bf16 != d.skip_bf16 || d.g_bf16 != d.fast_gelu ||d.P < 1 || d.NI % d.P != 0 || d.H < 1 || d.W < 1 || d.C_skip < 4 || d.H_skip < 1 || !d.g || !d.stats ||
+        d.C_skip2 < DL_C || d.C_skip2 % 8 != 0 || d.H_skip2 < 1)
+        return -1;
+    const int nch = (d.H + FL_DC - 1) / FL_DC;
+    const int waves = nch * ((d.W + 15) / 16);
+    const dim3 grid((unsigned)((waves + 3) / 4), (unsigned)d.NI);
+    KScope ks(s);
+    if (ks.on()) {
+        // the two kept ConvT rows per output row once, level-2 skip rows (48 channels, 2 per output row) and level-3
+        // skip rows (4 channels) once per segment, FO once
+        const double eg = d.g_bf16 ? 2 : 4, es2 = d.skip2_bf16 ? 2 : 4, es = d.skip_bf16 ? 2 : 4;
+        const double segs = d.NI / d.P;
+        const double by = (double)d.NI * 2 * d.H * d.W * DL_C * eg + segs * std::min(d.H_skip2, 2 * d.H) * d.W * DL_C * es2 +
+                          segs * 2 * d.H * d.W * 4 * es + (double)d.NI * d.H * d.W * 2 * 4;
+        ks.begin("fdec_tail_kernel", 0.0, by);
+    }
+    if (d.g_bf16) hipLaunchKernelGGL(fdec_tail_kernel<true>, grid, dim3(256), 0, s, d);
+    else hipLaunchKernelGGL(fdec_tail_kernel<false>, grid, dim3(256), 0, s, d);
+    return (int)hipGetLastError();
+}
+
+bool tdec_tail_supported(const DecLastDesc& d) {
+    if (4 * (int64_t)d.H != d.T || d.H < 1 || d.Hg < 1 || !d.g || !d.stats || d.C_skip2 < DL_C || d.C_skip2 % 8 != 0)
+        return false;
+    const int nb = (d.H + TL_IN - 1) / TL_IN;
+    for (int bx = 0; bx < nb; ++bx) {
+        int r0;
+        const int nr = tt_span(bx, d.H, d.Hg, r0);
+        if (nr < 1 || nr > TT_ROWS || r0 < 0 || r0 + nr > d.Hg) return false;
+    }
+    return true;
+}
+
+int tdec_tail_launch(const DecLastDesc& d, hipStream_t s) {
+    if (d.g_bf16 != d.skip2_bf16 || d.g_bf16 != d.skip_bf16 || d.g_bf16 != d.fast_gelu ||d.P < 1 || d.NI % d.P != 0 || d.C_skip < 4 || d.H_skip < 1 || d.H_skip2 < 1 || !tdec_tail_supported(d)) return -1;
+    KScope ks(s);
+    if (ks.on()) {
+        const double eg = d.g_bf16 ? 2 : 4, es2 = d.skip2_bf16 ? 2 : 4, es = d.skip_bf16 ? 2 : 4;
+        const double segs = d.NI / d.P;
+        const double by = (double)d.NI * d.Hg * DL_C * eg + segs * d.H_skip2 * DL_C * es2 + segs * d.H_skip * 4 * es +
+                          (double)d.NI * d.T * 2 * 4;
+        ks.begin("tdec_tail_kernel", 0.0, by);
+    }
+    const dim3 grid((unsigned)((d.H + TL_IN - 1) / TL_IN), (unsigned)d.NI);
+    if (d.g_bf16) hipLaunchKernelGGL(tdec_tail_kernel<true>, grid, dim3(TL_NT), 0, s, d);
+    else hipLaunchKernelGGL(tdec_tail_kernel<false>, grid, dim3(TL_NT), 0, s, d);
+    return (int)hipGetLastError();
 }
 
 int fdec_last_launch(const DecLastDesc& d, hipStream_t s) {

@@ -67,6 +67,7 @@ struct Bufs {
     void* Hm;
     float *G, *D, *FO, *frames;
     void *S, *Z, *Zs;   // freq level 1 re-associated (fdec_lr.hip): per-tap products of the 32 / 8 source rows
+    mutable float* xt2 = nullptr;   // time_out(time decoder) of the last decode chunk: D (fused tail) or G (ragged T)
 };
 
 size_t plan(Arena& ar, const Dims& d, Bufs& b, bool actbf) {
@@ -531,43 +532,36 @@ void decode_chunk(Run& r, const Dims& d, const Bufs& b, int64_t s0, int64_t Bc, 
         const int skH[3] = {32, 128, 512};
         const int skC[3] = {192, 96, 48};
         {
-            const int i = 2;
-            const DecW& w = c->fdec[i];
+            // level 2 ConvT (only rows 4d+1, 4d+2 stored; statistics over all four residues), then its merge (GN +
+            // GELU + resize + skip) fused with level 3 + resize + skip + freq_out 1x1 (4 -> 2) in one pass over the
+            // stored ConvT rows (dec_last.hip::fdec_tail_kernel)
+            const DecW& w = c->fdec[2];
             double* sti = r.stats(NI);
             conv_t(r, w, b.D, ab, NI, (int)Ts, (int)Ts, b.G, ab, sti, 1, "fdec2");
-            KStage kst2("fdec2");
-            MergeDesc mm;
-            mm.src = b.G; mm.src_bf16 = ab; mm.H_src = 4 * (int)Ts; mm.kept = 1; mm.C = w.cout; mm.fast_gelu = ab;
-            mm.stats = sti; mm.gn_count = 4 * Ts * Ts * w.cout; mm.gn_w = w.gnw; mm.gn_b = w.gnb;
-            mm.skip = sv[3 - i]; mm.skip_bf16 = ab; mm.H_skip = skH[i - 1]; mm.C_skip = skC[i - 1]; mm.P = P;
-            mm.H_out = (int)Ts; mm.W = (int)Ts; mm.NI = NI;
-            mm.out = b.D; mm.out_bf16 = ab;
-            r.check(dec_merge_launch(mm, r.s), "dec_merge");
-        }
-        {
-            // level 3 + resize + skip + freq_out 1x1 (4 -> 2) as one pass over the 48-channel input (dec_last.hip)
             KStage kst3("fdec3");
             DecLastDesc dl;
-            dl.in = b.D; dl.in_bf16 = ab; dl.NI = NI; dl.P = P; dl.H = (int)Ts; dl.W = (int)Ts;
+            dl.g = b.G; dl.g_bf16 = ab; dl.stats = sti; dl.gn_count = 4 * Ts * Ts * w.cout; dl.gn_w = w.gnw; dl.gn_b = w.gnb;
+            dl.fast_gelu = ab; dl.skip2 = sv[1]; dl.skip2_bf16 = ab; dl.H_skip2 = skH[1]; dl.C_skip2 = skC[1];
+            dl.NI = NI; dl.P = P; dl.H = (int)Ts; dl.W = (int)Ts;
             dl.fold = c->flast; dl.skip = sv[0]; dl.skip_bf16 = ab; dl.H_skip = skH[2]; dl.C_skip = skC[2];
             dl.out = b.FO;
-            r.check(fdec_last_launch(dl, r.s), "fdec_last");
+            r.check(fdec_tail_launch(dl, r.s), "fdec_tail");
         }
     }
     // ---- mask + iSTFT frames (ATHTDemucs_v2.py:297-310) ----
     istft_frames_launch(b.FO, NI, (int)Ts, P, b.specT + s0 * 2048 * Ts * 4, c->tw, c->win, b.frames, r.s);
 
     // ---- time decoder (ATHTDemucs_v2.py:125-139, 313-321) ----
+    float* xt2 = nullptr;                            // time_out(time decoder) [NI][T][2]
     {
         const void* svt[4] = {eoff(b.saved_t[0], s0 * d.L[1] * 48, ea), eoff(b.saved_t[1], s0 * d.L[2] * 96, ea),
                               eoff(b.saved_t[2], s0 * d.L[3] * 192, ea), eoff(b.saved_t[3], s0 * d.L[4] * 384, ea)};
         const void* A = b.xt_cond;
         int64_t Lin = d.Nt;
+        static const char* const kT[3] = {"tdec0", "tdec1", "tdec2"};
         for (int i = 0; i < 3; ++i) {
             const DecW& w = c->tdec[i];
-            const bool last = i == 3;
-            double* st = last ? nullptr : r.stats(NI);
-            static const char* const kT[4] = {"tdec0", "tdec1", "tdec2", "tdec3"};
+            double* st = r.stats(NI);
             conv_t(r, w, A, ab, NI, (int)Lin, 1, b.G, ab, st, -1, kT[i]);
             KStage kst(kT[i]);
             const int64_t target = d.L[3 - i];       // lengths_t reversed
@@ -575,21 +569,42 @@ void decode_chunk(Run& r, const Dims& d, const Bufs& b, int64_t s0, int64_t Bc, 
             m.src = b.G; m.src_bf16 = ab; m.H_src = (int)(4 * Lin); m.kept = 0; m.C = w.cout; m.fast_gelu = ab;
             m.stats = st; m.gn_count = 4 * Lin * w.cout; m.gn_w = w.gnw; m.gn_b = w.gnb;
             m.skip = svt[3 - i]; m.skip_bf16 = ab; m.H_skip = (int)d.L[4 - i]; m.C_skip = ENC_CH[3 - i]; m.P = P;
-            m.out = b.D; m.out_bf16 = last ? 0 : ab; m.H_out = (int)target; m.W = 1; m.NI = NI;
+            m.out = b.D; m.out_bf16 = ab; m.H_out = (int)target; m.W = 1; m.NI = NI;
+            if (i == 2) {
+                // level 2's merge fused with level 3 + resize + skip + time_out 1x1 (4 -> 2) when 4 L1 == T
+                // (dec_last.hip::tdec_tail_kernel): one pass over the ConvT output, xt2 -> D
+                DecLastDesc dl;
+                dl.g = b.G; dl.g_bf16 = ab; dl.Hg = (int)(4 * Lin); dl.stats = st; dl.gn_count = m.gn_count;
+                dl.gn_w = w.gnw; dl.gn_b = w.gnb; dl.fast_gelu = ab;
+                dl.skip2 = svt[1]; dl.skip2_bf16 = ab; dl.H_skip2 = (int)d.L[2]; dl.C_skip2 = ENC_CH[1];
+                dl.NI = NI; dl.P = P; dl.H = (int)target; dl.T = d.T;
+                dl.fold = c->tlast; dl.skip = svt[0]; dl.skip_bf16 = ab; dl.H_skip = (int)d.L[1]; dl.C_skip = ENC_CH[0];
+                dl.out = b.D;
+                if (tdec_tail_supported(dl)) {
+                    KStage kst3("tdec3");
+                    r.check(tdec_tail_launch(dl, r.s), "tdec_tail");
+                    xt2 = b.D;
+                    break;
+                }
+            }
             r.check(dec_merge_launch(m, r.s), "dec_merge");
             A = b.D;
             Lin = target;
         }
-        // level 3 + resize + skip + time_out 1x1 (4 -> 2) as one pass over the 48-channel input (dec_last.hip)
-        KStage kst("tdec3");
-        DecLastDesc dl;
-        dl.in = b.D; dl.in_bf16 = ab; dl.NI = NI; dl.P = P; dl.H = (int)Lin; dl.T = d.T;
-        dl.fold = c->tlast; dl.skip = svt[0]; dl.skip_bf16 = ab; dl.H_skip = (int)d.L[1]; dl.C_skip = ENC_CH[0];
-        dl.out = b.G;
-        r.check(tdec_last_launch(dl, r.s), "tdec_last");
+        if (!xt2) {
+            // ragged T: level 3 + resize + skip + time_out 1x1 (4 -> 2) over the merged 48-channel input (dec_last.hip)
+            KStage kst("tdec3");
+            DecLastDesc dl;
+            dl.in = b.D; dl.in_bf16 = ab; dl.NI = NI; dl.P = P; dl.H = (int)Lin; dl.T = d.T;
+            dl.fold = c->tlast; dl.skip = svt[0]; dl.skip_bf16 = ab; dl.H_skip = (int)d.L[1]; dl.C_skip = ENC_CH[0];
+            dl.out = b.G;
+            r.check(tdec_last_launch(dl, r.s), "tdec_last");
+            xt2 = b.G;
+        }
     }
     // ---- iSTFT overlap-add + denorm + branch sum (ATHTDemucs_v2.py:310-324) ----
-    combine_launch(b.frames, NI, (int)Ts, d.T, c->win2, b.G, b.tnorm_std + 2 * s0, P, out + s0 * P * 2 * d.T, r.s);
+    b.xt2 = xt2;
+    combine_launch(b.frames, NI, (int)Ts, d.T, c->win2, xt2, b.tnorm_std + 2 * s0, P, out + s0 * P * 2 * d.T, r.s);
 }
 
 // Debug aid: ATHD_DUMP=<dir> makes the forward synchronise at the end and write the main intermediates of the
@@ -602,6 +617,8 @@ void dump_all(const Dims& d, const Bufs& b, hipStream_t s) {
     struct E { std::string name; const void* p; int64_t n; std::string shape; };
     std::vector<E> es = {
         {"spec", b.spec, B * 2048 * Ts * 4, "B,2048,Ts,4"},
+        {"specT", b.specT, B * Ts * 2048 * 4, "B,Ts,2048,4"},
+        {"frames", b.frames, NI * Ts * 2 * 4096, "NI,Ts,2,4096"},
         {"snorm", b.snorm, 2 * B, "B,2"},
         {"tnorm_std", b.tnorm_std, 2 * B, "B,2"},
         {"x_enc", b.x_enc, B * d.Nf * 384, "B,Nf,384"},
@@ -609,7 +626,7 @@ void dump_all(const Dims& d, const Bufs& b, hipStream_t s) {
         {"x_cond", b.x_cond, NI * d.Nf * 384, "NI,Nf,384"},
         {"xt_cond", b.xt_cond, NI * d.Nt * 384, "NI,Nt,384"},
         {"FO", b.FO, NI * Ts * Ts * 2, "NI,t,row,2"},
-        {"XT2", b.G, NI * d.T * 2, "NI,T,2"},
+        {"XT2", b.xt2, NI * d.T * 2, "NI,T,2"},
     };
     for (int i = 0; i < 4 && b.ea == 4; ++i) {      // encoder activations are f32 only in parity mode
         es.push_back({"saved" + std::to_string(i), b.saved[i], B * d.F[i + 1] * Ts * ENC_CH[i], "B,F,Ts,C"});

@@ -111,9 +111,19 @@ struct DecLastDesc {
     const float* fold = nullptr;
     const void* skip = nullptr; int skip_bf16 = 0; int H_skip = 0; int C_skip = 0;
     float* out = nullptr;
+    // dec_tail: the level-2 merge (GroupNorm -> GELU -> resize -> + 0.1 resize(skip2[:, :48])) fused in front, so the
+    // 48-channel input x is computed from the level-2 ConvT output g instead of read from `in`:
+    //   freq: g = kept slots [NI][2H][W][48] (logical rows 4d+1, 4d+2); time: g = [NI][Hg][48] (Hg = 4 L2 rows)
+    const void* g = nullptr; int g_bf16 = 0; int Hg = 0;
+    const double* stats = nullptr; int64_t gn_count = 0; const float* gn_w = nullptr; const float* gn_b = nullptr;
+    int fast_gelu = 0;
+    const void* skip2 = nullptr; int skip2_bf16 = 0; int H_skip2 = 0; int C_skip2 = 0;
 };
 int fdec_last_launch(const DecLastDesc& d, hipStream_t s);
 int tdec_last_launch(const DecLastDesc& d, hipStream_t s);
+int fdec_tail_launch(const DecLastDesc& d, hipStream_t s);
+bool tdec_tail_supported(const DecLastDesc& d);     // 4 H == T and every block's g rows fit its LDS tile
+int tdec_tail_launch(const DecLastDesc& d, hipStream_t s);
 // dconv.hip: one DConv layer (conv3 -> GN -> GELU -> 1x1 -> GN -> GLU -> LayerScale -> residual) for C in {48, 96}
 // x: [nb][L][C] f32 or bf16 (x_bf16), updated in place; h: [nb][L][C/8] f32 scratch
 int dconv_small_launch(void* x, int x_bf16, float* h, int64_t nb, int64_t L, int C, int dil, const float* w3,

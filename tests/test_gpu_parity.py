@@ -96,6 +96,36 @@ def test_full_segment_6s(models, oracle_model, text_table, dt):
     assert s >= thr and s_fix >= thr, (s, s_fix)
 
 
+PHASE_COND_MIN = 5e-8
+
+
+def _phase_cond(z):
+    """min |m + 1e-8| over the nonzero CaC magnitudes the reference divides by (`phase = z / (mag + 1e-8)`,
+    ATHTDemucs_v2.py:308; mag[:, :2] = Re, Im of the left channel).  Where a bin has m close to -1e-8 the mask
+    formula is singular: its output depends on the last bits of that STFT bin, which no two FFTs share (a bin
+    with |m + 1e-8| = 4e-9 costs ~50 dB of whole-output SDR).  Parity inputs are chosen away from that set."""
+    zl = z[:, 0].numpy()
+    m = np.stack([zl.real, zl.imag])
+    return float(np.abs(m + 1e-8)[m != 0].min())
+
+
+@pytest.mark.parametrize("T", [30001, 44102, 9999])
+def test_ragged_length(models, oracle_model, text_table, T):
+    """T % 4 != 0: the time encoder's right pad and the time decoder's last ConvT output (4 L1 samples) linearly
+    resized to T (ATHTDemucs_v2.py:128-131), the general branch of tdec_last (dec_last.hip)."""
+    from athd.synth import synthetic_batch
+    wav = torch.as_tensor(synthetic_batch(1, T, seed0=6))
+    cap = {}
+    ref = oracle_model.forward(wav, torch.as_tensor(text_table[1:2]), capture=cap).numpy()
+    assert _phase_cond(cap["z"]) >= PHASE_COND_MIN
+    for dt in ("f32", "bf16"):
+        out = models[dt](wav.cuda(), "bass").cpu().numpy()
+        assert out.shape == ref.shape
+        s = sdr_db(ref, out)
+        _report(f"ragged_T{T}/{dt}", {"sdr_db_vs_oracle": s})
+        assert s >= (F32_SDR_DB if dt == "f32" else BF16_SDR_DB), (dt, s)
+
+
 def test_forward_prompts_matches_forward(models):
     """Encode-once/decode-P path == P separate forwards.  f32 model: equal to fp32 rounding (GroupNorm statistics
     are fp64 atomics whose order varies); bf16 model: the two paths agree to >= 40 dB (order-dependent statistics
@@ -124,16 +154,18 @@ def test_batch_independence(models):
     assert torch.allclose(full[1:2], one, atol=1e-5, rtol=1e-5)
 
 
-def test_intermediates_f32(models, oracle_model, text_table):
-    """Stage-by-stage parity (f32) via the ATHD_DUMP debug dump: localises any divergence."""
+@pytest.mark.parametrize("T", [30000, 30001])
+def test_intermediates_f32(models, oracle_model, text_table, T):
+    """Stage-by-stage parity (f32) via the ATHD_DUMP debug dump: localises any divergence.  T = 30001 runs the
+    ragged-length paths (time encoder right pad, last time level resized 4 L1 -> T)."""
     from athd.synth import synthetic_batch
-    B, T = 2, 30000
-    wav = torch.as_tensor(synthetic_batch(B, T, seed0=5))
+    B = 2
+    wav = torch.as_tensor(synthetic_batch(B, T, seed0=5 if T == 30000 else 6))
     te = torch.as_tensor(text_table[[0, 3]])
     with tempfile.TemporaryDirectory() as tmp:
         os.environ["ATHD_DUMP"] = tmp
         try:
-            models["f32"](wav.cuda(), ["drums", "vocals"])
+            out = models["f32"](wav.cuda(), ["drums", "vocals"]).cpu().numpy()
             torch.cuda.synchronize()
         finally:
             del os.environ["ATHD_DUMP"]
@@ -142,8 +174,10 @@ def test_intermediates_f32(models, oracle_model, text_table):
             name, n, _ = line.split()
             dump[name] = np.fromfile(os.path.join(tmp, name + ".f32"), dtype=np.float32, count=int(n))
     cap = {}
-    oracle_model.forward(wav, te, capture=cap)
+    ref_out = oracle_model.forward(wav, te, capture=cap).numpy()
     Ts = cap["z"].shape[-1]
+    if T != 30000:
+        assert _phase_cond(cap["z"]) >= PHASE_COND_MIN
     res = {}
 
     def cmp(name, ref, got):
@@ -155,6 +189,22 @@ def test_intermediates_f32(models, oracle_model, text_table):
     z = cap["z"]
     spec = torch.view_as_real(z).permute(0, 2, 3, 1, 4).reshape(B, 2048, Ts, 4).numpy()
     cmp("spec", spec, dump["spec"])
+    cmp("specT", spec.transpose(0, 2, 1, 3), dump["specT"])
+    # iSTFT frames: masked spectrum (ATHTDemucs_v2.py:300-309), Nyquist bin zero (HTDemucs._ispec), inverse real
+    # FFT, periodic Hann window, normalized=True (x sqrt(4096) / 4096 per frame)
+    mag = cap["mag"] if "mag" in cap else None
+    zz = z[:, :2].numpy().astype(np.complex128)
+    mask = cap["mask"].numpy().astype(np.float64)
+    m = np.stack([zz[:, 0].real, zz[:, 0].imag], 1) if mag is None else mag[:, :2].numpy()
+    mz = (m * mask) * (zz / (m + 1e-8))                                   # (NI=B here, 2, 2048, Ts)
+    mz = np.concatenate([mz, np.zeros_like(mz[:, :, :1])], 2)            # Nyquist
+    win = 0.5 - 0.5 * np.cos(2 * np.pi * np.arange(4096) / 4096)
+    fr = np.fft.irfft(mz, n=4096, axis=2) * 64.0 * win[None, None, :, None]   # (B, 2, 4096, Ts)
+    cmp("frames", fr.transpose(0, 3, 1, 2), dump["frames"])
+    if os.environ.get("ATHD_TEST_SAVE"):
+        np.savez(os.path.join(REPO, "gpurun_out", f"frames_T{T}.npz"), ref=fr.transpose(0, 3, 1, 2).astype(np.float32),
+                 got=dump["frames"].reshape(fr.shape[0], fr.shape[3], 2, 4096), mask=mask.astype(np.float32),
+                 fo=dump["FO"], spec=dump["spec"])
     for i in range(4):
         cmp(f"saved{i}", cap["saved"][i].permute(0, 2, 3, 1).numpy(), dump[f"saved{i}"])
         cmp(f"saved_t{i}", cap["saved_t"][i].permute(0, 2, 1).numpy(), dump[f"saved_t{i}"])
@@ -164,7 +214,9 @@ def test_intermediates_f32(models, oracle_model, text_table):
     cmp("xt_cond", cap["xt_cond"].permute(0, 2, 1).numpy(), dump["xt_cond"])
     cmp("FO", cap["x_fo"].permute(0, 3, 2, 1).numpy(), dump["FO"])          # FO^T [item][t][row][2]
     cmp("XT2", cap["xt_out"].permute(0, 2, 1).numpy(), dump["XT2"])      # time_out(time decoder) [item][n][2]
-    _report("intermediates_f32", res)
+    cmp("freq_wav", cap["freq_wav"].numpy(), out - cap["xt_dec"].numpy())
+    cmp("out", ref_out, out)
+    _report(f"intermediates_f32_T{T}", res)
     bad = {k: v for k, v in res.items() if v["sdr_db"] < F32_SDR_DB}
     assert not bad, bad
 
