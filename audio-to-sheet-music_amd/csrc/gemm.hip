@@ -275,11 +275,15 @@ bool gemm2_supported(const GemmDesc& d);
 int gemm2_launch(const GemmDesc& d, hipStream_t s);
 bool gemm3_supported(const GemmDesc& d);
 int gemm3_launch(const GemmDesc& d, hipStream_t s, int variant);
+bool gemm4_supported(const GemmDesc& d);
+int gemm4_launch(const GemmDesc& d, hipStream_t s);
 
 int gemm_launch(const GemmDesc& d, int mode, hipStream_t s) {
     if (d.Kp % BK != 0 || d.Kp < d.K || d.C_in <= 0 || d.N <= 0) return -2;
     if (d.act == ACT_GLU && (d.N % 32 != 0)) return -2;
-    // bf16 activations with N >= 192: 256x192 tile, 8 waves (gemm3.hip); measured best on every large shape here
+    // bf16 activations, N a multiple of 256: 256x256 tile, half-tile staged pipeline (gemm4.hip)
+    if (mode == 1 && gemm4_supported(d) && d.N % 256 == 0) return gemm4_launch(d, s);
+    // other N >= 192: 256x192 tile, 8 waves (gemm3.hip)
     if (mode == 1 && gemm3_supported(d) && d.N >= 192) return gemm3_launch(d, s, 3);
     if (mode == 1 && gemm2_supported(d)) return gemm2_launch(d, s);
     if (mode == 1) launch_mode<1>(d, s);

@@ -232,6 +232,8 @@ ATHD_DEV void gemm_epilogue(const GemmDesc& d, const f32x4_t (&acc)[TM][TN], int
         __syncthreads();
         if (threadIdx.x < EPI_MAXG) {
             const double a = st_lds[2 * threadIdx.x], q = st_lds[2 * threadIdx.x + 1];
+            st_lds[2 * threadIdx.x] = 0.0;          // ready for the next tile of a persistent kernel
+            st_lds[2 * threadIdx.x + 1] = 0.0;
             if (a != 0.0 || q != 0.0) {
                 atomicAdd(&d.stats[2 * (g0 + threadIdx.x)], a);
                 atomicAdd(&d.stats[2 * (g0 + threadIdx.x) + 1], q);

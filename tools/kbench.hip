@@ -9,6 +9,7 @@ using namespace athd;
 namespace athd {
 int gemm2_launch(const GemmDesc& d, hipStream_t s);
 int gemm3_launch(const GemmDesc& d, hipStream_t s, int variant);
+int gemm4_launch(const GemmDesc& d, hipStream_t s);
 }
 
 extern "C" {
@@ -19,6 +20,7 @@ int kb_gemm(int variant, const void* A, int a_bf16, const void* W, const float* 
     d.A = A; d.a_bf16 = a_bf16; d.nb = 1; d.H_in = M; d.W = 1; d.C_in = K; d.a_ld = K; d.H_out = M;
     d.Wp = W; d.N = N; d.K = K; d.Kp = Kp; d.bias = bias; d.C = C; d.c_bf16 = c_bf16; d.H_out_total = M; d.ldo = N;
     d.act = act;
+    if (variant == 40) return gemm4_launch(d, (hipStream_t)stream);
     if (variant == 2) return gemm2_launch(d, (hipStream_t)stream);
     if (variant >= 30) return gemm3_launch(d, (hipStream_t)stream, variant - 30);
     return gemm_launch(d, 1, (hipStream_t)stream);

@@ -6,7 +6,7 @@ import sys
 import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-VARIANTS = (2, 31, 32, 33)
+VARIANTS = (33, 40)
 lib = ctypes.CDLL(os.path.join(HERE, "libkbench.so"))
 vp = ctypes.c_void_p
 
@@ -111,6 +111,14 @@ if __name__ == "__main__":
         attn_case(64, 2072)
         sys.exit(0)
     M = 64 * 2072
+    if "g4" in sys.argv[1:]:
+        gemm_case(M, 1536, 512)
+        gemm_case(M, 2048, 512, act=1)
+        gemm_case(M, 512, 2048)
+        gemm_case(M, 512, 512)
+        gemm_case(4096, 4096, 4096)
+        gemm_case(M, 1536, 512)
+        sys.exit(0)
     gemm_case(M, 1536, 512)
     gemm_case(M, 2048, 512, act=1)
     gemm_case(M, 512, 2048)
