@@ -1,25 +1,24 @@
-// GEMM v4 (bf16 MFMA, gfx950) for the wide layers (N a multiple of 256 or close to it): 256 x 256 x 64 tiles,
-// 8 waves as 2 (M) x 4 (N), each wave 128 x 64 outputs = 8 x 4 accumulator tiles of v_mfma_f32_16x16x32_bf16.
+// GEMM v4 (bf16 MFMA, gfx950) for the wide layers (N a multiple of 256): 256 x 256 x 64 tiles, 8 waves as 2 (M) x
+// 4 (N), each wave 128 x 64 outputs = 8 x 4 accumulator tiles of v_mfma_f32_16x16x32_bf16.
 //
-// Staging (cdna_hip_programming.md §5 "Pipelining across barriers", "The 256² 8-phase template"): two K-tile
-// buffers of four 16 KB half-tile slots, filled by global_load_lds_dwordx4 (lane-linear LDS image, XOR swizzle
-// on the source chunk as in gemm2/gemm3):
+// Staging (cdna_hip_programming.md §5 "Pipelining across barriers"): two K-tile buffers of four 16 KB half-tile
+// slots, filled by global_load_lds_dwordx4 (lane-linear LDS image, XOR swizzle on the source chunk as in
+// gemm2/gemm3):
 //   A0 = tile rows {0..63, 128..191}, A1 = rows {64..127, 192..255}   (slot row sr <-> (sr/64)*128 + 64h + sr%64)
 //   B0 = tile cols {64w + 0..31},     B1 = cols {64w + 32..63}        (slot row sr <-> (sr/32)*64 + 32h + sr%32)
-// so that wave quadrant (mh, nh) of a K-tile reads exactly slots A_mh and B_nh.  A K-tile is computed in four
-// phases, quadrant order (0,0) (0,1) (1,1) (1,0); the B0 fragments stay in registers from the first phase to the
-// last, so each slot is read once, in one phase:
-//   phase 0: read A0, B0        | phase 1: read B1, restage A0, B0 of tile t+2
-//   phase 2: read A1, restage B1 | phase 3: restage A1
-// Every phase starts with [counted vmcnt] + s_barrier: the barrier both publishes the slots the phase reads
-// (their LDS-DMA retired by each issuing wave's vmcnt before it) and retires the previous phase's reads before a
-// slot is restaged.  In steady state two whole K-tiles of loads are in flight (12 glds per wave), so the barrier
-// never drains the load queue (a __syncthreads() would: it waits vmcnt(0)).
+// so that a wave's rows 0..63 / 64..127 read exactly slot A0 / A1.  A K-tile is two phases (A0 against both B
+// halves, then A1): each phase starts with [counted vmcnt] + s_barrier, which both publishes the slots the phase
+// reads (their LDS-DMA retired by each issuing wave's vmcnt before it) and retires the previous phase's reads, so
+// the slots read there can be restaged right after it.  About 1.5 K-tiles of loads stay in flight across every
+// barrier (a __syncthreads() would drain them: it waits vmcnt(0)).  Register budget (2 waves per SIMD): 128
+// accumulators + 64 fragment registers + compact 32-bit addressing, no spills.
 // Same descriptor, implicit-conv A addressing and epilogue (C^T tiles, gemm_epi.h) as the other GEMM kernels.
 #include "common.h"
 #include "prof.h"
 #include "gemm.h"
 #include "gemm_epi.h"
+
+#include <climits>
 
 namespace athd {
 
@@ -52,10 +51,17 @@ ATHD_DEV int xcd_remap4(int i, int n) {
 }  // namespace
 
 __device__ __attribute__((aligned(64))) uint4 g_zero_page4[4];
+#ifdef ATHD_G4_STAMP
+// measurement aid (tools/kbench build only): when set, wave 0 lane 0 of each block records s_memtime at the phase
+// points (kernel start, prologue issued, phase 0 of K-tiles 0, 1 and the last, epilogue start / end)
+__device__ uint64_t* g4_stamp = nullptr;
+constexpr int G4_NSTAMP = 24;
+#endif
 
 template <unsigned F>
 __global__ __launch_bounds__(512) void gemm4_kernel(const GemmDesc d) {
     constexpr int TM = 8, TN = 4;
+    constexpr int NW = 8;
     __shared__ __attribute__((aligned(16))) char smem[8 * G4_SLOT + 2 * EPI_MAXG * 8];
     double* st_lds = reinterpret_cast<double*>(smem + 8 * G4_SLOT);
 
@@ -65,6 +71,17 @@ __global__ __launch_bounds__(512) void gemm4_kernel(const GemmDesc d) {
     const int wm0 = wr * 128, wn0 = wc * 64;
     const int64_t M = (int64_t)d.nb * d.H_out * d.W;
     const int ntn = (d.N + 255) / 256;
+#ifdef ATHD_G4_STAMP
+    uint64_t* stamp = g4_stamp && tid == 0 ? g4_stamp + (int64_t)blockIdx.x * G4_NSTAMP : nullptr;
+    int nst = 0;
+    auto mark = [&]() {
+        if (stamp && nst < G4_NSTAMP) stamp[nst] = __builtin_amdgcn_s_memtime();
+        ++nst;
+    };
+#else
+    auto mark = [&]() {};
+#endif
+    mark();
     // XCD-aware order (T1): the N tiles of one M tile are consecutive ids on one XCD, sharing its A rows in L2
     const int id = xcd_remap4(blockIdx.x, gridDim.x);
     const int64_t m0 = (int64_t)(id / ntn) * 256;
@@ -75,30 +92,30 @@ __global__ __launch_bounds__(512) void gemm4_kernel(const GemmDesc d) {
     const int chunk = (lane & 7) ^ lrow;       // global 16-B chunk this lane fetches (LDS slot = chunk ^ row&7)
     const char* zero = reinterpret_cast<const char*>(g_zero_page4);
 
-    // this lane's slot rows: sr = 8 (wave + 8 q) + lrow, q = 0, 1 (both slot halves h use the same sr)
-    int64_t a_base[2][2];
+    // this lane's slot rows: sr = 8 (wave + 8 q) + lrow, q = 0, 1 (both slot halves h use the same sr).
+    // 32-bit element offsets (gemm4_supported: A < 2^31 elements, N % 256 == 0 so every B row exists); a row past M
+    // gets a_h0 = INT_MIN / 2, which fails the row >= 0 test for every tap.
+    uint32_t a_base[2][2];
     int a_h0[2][2];
-    bool a_ok[2][2];
-    const char* bptr[2][2];
+    uint32_t b_off[2];
 #pragma unroll
     for (int h = 0; h < 2; ++h)
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
-            const int sr = 8 * (wave + 8 * q) + lrow;
+            const int sr = 8 * (wave + NW * q) + lrow;
             const int r = (sr >> 6) * 128 + 64 * h + (sr & 63);
             const uint32_t m = (uint32_t)(m0 + r);
-            a_ok[h][q] = m < (uint32_t)M;
-            const uint32_t mm = a_ok[h][q] ? m : 0u;
+            const bool ok = m < (uint32_t)M;
+            const uint32_t mm = ok ? m : 0u;
             const uint32_t w = mm % (uint32_t)d.W;
             const uint32_t t = mm / (uint32_t)d.W;
             const uint32_t ho = t % (uint32_t)d.H_out;
             const uint32_t b = t / (uint32_t)d.H_out;
-            a_base[h][q] = (int64_t)b * a_bs + (int64_t)w * d.a_ld;
-            a_h0[h][q] = (int)ho * d.in_stride + d.in_off;
-            const int c = (sr >> 5) * 64 + 32 * h + (sr & 31);
-            const int n = n0 + c;
-            bptr[h][q] = n < d.N ? (const char*)d.Wp + ((int64_t)n * d.Kp + 8 * chunk) * 2 : nullptr;
+            a_base[h][q] = (uint32_t)(b * a_bs + (int64_t)w * d.a_ld);
+            a_h0[h][q] = ok ? (int)ho * d.in_stride + d.in_off : (INT_MIN / 2);
+            if (h == 0) b_off[q] = (uint32_t)(((int64_t)(n0 + (sr >> 5) * 64 + (sr & 31)) * d.Kp + 8 * chunk) * 2);
         }
+    const uint32_t b_h1 = (uint32_t)(32 * d.Kp * 2);     // slot B1 rows are 32 columns further
     const int nk = d.Kp / 64;
 
     auto issueA = [&](int kt, int h) {
@@ -109,18 +126,17 @@ __global__ __launch_bounds__(512) void gemm4_kernel(const GemmDesc d) {
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
             const int row = a_h0[h][q] + tap * d.dil;
-            const bool ok = a_ok[h][q] && kok && row >= 0 && row < d.H_in;
-            const char* src = ok ? (const char*)d.A + (a_base[h][q] + (int64_t)row * rowpitch + ci) * 2 : zero;
-            __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(dst + (wave + 8 * q) * 1024), 16, 0, 0);
+            const bool ok = kok && row >= 0 && row < d.H_in;
+            const char* src = ok ? (const char*)d.A + ((int64_t)a_base[h][q] + (int64_t)row * rowpitch + ci) * 2 : zero;
+            __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(dst + (wave + NW * q) * 1024), 16, 0, 0);
         }
     };
     auto issueB = [&](int kt, int h) {
         char* dst = smem + ((kt & 1) * 4 + 2 + h) * G4_SLOT;
+        const char* wb = (const char*)d.Wp + (int64_t)kt * 128 + (h ? b_h1 : 0u);
 #pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            const char* src = bptr[h][q] ? bptr[h][q] + (int64_t)kt * 128 : zero;
-            __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(dst + (wave + 8 * q) * 1024), 16, 0, 0);
-        }
+        for (int q = 0; q < 2; ++q)
+            __builtin_amdgcn_global_load_lds((gbl_void*)(wb + b_off[q]), (lds_void*)(dst + (wave + NW * q) * 1024), 16, 0, 0);
     };
 
     const int fr = lane & 15, g = lane >> 4;
@@ -159,60 +175,67 @@ __global__ __launch_bounds__(512) void gemm4_kernel(const GemmDesc d) {
     };
     if (d.stats && tid < 2 * EPI_MAXG) st_lds[tid] = 0.0;
 
-    // prologue: tiles 0 and 1 in the steady-state issue order (A0 B0 | B1 | A1)
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-        if (t < nk) {
-            issueA(t, 0);
-            issueB(t, 0);
-            issueB(t, 1);
-            issueA(t, 1);
-        }
-
+    // Two phases per K-tile (2 glds per slot and wave):
+    //   phase A(t): publish A0, B0, B1 (t); restage A1 <- t+1 (its last reads were phase B(t-1)); read A0, B0, B1;
+    //               MFMA (A0, B0), (A0, B1)
+    //   phase B(t): publish A1(t); restage A0, B0, B1 <- t+2 (last read in phase A(t)); read A1; MFMA (A1, B1),
+    //               (A1, B0)
+    // Issue order: ... A0B0B1(t) | A1(t) | A0B0B1(t+1) | A1(t+1) | ...  (each load gets ~1.5 K-tiles to land)
+    // prologue: A0 B0 B1 (0), A1 (0), A0 B0 B1 (1)
+    issueA(0, 0);
+    issueB(0, 0);
+    issueB(0, 1);
+    issueA(0, 1);
+    if (nk > 1) {
+        issueA(1, 0);
+        issueB(1, 0);
+        issueB(1, 1);
+    }
+    mark();
     bf16v8 af[4][2], bf0[2][2], bf1[2][2];
     for (int t = 0; t < nk; ++t) {
         const int buf = t & 1;
-        const bool has_next = t + 1 < nk;       // tile t+1's 8 glds were issued before tile t's phases
-        const bool issue2 = t + 2 < nk;         // tile t+2 is restaged during tile t
-        // phase 0: A0, B0 of tile t (issued after them: B1, A1 of tile t [4] + tile t+1 [8])
-        if (has_next) vm_wait<12>();
-        else vm_wait<4>();
-        phase_barrier();
-        readA(buf, 0, af);
-        readB(buf, 0, bf0);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        quad(0, 0, af, bf0);
-        // phase 1: B1 of tile t (after it: A1 of tile t [2] + tile t+1 [8]); restage A0, B0 with tile t+2
-        if (has_next) vm_wait<10>();
+        const bool has1 = t + 1 < nk, has2 = t + 2 < nk;
+        // phase A: after A0B0B1(t): A1(t) [2] + A0B0B1(t+1) [6]
+        if (has1) vm_wait<8>();
         else vm_wait<2>();
         phase_barrier();
-        if (issue2) {
-            issueA(t + 2, 0);
-            issueB(t + 2, 0);
-        }
+        if (t < 2 || t == nk - 1) mark();
+        if (has1) issueA(t + 1, 1);
+        readA(buf, 0, af);
+        readB(buf, 0, bf0);
         readB(buf, 1, bf1);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        quad(0, 0, af, bf0);
         quad(0, 1, af, bf1);
-        // phase 2: A1 of tile t (after it: tile t+1 [8] + A0, B0 of tile t+2 [4]); restage B1
-        if (issue2) vm_wait<12>();
-        else if (has_next) vm_wait<8>();
+        // phase B: after A1(t): A0B0B1(t+1) [6] + A1(t+1) [2]
+        if (has1) vm_wait<8>();
         else vm_wait<0>();
         phase_barrier();
-        if (issue2) issueB(t + 2, 1);
+        if (has2) {
+            issueA(t + 2, 0);
+            issueB(t + 2, 0);
+            issueB(t + 2, 1);
+        }
         readA(buf, 1, af);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         quad(1, 1, af, bf1);
-        // phase 3: restage A1 (every wave's phase-2 reads retired by the barrier); B0 still in registers
-        phase_barrier();
-        if (issue2) issueA(t + 2, 1);
         quad(1, 0, af, bf0);
     }
+    mark();
     gemm_epilogue<TM, TN, F, true>(d, acc, m0, n0, wm0, wn0, lane, st_lds, 256);
+#ifdef ATHD_G4_STAMP
+    if (stamp) {
+        __builtin_amdgcn_s_waitcnt(0);
+        mark();
+        stamp[G4_NSTAMP - 1] = nst;
+    }
+#endif
 }
 
 bool gemm4_supported(const GemmDesc& d) {
+    const int64_t a_elems = (d.a_bs >= 0 ? d.a_bs : (int64_t)d.H_in * d.W * d.a_ld) * d.nb;
     return d.a_bf16 && !d.a_norm && d.C_in % 8 == 0 && d.a_ld % 8 == 0 && d.a_cs == 1 && d.Kp % 64 == 0 &&
-           d.N >= 256 && d.col_split % 4 == 0 && (d.act != ACT_GLU || d.N % 32 == 0);
+           d.N % 256 == 0 && (int64_t)d.N * d.Kp * 2 < (1LL << 31) && a_elems < (1LL << 31) &&
+           d.col_split % 4 == 0 && (d.act != ACT_GLU || d.N % 32 == 0);
 }
 
 template <unsigned F>
@@ -227,6 +250,12 @@ static void launch4f(const GemmDesc& d, hipStream_t s) {
     }
     hipLaunchKernelGGL((gemm4_kernel<F>), dim3((unsigned)tiles), dim3(512), 0, s, d);
 }
+
+#ifdef ATHD_G4_STAMP
+extern "C" int athd_g4_stamp_set(uint64_t* p) {
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(g4_stamp), &p, sizeof(p));
+}
+#endif
 
 int gemm4_launch(const GemmDesc& d, hipStream_t s) {
     switch (epi_flags(d)) {

@@ -97,8 +97,45 @@ def tr_probe():
         print(f"TR lane {lane:2d}: " + " ".join(f"({v // 256},{v % 256})" for v in o[lane]), flush=True)
 
 
+def g4_stamps(M, N, K, act=0):
+    """Per-block s_memtime stamps of one gemm4 launch: where a 256x256 tile's time goes."""
+    import numpy as np
+    dev = "cuda"
+    A = (torch.randn(M, K, device=dev) * 0.5).to(torch.bfloat16)
+    Kp = (K + 63) // 64 * 64
+    W = (torch.randn(N, Kp, device=dev) * 0.05).to(torch.bfloat16)
+    bias = torch.randn(N, device=dev) * 0.1
+    C = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    st = torch.cuda.current_stream().cuda_stream
+    tiles = ((M + 255) // 256) * ((N + 255) // 256)
+    buf = torch.zeros(tiles * 24, dtype=torch.int64, device=dev)
+    run = lambda: lib.kb_gemm(40, vp(A.data_ptr()), 1, vp(W.data_ptr()), vp(bias.data_ptr()), vp(C.data_ptr()), 1,
+                              M, N, K, Kp, act, vp(st))
+    run()
+    lib.athd_g4_stamp_set(vp(buf.data_ptr()))
+    run()
+    torch.cuda.synchronize()
+    lib.athd_g4_stamp_set(vp(0))
+    s = buf.view(tiles, 24).cpu().numpy()
+    n = int(s[0, 23])
+    t0 = s[:, 0].min()
+    rel = s[:, :n] - t0
+    names = ["start", "issued", "kt0", "kt1", "ktlast", "epi", "end"][:n]
+    d = np.diff(s[:, :n], axis=1)
+    print(f"G4STAMP M={M} N={N} K={K}: tiles={tiles} stamps={n} span={(s[:, n-1].max() - t0)} (s_memtime ticks)")
+    for i in range(n - 1):
+        print(f"  {names[i]:>7s}->{names[i+1]:<7s} median {np.median(d[:, i]):9.0f}  p10 {np.percentile(d[:, i], 10):9.0f}  p90 {np.percentile(d[:, i], 90):9.0f}")
+    starts = np.sort(rel[:, 0])
+    print("  block start times (pct 0,10,50,90,100):", [int(np.percentile(starts, p)) for p in (0, 10, 50, 90, 100)])
+
+
 if __name__ == "__main__":
     torch.manual_seed(0)
+    if "stamp" in sys.argv[1:]:
+        g4_stamps(64 * 2072, 1536, 512)
+        g4_stamps(64 * 2072, 512, 2048)
+        g4_stamps(64 * 2072, 2048, 512, act=1)
+        sys.exit(0)
     if "tr" in sys.argv[1:]:
         tr_probe()
     if "convt" in sys.argv[1:]:
