@@ -17,6 +17,14 @@ ATHD_DEV bf16_t f2bf(float f) {
     u += 0x7FFFu + ((u >> 16) & 1u);
     return (bf16_t)(u >> 16);
 }
+// Two floats -> packed bf16 pair (lo = a) by v_cvt_pk_bf16_f32: the same round-to-nearest-even as f2bf for finite
+// values, one instruction for both.
+typedef __attribute__((ext_vector_type(2))) float athd_f2v;
+typedef __attribute__((ext_vector_type(2))) __bf16 athd_b2v;
+ATHD_DEV uint32_t pack2bf(float a, float b) {
+    const athd_b2v r = __builtin_convertvector((athd_f2v){a, b}, athd_b2v);
+    return __builtin_bit_cast(uint32_t, r);
+}
 ATHD_DEV float bf2f(bf16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
 
 ATHD_DEV float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752440f)); }
@@ -37,6 +45,11 @@ ATHD_DEV float gelu_fast(float x) { return 0.5f * x * (1.0f + erf_fast(x * 0.707
 template <bool FAST>
 ATHD_DEV float gelu(float x) { if constexpr (FAST) return gelu_fast(x); else return gelu_erf(x); }
 ATHD_DEV float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
+// bf16-mode sigmoid: v_exp_f32 + v_rcp_f32 (~1 ulp each; 4 instructions vs ~25 for expf and an IEEE divide).  The
+// f32 parity mode keeps sigmoidf_.
+ATHD_DEV float sigmoid_fast(float x) { return __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
+template <bool FAST>
+ATHD_DEV float sigmoid(float x) { if constexpr (FAST) return sigmoid_fast(x); else return sigmoidf_(x); }
 
 ATHD_DEV float wave_sum(float v) {
 #pragma unroll

@@ -227,7 +227,7 @@ __global__ __launch_bounds__(256) void dconv_c1_apply_kernel(TS* __restrict__ x,
         }
         a = (a - m2) * r2 * gw2[c] + gb2[c];
         gt = (gt - m2) * r2 * gw2[C + c] + gb2[C + c];
-        o[q] = scl[c] * (a * sigmoidf_(gt));
+        o[q] = scl[c] * (a * sigmoid<FAST>(gt));
     }
     uint4* xp = reinterpret_cast<uint4*>(x + p * C + c0);
     uint4 v[2] = {xp[0], xp[1]};

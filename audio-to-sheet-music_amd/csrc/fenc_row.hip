@@ -39,8 +39,7 @@ ATHD_DEV f32x4_t mfma(const bf16x8_t& a, const bf16x8_t& b, const f32x4_t& c) {
 }
 
 ATHD_DEV void st4bf(bf16_t* p, float a, float b, float c, float d) {
-    bf16_t h[4] = {f2bf(a), f2bf(b), f2bf(c), f2bf(d)};
-    *reinterpret_cast<uint2*>(p) = *reinterpret_cast<const uint2*>(h);
+    *reinterpret_cast<uint2*>(p) = make_uint2(pack2bf(a, b), pack2bf(c, d));
 }
 
 // sum of (s1, s2) over the workgroup; `red` is a fresh [2][FR_NW] slot per call
@@ -72,7 +71,7 @@ ATHD_DEV void gn_from_sums(float s1, float s2, float cnt, float& mean, float& rs
 }  // namespace
 
 template <int CIN, int C>
-__global__ __launch_bounds__(FR_NT) void fenc_row_kernel(const FencRowDesc d) {
+__global__ __launch_bounds__(FR_NT, CIN == 4 ? 3 : 1) void fenc_row_kernel(const FencRowDesc d) {
     constexpr int NCT = C / 16;                  // x channel tiles
     constexpr int MG = FR_NW / NCT;              // m-tile groups per channel tile
     constexpr int MTW = (FR_MT_MAX + MG - 1) / MG;
@@ -86,11 +85,16 @@ __global__ __launch_bounds__(FR_NT) void fenc_row_kernel(const FencRowDesc d) {
     constexpr int HS_P = 40;
     constexpr int K3 = 3 * C, K3S = (K3 + 31) / 32;
     constexpr int KRS = (C + 31) / 32;
-    constexpr int XIN_E = (TPM * XIN_P > TPM * C) ? TPM * XIN_P : TPM * C;   // also the output staging buffer
-    static_assert(C % 16 == 0 && FR_NW % NCT == 0 && KC % KS == 0 && KS % 32 == 0, "fenc_row shape");
+    // LDS: the conv input stage and the DConv hidden tile share one buffer (the conv is done before the first
+    // hidden tile is written); the output row is staged in xs once the rewrite has read it.  C = 48: 52.7 KB and
+    // <= 168 VGPRs (launch bound: 3 waves per SIMD), so two 6-wave workgroups share a CU.
+    constexpr int XIN_E = (TPM * XIN_P > TPM * HS_P) ? TPM * XIN_P : TPM * HS_P;
+    static_assert(C % 16 == 0 && FR_NW % NCT == 0 && KC % KS == 0 && KS % 32 == 0 && (CIN == 4 || CIN % 8 == 0),
+                  "fenc_row shape");
+    static_assert(TPM * C <= (TPM + 2 * FR_HALO) * XS_P, "output staging fits xs");
     __shared__ __attribute__((aligned(16))) bf16_t xin[XIN_E];
     __shared__ __attribute__((aligned(16))) bf16_t xs[(TPM + 2 * FR_HALO) * XS_P];
-    __shared__ __attribute__((aligned(16))) bf16_t hs[TPM * HS_P];
+    bf16_t* const hs = xin;
     __shared__ float red[4][2 * FR_NW];
 
     // row r -> block: the 8 XCDs each take a contiguous run of rows, so neighbouring output rows (which share 4 of
@@ -108,10 +112,9 @@ __global__ __launch_bounds__(FR_NT) void fenc_row_kernel(const FencRowDesc d) {
     const int ct = wave % NCT, mg = wave / NCT;
     const int cb = ct * 16 + 4 * l4;             // first of this lane's 4 x channels
 
-    // zero xs (conv3 zero padding: halo rows and positions >= T) and hs (K padding columns)
+    // zero xs (conv3 zero padding: halo rows and positions >= T)
     for (int i = tid; i < (TPM + 2 * FR_HALO) * XS_P / 8; i += FR_NT)
         reinterpret_cast<uint4*>(xs)[i] = make_uint4(0u, 0u, 0u, 0u);
-    for (int i = tid; i < TPM * HS_P / 8; i += FR_NT) reinterpret_cast<uint4*>(hs)[i] = make_uint4(0u, 0u, 0u, 0u);
 
     // ---------------------------------------------------------------- conv (8,1)/(4,1)/(2,0) + GELU
     f32x4_t xr[MTW];
@@ -130,12 +133,9 @@ __global__ __launch_bounds__(FR_NT) void fenc_row_kernel(const FencRowDesc d) {
                     const float* p = (const float*)d.in + (((int64_t)b * T + m) * d.Fin + fi) * 4;
                     const float4 u0 = *reinterpret_cast<const float4*>(p);
                     const float4 u1 = *reinterpret_cast<const float4*>(p + 4);
-                    const float sub = d.a_norm[2 * b], dv = d.a_norm[2 * b + 1];
-                    const float e[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
-                    bf16_t h8[8];
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) h8[j] = f2bf((e[j] - sub) / dv);
-                    v = *reinterpret_cast<const uint4*>(h8);
+                    const float sub = d.a_norm[2 * b], rdv = 1.0f / d.a_norm[2 * b + 1];
+                    v = make_uint4(pack2bf((u0.x - sub) * rdv, (u0.y - sub) * rdv), pack2bf((u0.z - sub) * rdv, (u0.w - sub) * rdv),
+                                   pack2bf((u1.x - sub) * rdv, (u1.y - sub) * rdv), pack2bf((u1.z - sub) * rdv, (u1.w - sub) * rdv));
                 }
             } else {
                 const int k0 = s * KS + q * 8;
@@ -171,6 +171,10 @@ __global__ __launch_bounds__(FR_NT) void fenc_row_kernel(const FencRowDesc d) {
         }
     }
     __syncthreads();
+    // the conv input stage is dead: zero the hidden tile's K padding columns 16..31 (columns 0..15 are written by
+    // every conv3 pass, zeros past H included)
+    for (int i = tid; i < TPM * 2; i += FR_NT)
+        *reinterpret_cast<uint4*>(&hs[(i >> 1) * HS_P + 16 + 8 * (i & 1)]) = make_uint4(0u, 0u, 0u, 0u);
 
     // ---------------------------------------------------------------- DConv: x += LayerScale(GLU(GN(1x1(GELU(GN(conv3(x)))))))
 #pragma unroll 1
@@ -282,7 +286,7 @@ __global__ __launch_bounds__(FR_NT) void fenc_row_kernel(const FencRowDesc d) {
             for (int q = 0; q < 4; ++q) {
                 const float a = (ya[q] + ba[q] - ym) * yr * gwa[q] + gba[q];
                 const float g = (yg[q] + bg[q] - ym) * yr * gwg[q] + gbg[q];
-                xr[i][q] = xr[i][q] + sc[q] * (a * sigmoidf_(g));
+                xr[i][q] = xr[i][q] + sc[q] * (a * sigmoid_fast(g));
             }
             st4bf(&xs[(FR_HALO + m) * XS_P + cb], xr[i][0], xr[i][1], xr[i][2], xr[i][3]);
         }
@@ -305,11 +309,12 @@ __global__ __launch_bounds__(FR_NT) void fenc_row_kernel(const FencRowDesc d) {
             wa[ks] = ldfrag(d.wr + (int64_t)(32 * ct + l15) * d.wr_ld + ks * 32 + 8 * l4);
             wg[ks] = ldfrag(d.wr + (int64_t)(32 * ct + 16 + l15) * d.wr_ld + ks * 32 + 8 * l4);
         }
-        bf16_t* ob = xin;        // output staging [T][C] (the conv input buffer is free)
+        uint2 ov[MTW];           // the wave's output values (bf16 x 4 per m-tile), held until xs is free
 #pragma unroll
         for (int i = 0; i < MTW; ++i) {
             const int mt = mg + MG * i;
             const int m = mt * 16 + l15;
+            ov[i] = make_uint2(0u, 0u);
             if (mt >= MT) continue;
             f32x4_t za = f32x4_t{0.f, 0.f, 0.f, 0.f}, zg = za;
 #pragma unroll
@@ -323,9 +328,17 @@ __global__ __launch_bounds__(FR_NT) void fenc_row_kernel(const FencRowDesc d) {
             if (m < T) {
                 float o[4];
 #pragma unroll
-                for (int q = 0; q < 4; ++q) o[q] = (za[q] + ba[q]) * sigmoidf_(zg[q] + bg[q]) + ra[q];
-                st4bf(&ob[m * C + cb], o[0], o[1], o[2], o[3]);
+                for (int q = 0; q < 4; ++q) o[q] = (za[q] + ba[q]) * sigmoid_fast(zg[q] + bg[q]) + ra[q];
+                ov[i] = make_uint2(pack2bf(o[0], o[1]), pack2bf(o[2], o[3]));
             }
+        }
+        __syncthreads();         // every wave has read xs: stage the output row [T][C] there
+        bf16_t* ob = xs;
+#pragma unroll
+        for (int i = 0; i < MTW; ++i) {
+            const int mt = mg + MG * i;
+            const int m = mt * 16 + l15;
+            if (mt < MT && m < T) *reinterpret_cast<uint2*>(&ob[m * C + cb]) = ov[i];
         }
         __syncthreads();
         bf16_t* dst = d.out + ((int64_t)b * d.Fout + f) * (int64_t)T * C;

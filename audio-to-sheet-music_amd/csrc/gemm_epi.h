@@ -134,7 +134,7 @@ ATHD_DEV void gemm_epilogue(const GemmDesc& d, const f32x4_t (&acc)[TM][TN], int
                             a = (a - gm) * gr * d.gn_w[na + q] + d.gn_b[na + q];
                             g = (g - gm) * gr * d.gn_w[na + 16 + q] + d.gn_b[na + 16 + q];
                         }
-                        float v = a * sigmoidf_(g);
+                        float v = a * sigmoid<FASTG>(g);
                         if (f_row) v += d.row_add[(int64_t)ho * Nout + oc + q];
                         o[q] = v;
                     }
@@ -146,8 +146,7 @@ ATHD_DEV void gemm_epilogue(const GemmDesc& d, const f32x4_t (&acc)[TM][TN], int
                     }
                     if (f_store) {
                         if (f_cbf) {
-                            bf16_t h[4] = {f2bf(o[0]), f2bf(o[1]), f2bf(o[2]), f2bf(o[3])};
-                            *reinterpret_cast<uint2*>((bf16_t*)d.C + obase + oc) = *reinterpret_cast<uint2*>(h);
+                            *reinterpret_cast<uint2*>((bf16_t*)d.C + obase + oc) = make_uint2(pack2bf(o[0], o[1]), pack2bf(o[2], o[3]));
                         } else {
                             *reinterpret_cast<float4*>((float*)d.C + obase + oc) = make_float4(o[0], o[1], o[2], o[3]);
                         }
@@ -190,8 +189,7 @@ ATHD_DEV void gemm_epilogue(const GemmDesc& d, const f32x4_t (&acc)[TM][TN], int
                         }
                         if (st) {
                             if (f_cbf) {
-                                bf16_t h[4] = {f2bf(o[0]), f2bf(o[1]), f2bf(o[2]), f2bf(o[3])};
-                                *reinterpret_cast<uint2*>((bf16_t*)d.C + off) = *reinterpret_cast<uint2*>(h);
+                                *reinterpret_cast<uint2*>((bf16_t*)d.C + off) = make_uint2(pack2bf(o[0], o[1]), pack2bf(o[2], o[3]));
                             } else {
                                 *reinterpret_cast<float4*>((float*)d.C + off) = make_float4(o[0], o[1], o[2], o[3]);
                             }
