@@ -239,7 +239,7 @@ __global__ __launch_bounds__(256) void attn_kernel(const AttnDesc d) {
 typedef short v4i16 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
 
-__global__ __launch_bounds__(256) void attn_bf16_kernel(const AttnDesc d) {
+__global__ __launch_bounds__(256, 3) void attn_bf16_kernel(const AttnDesc d) {
     constexpr int LDK = 72;                        // bf16 per LDS row (64 + 8 pad)
     __shared__ __attribute__((aligned(16))) bf16_t Ks[2][64 * LDK];
     __shared__ __attribute__((aligned(16))) bf16_t Vs[2][64 * LDK];
