@@ -195,6 +195,8 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmDesc d) {
         for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
     if (d.stats && threadIdx.x < 2 * EPI_MAXG) st_lds[threadIdx.x] = 0.0;
+    float4 bias4[TN];                             // loaded before the main loop (gemm_epi.h: load_bias4)
+    load_bias4<TN>(d, n0, wn0, lane, bias4);
     load_tile(0);
     store_tile(0);
     __syncthreads();
@@ -245,7 +247,9 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmDesc d) {
         __syncthreads();
     }
 
-    gemm_epilogue<TM, TN, F_ALL, MODE == 1>(d, acc, m0, n0, wm0, wn0, lane, st_lds, BM);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(bias4[j].x), "v"(bias4[j].y), "v"(bias4[j].z), "v"(bias4[j].w));
+    gemm_epilogue<TM, TN, F_ALL, MODE == 1>(d, acc, m0, n0, wm0, wn0, lane, st_lds, BM, bias4);
 }
 
 template <int MODE, int BM, int BN, int WM, int WN>

@@ -159,6 +159,8 @@ __global__ __launch_bounds__(256) void gemm2_kernel(const GemmDesc d) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
     if (d.stats && tid < 2 * EPI_MAXG) st_lds[tid] = 0.0;
+    float4 bias4[TN];                             // loaded before the main loop (gemm_epi.h: load_bias4)
+    load_bias4<TN>(d, n0, wn0, lane, bias4);
 
     issue(0, 0);
     write_a(0);
@@ -189,7 +191,9 @@ __global__ __launch_bounds__(256) void gemm2_kernel(const GemmDesc d) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
     }
-    gemm_epilogue<TM, TN, F, true>(d, acc, m0, n0, wm0, wn0, lane, st_lds, BM);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(bias4[j].x), "v"(bias4[j].y), "v"(bias4[j].z), "v"(bias4[j].w));
+    gemm_epilogue<TM, TN, F, true>(d, acc, m0, n0, wm0, wn0, lane, st_lds, BM, bias4);
 }
 
 bool gemm2_supported(const GemmDesc& d) {

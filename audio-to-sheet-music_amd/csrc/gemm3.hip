@@ -104,6 +104,8 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm3_kernel(const GemmDesc d) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
     if (d.stats && tid < 2 * EPI_MAXG) st_lds[tid] = 0.0;
+    float4 bias4[TN];                             // loaded before the main loop (gemm_epi.h: load_bias4)
+    load_bias4<TN>(d, n0, wn0, lane, bias4);
 
     // prologue: STAGES-1 tiles in flight, wait for tile 0
 #pragma unroll
@@ -141,7 +143,9 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm3_kernel(const GemmDesc d) {
         __builtin_amdgcn_s_barrier();
         cur = cur + 1 == STAGES ? 0 : cur + 1;
     }
-    gemm_epilogue<TM, TN, F, true>(d, acc, m0, n0, wm0, wn0, lane, st_lds, BM);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(bias4[j].x), "v"(bias4[j].y), "v"(bias4[j].z), "v"(bias4[j].w));
+    gemm_epilogue<TM, TN, F, true>(d, acc, m0, n0, wm0, wn0, lane, st_lds, BM, bias4);
 }
 
 bool gemm3_supported(const GemmDesc& d) {

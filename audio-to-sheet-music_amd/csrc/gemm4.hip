@@ -16,6 +16,17 @@
 #include "common.h"
 #include "prof.h"
 #include "gemm.h"
+#ifdef ATHD_G4_STAMP
+namespace athd {
+__device__ uint64_t* g4_stamp = nullptr;
+constexpr int G4_NSTAMP = 24;
+}
+#define ATHD_EPI_MARK(i)                                                                                       \
+    do {                                                                                                       \
+        if (athd::g4_stamp && threadIdx.x == 0)                                                                \
+            athd::g4_stamp[(int64_t)blockIdx.x * athd::G4_NSTAMP + (i)] = __builtin_amdgcn_s_memtime();        \
+    } while (0)
+#endif
 #include "gemm_epi.h"
 
 #include <climits>
@@ -51,12 +62,8 @@ ATHD_DEV int xcd_remap4(int i, int n) {
 }  // namespace
 
 __device__ __attribute__((aligned(64))) uint4 g_zero_page4[4];
-#ifdef ATHD_G4_STAMP
-// measurement aid (tools/kbench build only): when set, wave 0 lane 0 of each block records s_memtime at the phase
-// points (kernel start, prologue issued, phase 0 of K-tiles 0, 1 and the last, epilogue start / end)
-__device__ uint64_t* g4_stamp = nullptr;
-constexpr int G4_NSTAMP = 24;
-#endif
+// ATHD_G4_STAMP (tools/kbench build only): wave 0 lane 0 of each block records s_memtime at the phase points
+// (kernel start, prologue issued, phase 0 of K-tiles 0, 1 and the last, epilogue start / end) into g4_stamp.
 
 template <unsigned F>
 __global__ __launch_bounds__(512) void gemm4_kernel(const GemmDesc d) {
@@ -174,6 +181,17 @@ __global__ __launch_bounds__(512) void gemm4_kernel(const GemmDesc d) {
                         __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][ks], af[i][ks], acc[4 * mh + i][2 * nh + j], 0, 0, 0);
     };
     if (d.stats && tid < 2 * EPI_MAXG) st_lds[tid] = 0.0;
+    float4 bias4[TN];                             // loaded now: retired long before the epilogue needs it
+    load_bias4<TN>(d, n0, wn0, lane, bias4);
+    // Desynchronise the first wave of workgroups (one per CU): with equal tiles everywhere every CU would reach its
+    // epilogue at the same moment, and the C stores of all CUs share the HBM write bandwidth (~7 B/clk/CU when all
+    // store at once) while the matrix cores idle.  Offsetting the CUs by quarter tiles lets one CU's store burst
+    // overlap the others' K-loops; later workgroups inherit the offsets.
+    if (blockIdx.x < 256) {
+        const int q = (int)(blockIdx.x >> 3) & 3;
+        const int n = q * (nk + 5) / 8;
+        for (int i = 0; i < n; ++i) __builtin_amdgcn_s_sleep(127);
+    }
 
     // Two phases per K-tile (2 glds per slot and wave):
     //   phase A(t): publish A0, B0, B1 (t); restage A1 <- t+1 (its last reads were phase B(t-1)); read A0, B0, B1;
@@ -221,11 +239,18 @@ __global__ __launch_bounds__(512) void gemm4_kernel(const GemmDesc d) {
         quad(1, 0, af, bf0);
     }
     mark();
-    gemm_epilogue<TM, TN, F, true>(d, acc, m0, n0, wm0, wn0, lane, st_lds, 256);
+    // consume the bias registers once, unconditionally: the compiler places their (now free) vmcnt wait here instead
+    // of before every branch-guarded use
+#pragma unroll
+    for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(bias4[j].x), "v"(bias4[j].y), "v"(bias4[j].z), "v"(bias4[j].w));
+    gemm_epilogue<TM, TN, F, true>(d, acc, m0, n0, wm0, wn0, lane, st_lds, 256, bias4);
 #ifdef ATHD_G4_STAMP
     if (stamp) {
+        mark();                                  // epilogue issued
         __builtin_amdgcn_s_waitcnt(0);
-        mark();
+        mark();                                  // its stores retired
+        stamp[G4_NSTAMP - 3] = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_ID: CU / SH / SE
+        stamp[G4_NSTAMP - 2] = __builtin_amdgcn_s_getreg((31 << 11) | 20);   // XCC_ID
         stamp[G4_NSTAMP - 1] = nst;
     }
 #endif

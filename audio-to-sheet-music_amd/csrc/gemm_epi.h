@@ -13,6 +13,10 @@ namespace athd {
 
 constexpr int EPI_MAXG = 32;   // GroupNorm groups tracked per block in LDS
 
+#ifndef ATHD_EPI_MARK
+#define ATHD_EPI_MARK(i)           // measurement hook (tools/kbench build of gemm4 only)
+#endif
+
 enum EpiFlag : unsigned {
     F_GELU = 1u, F_GLU = 2u, F_RES = 4u, F_STATS = 8u, F_GN = 16u, F_ROWADD = 32u, F_SPLIT = 64u, F_CBF16 = 128u,
     F_NOSTORE = 256u, F_ALL = 0xFFFFu
@@ -56,9 +60,28 @@ ATHD_DEV void ld_res4(const GemmDesc& d, int64_t off, float* r) {
     }
 }
 
+// Per-column bias of the lane's TN 4-column groups (the epilogue's only loads besides the residual).
+template <int TN>
+ATHD_DEV void load_bias4(const GemmDesc& d, int n0, int wn0, int lane, float4 (&bj)[TN]) {
+    const int fg = lane >> 4;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        const int nb = n0 + wn0 + 16 * j + 4 * fg;
+        bj[j] = (d.bias && nb + 3 < d.N) ? *reinterpret_cast<const float4*>(d.bias + nb) : make_float4(0.f, 0.f, 0.f, 0.f);
+        if (d.bias && nb < d.N && nb + 3 >= d.N) {   // ragged N (N % 4 != 0 never occurs; keep it exact anyway)
+            float t[4] = {0.f, 0.f, 0.f, 0.f};
+            for (int q = 0; q < 4 && nb + q < d.N; ++q) t[q] = d.bias[nb + q];
+            bj[j] = make_float4(t[0], t[1], t[2], t[3]);
+        }
+    }
+}
+
+// bpre: the bias already loaded by the kernel (load_bias4 before its main loop).  Loaded here instead, its
+// vmcnt wait lands inside the per-store branches, where the compiler can only use vmcnt(0): every store then
+// waits for all earlier stores to retire (measured: 16-18k cycles for 32 stores per lane on gemm4).
 template <int TM, int TN, unsigned F, bool FASTG>
 ATHD_DEV void gemm_epilogue(const GemmDesc& d, const f32x4_t (&acc)[TM][TN], int64_t m0, int n0, int wm0, int wn0,
-                            int lane, double* st_lds, int BM) {
+                            int lane, double* st_lds, int BM, const float4* bpre = nullptr) {
     // Transposed accumulators (the kernels issue mfma(W_frag, A_frag)): lane l holds, for tile (i, j), output row
     // m = m0 + wm0 + 16 i + (l & 15) and the 4 consecutive columns n = n0 + wn0 + 16 j + 4 (l >> 4) + {0..3}.
     constexpr bool GEN = F == F_ALL;
@@ -82,31 +105,41 @@ ATHD_DEV void gemm_epilogue(const GemmDesc& d, const f32x4_t (&acc)[TM][TN], int
     if (mlast >= M) mlast = M - 1;
     const bool one_group = (mlast / HW) == g0;                // fast path: the whole tile in one group
     const int64_t hi_off = f_split ? (int64_t)d.hi_row_off * d.W * d.ldo - d.col_split : 0;
+    // one batch of W = 1 rows (the transformer / linear layers): row m is (b, ho, w) = (0, m, 0), no divisions
+    const bool linear = d.W == 1 && d.nb == 1;
+    // paired 16-B bf16 stores (T21): whole 32-column pairs (N % 32 == 0, pair starts 32-aligned), no column split
+    const bool f_wide = TN % 2 == 0 && f_cbf && !f_split && !f_glu && f_store && d.N % 32 == 0 && (n0 + wn0) % 32 == 0;
     float q1 = 0.f, q2 = 0.f;
 
+    ATHD_EPI_MARK(12);
     // per-column constants (hoisted out of the row loop): columns n = nb_j + {0..3}
     float4 bj[TN];
     int grp[TN];     // ConvT residue group of the lane's 4 columns (col_split % 4 == 0: a 4-group never straddles)
+    if (bpre) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) bj[j] = bpre[j];
+    } else {
+        load_bias4<TN>(d, n0, wn0, lane, bj);
+    }
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
         const int nb = n0 + wn0 + 16 * j + 4 * fg;
         grp[j] = f_split ? nb / d.col_split : 0;
-        bj[j] = (d.bias && nb + 3 < d.N) ? *reinterpret_cast<const float4*>(d.bias + nb) : make_float4(0.f, 0.f, 0.f, 0.f);
-        if (d.bias && nb < d.N && nb + 3 >= d.N) {   // ragged N (N % 4 != 0 never occurs; keep it exact anyway)
-            float t[4] = {0.f, 0.f, 0.f, 0.f};
-            for (int q = 0; q < 4 && nb + q < d.N; ++q) t[q] = d.bias[nb + q];
-            bj[j] = make_float4(t[0], t[1], t[2], t[3]);
-        }
     }
+    ATHD_EPI_MARK(13);
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
+        if (i == 1) ATHD_EPI_MARK(14);
         const uint32_t m = (uint32_t)m0 + wm0 + 16 * i + fr;
         float p1 = 0.f, p2 = 0.f;
         if (m < M) {
-            const uint32_t w = m % (uint32_t)d.W;
-            const uint32_t t = m / (uint32_t)d.W;
-            const uint32_t ho = t % (uint32_t)d.H_out;
-            const uint32_t b = t / (uint32_t)d.H_out;
+            uint32_t w = 0, ho = m, b = 0;
+            if (!linear) {
+                w = m % (uint32_t)d.W;
+                const uint32_t t = m / (uint32_t)d.W;
+                ho = t % (uint32_t)d.H_out;
+                b = t / (uint32_t)d.H_out;
+            }
             // signed row arithmetic: o_off may be negative (its row is then masked out by store_mask / hi_row_off)
             const int64_t orow = (int64_t)(int)ho * d.o_stride + d.o_off;
             const int64_t obase = (int64_t)b * c_bs + (orow * d.W + w) * d.ldo + d.col_off;
@@ -153,6 +186,7 @@ ATHD_DEV void gemm_epilogue(const GemmDesc& d, const f32x4_t (&acc)[TM][TN], int
                     }
                 }
             } else {
+                uint2 pk_even = make_uint2(0u, 0u);
 #pragma unroll
                 for (int j = 0; j < TN; ++j) {
                     const int n = n0 + wn0 + 16 * j + 4 * fg;
@@ -188,7 +222,20 @@ ATHD_DEV void gemm_epilogue(const GemmDesc& d, const f32x4_t (&acc)[TM][TN], int
                             off += grp[j] * hi_off;
                         }
                         if (st) {
-                            if (f_cbf) {
+                            if (f_wide) {
+                                // T21 (cdna_hip_programming.md): tiles j, j+1 of one row are trade halves between lane
+                                // groups fg and fg^1 with v_permlane16_swap, so each lane stores 8 consecutive
+                                // columns (16 B) instead of 4: half the store instructions, same bytes
+                                const uint2 pk = make_uint2(pack2bf(o[0], o[1]), pack2bf(o[2], o[3]));
+                                if ((j & 1) == 0) {
+                                    pk_even = pk;
+                                } else {
+                                    const auto rx = __builtin_amdgcn_permlane16_swap(pk_even.x, pk.x, false, false);
+                                    const auto ry = __builtin_amdgcn_permlane16_swap(pk_even.y, pk.y, false, false);
+                                    const int col = n0 + wn0 + 16 * (j - 1) + 16 * (fg & 1) + 8 * (fg >> 1);
+                                    *reinterpret_cast<uint4*>((bf16_t*)d.C + obase + col) = make_uint4(rx[0], ry[0], rx[1], ry[1]);
+                                }
+                            } else if (f_cbf) {
                                 *reinterpret_cast<uint2*>((bf16_t*)d.C + off) = make_uint2(pack2bf(o[0], o[1]), pack2bf(o[2], o[3]));
                             } else {
                                 *reinterpret_cast<float4*>((float*)d.C + off) = make_float4(o[0], o[1], o[2], o[3]);
@@ -219,6 +266,7 @@ ATHD_DEV void gemm_epilogue(const GemmDesc& d, const f32x4_t (&acc)[TM][TN], int
             }
         }
     }
+    ATHD_EPI_MARK(15);
     if (f_stats && one_group) {
         const double t1 = wave_sum_d((double)q1), t2 = wave_sum_d((double)q2);
         if (lane == 0) {

@@ -21,6 +21,8 @@ int kb_gemm(int variant, const void* A, int a_bf16, const void* W, const float* 
     d.Wp = W; d.N = N; d.K = K; d.Kp = Kp; d.bias = bias; d.C = C; d.c_bf16 = c_bf16; d.H_out_total = M; d.ldo = N;
     d.act = act;
     if (variant == 40) return gemm4_launch(d, (hipStream_t)stream);
+    if (variant == 41) { d.store = 0; return gemm4_launch(d, (hipStream_t)stream); }   // timing probe: no C stores
+    if (variant == 42) { d.bias = nullptr; return gemm4_launch(d, (hipStream_t)stream); }   // timing probe: no bias
     if (variant == 2) return gemm2_launch(d, (hipStream_t)stream);
     if (variant >= 30) return gemm3_launch(d, (hipStream_t)stream, variant - 30);
     return gemm_launch(d, 1, (hipStream_t)stream);

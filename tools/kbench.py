@@ -109,7 +109,7 @@ def g4_stamps(M, N, K, act=0):
     st = torch.cuda.current_stream().cuda_stream
     tiles = ((M + 255) // 256) * ((N + 255) // 256)
     buf = torch.zeros(tiles * 24, dtype=torch.int64, device=dev)
-    run = lambda: lib.kb_gemm(40, vp(A.data_ptr()), 1, vp(W.data_ptr()), vp(bias.data_ptr()), vp(C.data_ptr()), 1,
+    run = lambda: lib.kb_gemm(int(os.environ.get("G4V", "40")), vp(A.data_ptr()), 1, vp(W.data_ptr()), vp(bias.data_ptr()), vp(C.data_ptr()), 1,
                               M, N, K, Kp, act, vp(st))
     run()
     lib.athd_g4_stamp_set(vp(buf.data_ptr()))
@@ -120,13 +120,34 @@ def g4_stamps(M, N, K, act=0):
     n = int(s[0, 23])
     t0 = s[:, 0].min()
     rel = s[:, :n] - t0
-    names = ["start", "issued", "kt0", "kt1", "ktlast", "epi", "end"][:n]
+    names = ["start", "issued", "kt0", "kt1", "ktlast", "epi", "epi_iss", "end"][:n]
     d = np.diff(s[:, :n], axis=1)
     print(f"G4STAMP M={M} N={N} K={K}: tiles={tiles} stamps={n} span={(s[:, n-1].max() - t0)} (s_memtime ticks)")
     for i in range(n - 1):
         print(f"  {names[i]:>7s}->{names[i+1]:<7s} median {np.median(d[:, i]):9.0f}  p10 {np.percentile(d[:, i], 10):9.0f}  p90 {np.percentile(d[:, i], 90):9.0f}")
-    starts = np.sort(rel[:, 0])
-    print("  block start times (pct 0,10,50,90,100):", [int(np.percentile(starts, p)) for p in (0, 10, 50, 90, 100)])
+    e = s[:, 12:16].astype(np.int64)
+    ep = s[:, 5].astype(np.int64)
+    print("  epilogue marks rel. to 'epi' (bias loaded, rows start, row 1, rows done):",
+          [int(np.median(e[:, k] - ep)) for k in range(4)])
+    # per CU: blocks in start order; busy = sum(start -> epilogue issued), gap = next start - this block's end
+    hw = s[:, 21] & 0xFFFFFFFF
+    xcc = s[:, 22] & 0xF
+    cu_key = xcc * 100000 + ((hw >> 13) & 7) * 1000 + ((hw >> 12) & 1) * 100 + ((hw >> 8) & 15)
+    gaps, busy_frac, inflight = [], [], []
+    for key in np.unique(cu_key):
+        idx = np.where(cu_key == key)[0]
+        st = s[idx, 0]
+        o = np.argsort(st)
+        st = st[o]
+        ei = s[idx, 6][o]
+        en = s[idx, 7][o]
+        span = en.max() - st.min()
+        busy_frac.append((ei - st).sum() / max(span, 1))
+        gaps.extend(list(st[1:] - en[:-1]))
+        inflight.append(len(idx))
+    gaps = np.array(gaps)
+    print(f"  CUs={len(busy_frac)} blocks/CU median {np.median(inflight):.0f}; per-CU sum(start->epi issued)/span median {np.median(busy_frac):.2f}")
+    print(f"  gap next-start minus prev-end: median {np.median(gaps):.0f} p10 {np.percentile(gaps, 10):.0f} p90 {np.percentile(gaps, 90):.0f}")
 
 
 if __name__ == "__main__":
@@ -148,6 +169,13 @@ if __name__ == "__main__":
         attn_case(64, 2072)
         sys.exit(0)
     M = 64 * 2072
+    if "nostore" in sys.argv[1:]:
+        VARIANTS = (40, 41, 42)
+        gemm_case(M, 1536, 512)
+        gemm_case(M, 2048, 512, act=1)
+        gemm_case(M, 512, 2048)
+        gemm_case(M, 512, 512)
+        sys.exit(0)
     if "g4" in sys.argv[1:]:
         gemm_case(M, 1536, 512)
         gemm_case(M, 2048, 512, act=1)
