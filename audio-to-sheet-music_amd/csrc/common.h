@@ -41,7 +41,12 @@ ATHD_DEV float erf_fast(float x) {
     const float e = __builtin_amdgcn_exp2f(-ax * ax * 1.4426950408889634f);
     return copysignf(fmaf(-p, e, 1.0f), x);
 }
-ATHD_DEV float gelu_fast(float x) { return 0.5f * x * (1.0f + erf_fast(x * 0.70710678118654752440f)); }
+// bf16-mode GELU: the tanh form x * sigmoid(sqrt(8/pi) (x + 0.044715 x^3)) on v_exp_f32 + v_rcp_f32, 7 VALU ops.
+// |gelu_fast - gelu_erf| <= 4.8e-4 absolute (at x ~ 2.7, value 2.69: 1.8e-4 relative, below half a bf16 ulp).
+ATHD_DEV float gelu_fast(float x) {
+    const float u = x * fmaf(0.044715f * 1.5957691216057308f, x * x, 1.5957691216057308f);
+    return x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(u * -1.4426950408889634f));
+}
 template <bool FAST>
 ATHD_DEV float gelu(float x) { if constexpr (FAST) return gelu_fast(x); else return gelu_erf(x); }
 ATHD_DEV float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }

@@ -40,27 +40,13 @@ ATHD_DEV f2 ld2(const T* p) {
     }
 }
 
-// GELU with the branch-free erf of common.h::erf_fast on a packed pair (bf16 mode), or exact erf (f32 mode)
+// GELU on a packed pair: common.h::gelu_fast's tanh form (bf16 mode) or exact erf (f32 mode)
 template <bool FAST>
 ATHD_DEV f2 gelu2(f2 x) {
     if constexpr (!FAST) {
         return (f2){gelu_erf(x.x), gelu_erf(x.y)};
     } else {
-        const f2 u = x * splat(0.70710678118654752440f);
-        const f2 ax = (f2){fabsf(u.x), fabsf(u.y)};
-        const f2 den = pfma(splat(0.3275911f), ax, splat(1.0f));
-        const f2 t = (f2){__builtin_amdgcn_rcpf(den.x), __builtin_amdgcn_rcpf(den.y)};
-        f2 p = pfma(splat(1.061405429f), t, splat(-1.453152027f));
-        p = pfma(p, t, splat(1.421413741f));
-        p = pfma(p, t, splat(-0.284496736f));
-        p = pfma(p, t, splat(0.254829592f));
-        p = p * t;
-        const f2 q = ax * (ax * splat(-1.4426950408889634f));
-        const f2 e = (f2){__builtin_amdgcn_exp2f(q.x), __builtin_amdgcn_exp2f(q.y)};
-        const f2 em = pfma(-p, e, splat(1.0f));
-        const f2 erf = (f2){copysignf(em.x, u.x), copysignf(em.y, u.y)};
-        const f2 h = x * splat(0.5f);
-        return pfma(h, erf, h);
+        return (f2){gelu_fast(x.x), gelu_fast(x.y)};
     }
 }
 
