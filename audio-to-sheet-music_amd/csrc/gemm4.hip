@@ -243,6 +243,12 @@ __global__ __launch_bounds__(512) void gemm4_kernel(const GemmDesc d) {
     // of before every branch-guarded use
 #pragma unroll
     for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(bias4[j].x), "v"(bias4[j].y), "v"(bias4[j].z), "v"(bias4[j].w));
+    if constexpr ((F & F_RES) != 0 && (F & ~(F_RES | F_STATS)) == 0) {
+        if (epi_res_fast_ok(d)) {
+            gemm_epilogue_res<TM, TN, F>(d, acc, m0, n0, wm0, wn0, lane, st_lds, 256, bias4);
+            return;
+        }
+    }
     gemm_epilogue<TM, TN, F, true>(d, acc, m0, n0, wm0, wn0, lane, st_lds, 256, bias4);
 #ifdef ATHD_G4_STAMP
     if (stamp) {

@@ -288,4 +288,126 @@ ATHD_DEV void gemm_epilogue(const GemmDesc& d, const f32x4_t (&acc)[TM][TN], int
     }
 }
 
+// Residual-stream epilogue (F_RES [+ F_STATS], f32 output and residual, dense rows: row m at m*ldo): out = res +
+// res_scale * (acc + bias), GroupNorm statistics of out.  Written branch-free - rows past M read a clamped row and
+// store into a sink line - with the residual loads of row tile i+1 issued before the stores of tile i.  The compiler
+// then counts vmcnt exactly (straight-line code): a residual load waits only for the stores issued before it, two
+// tiles back, instead of vmcnt(0) behind every store (gemm_epilogue's branch-guarded loads).
+__device__ __attribute__((weak)) float4 g_epi_sink[64];
+
+ATHD_HD bool epi_res_fast_ok(const GemmDesc& d) {
+    return d.res && !d.res_bf16 && !d.c_bf16 && d.store && d.act == ACT_NONE && !d.gn_stats && !d.row_add &&
+           !d.col_split && d.o_stride == 1 && d.o_off == 0 && d.H_out_total == d.H_out && d.c_bs < 0 && d.N % 4 == 0;
+}
+
+template <int TM, int TN, unsigned F>
+ATHD_DEV void gemm_epilogue_res(const GemmDesc& d, const f32x4_t (&acc)[TM][TN], int64_t m0, int n0, int wm0, int wn0,
+                                int lane, double* st_lds, int BM, const float4* bj) {
+    constexpr bool f_stats = (F & F_STATS) != 0;
+    const int fr = lane & 15, fg = lane >> 4;
+    const uint32_t M = (uint32_t)d.nb * d.H_out * d.W;
+    const uint32_t HW = (uint32_t)d.H_out * d.W;
+    const uint32_t g0 = (uint32_t)(m0 / HW);
+    uint32_t mlast = (uint32_t)m0 + (uint32_t)BM - 1;
+    if (mlast >= M) mlast = M - 1;
+    const bool one_group = (mlast / HW) == g0;
+    int ncol[TN];
+    float4 sc[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        ncol[j] = n0 + wn0 + 16 * j + 4 * fg;
+        const int nc = ncol[j] < d.N ? ncol[j] : d.N - 4;
+        ncol[j] = nc;
+        sc[j] = d.res_scale ? *reinterpret_cast<const float4*>(d.res_scale + nc) : make_float4(1.f, 1.f, 1.f, 1.f);
+    }
+    bool colok[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) colok[j] = n0 + wn0 + 16 * j + 4 * fg < d.N;
+    int64_t rb[TM];
+    bool ok[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+        const uint32_t m = (uint32_t)m0 + wm0 + 16 * i + fr;
+        ok[i] = m < M;
+        rb[i] = (int64_t)(ok[i] ? m : M - 1) * d.ldo + d.col_off;
+    }
+    const float* res = (const float*)d.res;
+    float* C = (float*)d.C;
+    float* sink = reinterpret_cast<float*>(g_epi_sink + lane);
+    float4 rc[TN], rn[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) rc[j] = *reinterpret_cast<const float4*>(res + rb[0] + ncol[j]);
+    float p1[TM], p2[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+        if (i + 1 < TM) {
+#pragma unroll
+            for (int j = 0; j < TN; ++j) rn[j] = *reinterpret_cast<const float4*>(res + rb[i + 1] + ncol[j]);
+        }
+        float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const float4 o = make_float4(rc[j].x + sc[j].x * (acc[i][j][0] + bj[j].x), rc[j].y + sc[j].y * (acc[i][j][1] + bj[j].y),
+                                         rc[j].z + sc[j].z * (acc[i][j][2] + bj[j].z), rc[j].w + sc[j].w * (acc[i][j][3] + bj[j].w));
+            const bool st = ok[i] && colok[j];
+            if (f_stats && st) {
+                s1 += (o.x + o.y) + (o.z + o.w);
+                s2 += (o.x * o.x + o.y * o.y) + (o.z * o.z + o.w * o.w);
+            }
+            *reinterpret_cast<float4*>(st ? C + rb[i] + ncol[j] : sink) = o;
+        }
+        p1[i] = s1;
+        p2[i] = s2;
+        if (i + 1 < TM) {
+#pragma unroll
+            for (int j = 0; j < TN; ++j) rc[j] = rn[j];
+        }
+    }
+    if constexpr (f_stats) {
+        if (one_group) {
+            float q1 = 0.f, q2 = 0.f;
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                q1 += p1[i];
+                q2 += p2[i];
+            }
+            const double t1 = wave_sum_d((double)q1), t2 = wave_sum_d((double)q2);
+            if (lane == 0) {
+                atomicAdd(&st_lds[0], t1);
+                atomicAdd(&st_lds[1], t2);
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                float a = p1[i], b = p2[i];
+                a += __shfl_xor(a, 16, 64);
+                b += __shfl_xor(b, 16, 64);
+                a += __shfl_xor(a, 32, 64);
+                b += __shfl_xor(b, 32, 64);
+                const uint32_t m = (uint32_t)m0 + wm0 + 16 * i + fr;
+                if (fg == 0 && ok[i]) {
+                    const uint32_t gi = m / HW - g0;
+                    if (gi < (uint32_t)EPI_MAXG) {
+                        atomicAdd(&st_lds[2 * gi], (double)a);
+                        atomicAdd(&st_lds[2 * gi + 1], (double)b);
+                    } else {
+                        atomicAdd(&d.stats[2 * (g0 + gi)], (double)a);
+                        atomicAdd(&d.stats[2 * (g0 + gi) + 1], (double)b);
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x < EPI_MAXG) {
+            const double a = st_lds[2 * threadIdx.x], q = st_lds[2 * threadIdx.x + 1];
+            st_lds[2 * threadIdx.x] = 0.0;
+            st_lds[2 * threadIdx.x + 1] = 0.0;
+            if (a != 0.0 || q != 0.0) {
+                atomicAdd(&d.stats[2 * (g0 + threadIdx.x)], a);
+                atomicAdd(&d.stats[2 * (g0 + threadIdx.x) + 1], q);
+            }
+        }
+    }
+}
+
 }  // namespace athd
