@@ -239,6 +239,9 @@ __global__ __launch_bounds__(256) void attn_kernel(const AttnDesc d) {
 typedef short v4i16 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
 
+// defer-max threshold of the bf16 kernel's online softmax (log2 units): P <= 2^8 before the final 1/l
+constexpr float ATTN_RESCALE = 8.0f;
+
 __global__ __launch_bounds__(256, 3) void attn_bf16_kernel(const AttnDesc d) {
     constexpr int LDK = 72;                        // bf16 per LDS row (64 + 8 pad)
     __shared__ __attribute__((aligned(16))) bf16_t Ks[2][64 * LDK];
@@ -323,51 +326,74 @@ __global__ __launch_bounds__(256, 3) void attn_bf16_kernel(const AttnDesc d) {
                     s[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, qb[nt][c], s[mt][nt], 0, 0, 0);
             }
         // ---- online softmax (per query column) ----
+        // The running max moves only when the tile max exceeds it by more than ATTN_RESCALE (log2 units; T13
+        // "defer-max"): P = 2^(s - m) then stays <= 2^ATTN_RESCALE (exact in bf16's range) and the rescale of O and
+        // l - an exp and 32 multiplies per lane - runs only on the tiles where some query's max really jumps.
+        // Scores are scaled inside the exponent's FMA: the max is taken on the raw scores (scale > 0).
         float p[4][2][4];
         const bool tail = k0 + 64 > d.Nk;
+        if (tail) {
+#pragma unroll
+            for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    if (k0 + 16 * mt + 4 * g + r >= d.Nk) {
+                        s[mt][0][r] = -INFINITY;
+                        s[mt][1][r] = -INFINITY;
+                    }
+        }
+        float mnew[2];
+        bool jump = false;
 #pragma unroll
         for (int nt = 0; nt < 2; ++nt) {
             float mx = -INFINITY;
 #pragma unroll
             for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    float v = s[mt][nt][r] * sl2;
-                    if (tail && k0 + 16 * mt + 4 * g + r >= d.Nk) v = -INFINITY;
-                    p[mt][nt][r] = v;
-                    mx = fmaxf(mx, v);
-                }
+                mx = fmaxf(fmaxf(fmaxf(mx, s[mt][nt][0]), fmaxf(s[mt][nt][1], s[mt][nt][2])), s[mt][nt][3]);
             mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
             mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-            const float mnew = fmaxf(mrun[nt], mx);
-            const float alpha = __builtin_amdgcn_exp2f(mrun[nt] - mnew);
-            mrun[nt] = mnew;
+            mx *= sl2;
+            const bool up = mx > mrun[nt] + ATTN_RESCALE;
+            mnew[nt] = up ? mx : mrun[nt];
+            jump |= up;
+        }
+        if (__any(jump)) {
+#pragma unroll
+            for (int nt = 0; nt < 2; ++nt) {
+                const float alpha = __builtin_amdgcn_exp2f(mrun[nt] - mnew[nt]);
+                mrun[nt] = mnew[nt];
+                lrun[nt] *= alpha;
+#pragma unroll
+                for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) o[dt][nt][r] *= alpha;
+            }
+        }
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) {
+            const float nm = -mrun[nt];
             float ls = 0.f;
 #pragma unroll
             for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    const float e = __builtin_amdgcn_exp2f(p[mt][nt][r] - mnew);
+                    const float e = __builtin_amdgcn_exp2f(fmaf(s[mt][nt][r], sl2, nm));
                     p[mt][nt][r] = e;
                     ls += e;
                 }
-            lrun[nt] = lrun[nt] * alpha + ls;
-#pragma unroll
-            for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) o[dt][nt][r] *= alpha;
+            lrun[nt] += ls;
         }
         // ---- O^T += V^T P^T ----
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
             bf16v8 pb[2];
 #pragma unroll
-            for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    pb[nt][j] = (__bf16)p[2 * kk][nt][j];
-                    pb[nt][4 + j] = (__bf16)p[2 * kk + 1][nt][j];
-                }
+            for (int nt = 0; nt < 2; ++nt) {
+                const uint32_t w[4] = {pack2bf(p[2 * kk][nt][0], p[2 * kk][nt][1]), pack2bf(p[2 * kk][nt][2], p[2 * kk][nt][3]),
+                                       pack2bf(p[2 * kk + 1][nt][0], p[2 * kk + 1][nt][1]),
+                                       pack2bf(p[2 * kk + 1][nt][2], p[2 * kk + 1][nt][3])};
+                pb[nt] = __builtin_bit_cast(bf16v8, w);
+            }
             // tr-read addresses: lane 4q+p of group g -> row (key) k0' + q, columns d0 + 4p
             const int qrow = c16 >> 2, pcol = c16 & 3;
 #pragma unroll
