@@ -131,21 +131,24 @@ struct athd_ctx {
         return p;
     }
     float* up_key(const std::string& k) { return up_f32(W(k).v); }
-    // Pack a [N][K] fp32 host matrix (row-major, k contiguous) into the compute dtype, Kp = roundup(K, 32).
+    // Pack a [N][K] fp32 host matrix (row-major, k contiguous) into the compute dtype, Kp = roundup(K, 64).  The
+    // allocation holds roundup(N, 256) rows, the extra ones zero: a 256-column GEMM tile (gemm4.hip) may read
+    // whole tiles of rows past N.
     GemmW up_gemm(const std::vector<float>& w, int N, int K, const std::vector<float>& bias) {
         GemmW g;
         g.N = N;
         g.K = K;
         g.Kp = (int)rup(K, 64);
+        const int Nalloc = (int)rup(N, 256);
         if (mode == 1) {
-            std::vector<uint16_t> p((size_t)N * g.Kp, 0);
+            std::vector<uint16_t> p((size_t)Nalloc * g.Kp, 0);
             for (int n = 0; n < N; ++n)
                 for (int k = 0; k < K; ++k) p[(size_t)n * g.Kp + k] = host_f2bf(w[(size_t)n * K + k]);
             void* d = dalloc<uint16_t>(p.size());
             hipMemcpy(d, p.data(), p.size() * 2, hipMemcpyHostToDevice);
             g.w = d;
         } else {
-            std::vector<float> p((size_t)N * g.Kp, 0.f);
+            std::vector<float> p((size_t)Nalloc * g.Kp, 0.f);
             for (int n = 0; n < N; ++n)
                 for (int k = 0; k < K; ++k) p[(size_t)n * g.Kp + k] = w[(size_t)n * K + k];
             g.w = up_f32(p);

@@ -285,7 +285,8 @@ int gemm4_launch(const GemmDesc& d, hipStream_t s);
 int gemm_launch(const GemmDesc& d, int mode, hipStream_t s) {
     if (d.Kp % BK != 0 || d.Kp < d.K || d.C_in <= 0 || d.N <= 0) return -2;
     if (d.act == ACT_GLU && (d.N % 32 != 0)) return -2;
-    // bf16 activations, N a multiple of 256: 256x256 tile, half-tile staged pipeline (gemm4.hip)
+    // bf16 activations, N a multiple of 256: 256x256 tile, half-tile staged pipeline (gemm4.hip).  (Measured on
+    // N = 192 / 384: slower than gemm3's 256x192 tiles, which waste no columns.)
     if (mode == 1 && gemm4_supported(d) && d.N % 256 == 0) return gemm4_launch(d, s);
     // other N >= 192: 256x192 tile, 8 waves (gemm3.hip)
     if (mode == 1 && gemm3_supported(d) && d.N >= 192) return gemm3_launch(d, s, 3);

@@ -100,7 +100,7 @@ __global__ __launch_bounds__(512) void gemm4_kernel(const GemmDesc d) {
     const char* zero = reinterpret_cast<const char*>(g_zero_page4);
 
     // this lane's slot rows: sr = 8 (wave + 8 q) + lrow, q = 0, 1 (both slot halves h use the same sr).
-    // 32-bit element offsets (gemm4_supported: A < 2^31 elements, N % 256 == 0 so every B row exists); a row past M
+    // 32-bit element offsets (gemm4_supported: A < 2^31 elements; the weights hold whole 256-row tiles); a row past M
     // gets a_h0 = INT_MIN / 2, which fails the row >= 0 test for every tap.
     uint32_t a_base[2][2];
     int a_h0[2][2];
@@ -264,8 +264,9 @@ __global__ __launch_bounds__(512) void gemm4_kernel(const GemmDesc d) {
 
 bool gemm4_supported(const GemmDesc& d) {
     const int64_t a_elems = (d.a_bs >= 0 ? d.a_bs : (int64_t)d.H_in * d.W * d.a_ld) * d.nb;
+    // N % 64 == 0: the packed weights hold roundup(N, 256) rows (ctx.h up_gemm), the epilogue skips columns >= N
     return d.a_bf16 && !d.a_norm && d.C_in % 8 == 0 && d.a_ld % 8 == 0 && d.a_cs == 1 && d.Kp % 64 == 0 &&
-           d.N % 256 == 0 && (int64_t)d.N * d.Kp * 2 < (1LL << 31) && a_elems < (1LL << 31) &&
+           d.N % 64 == 0 && (int64_t)(d.N + 255) * d.Kp * 2 < (1LL << 31) && a_elems < (1LL << 31) &&
            d.col_split % 4 == 0 && (d.act != ACT_GLU || d.N % 32 == 0);
 }
 

@@ -20,6 +20,7 @@ int kb_gemm(int variant, const void* A, int a_bf16, const void* W, const float* 
     d.A = A; d.a_bf16 = a_bf16; d.nb = 1; d.H_in = M; d.W = 1; d.C_in = K; d.a_ld = K; d.H_out = M;
     d.Wp = W; d.N = N; d.K = K; d.Kp = Kp; d.bias = bias; d.C = C; d.c_bf16 = c_bf16; d.H_out_total = M; d.ldo = N;
     d.act = act;
+    if (variant >= 40 && N % 256 != 0) return -1;   // gemm4 reads whole 256-row weight tiles; W here has N rows
     if (variant == 40) return gemm4_launch(d, (hipStream_t)stream);
     if (variant == 41) { d.store = 0; return gemm4_launch(d, (hipStream_t)stream); }   // timing probe: no C stores
     if (variant == 42) { d.bias = nullptr; return gemm4_launch(d, (hipStream_t)stream); }   // timing probe: no bias
