@@ -393,16 +393,20 @@ int athd_finalize(athd_ctx* c) {
     // ---- FFT twiddles and the periodic Hann window (torch.hann_window(4096)) ----
     {
         std::vector<float2> tw(4096);
+        std::vector<double2> tw64(4096);
         std::vector<float> win(4096), win2(4096);
         for (int k = 0; k < 4096; ++k) {
             const double a = -2.0 * M_PI * (double)k / 4096.0;
             tw[k] = make_float2((float)cos(a), (float)sin(a));
+            tw64[k] = make_double2(cos(a), sin(a));
             const float w = (float)(0.5 - 0.5 * cos(2.0 * M_PI * (double)k / 4096.0));
             win[k] = w;
             win2[k] = w * w;
         }
         c->tw = c->dalloc<float2>(4096);
         hipMemcpy(c->tw, tw.data(), 4096 * sizeof(float2), hipMemcpyHostToDevice);
+        c->tw64 = c->dalloc<double2>(4096);
+        hipMemcpy(c->tw64, tw64.data(), 4096 * sizeof(double2), hipMemcpyHostToDevice);
         c->win = c->up_f32(win);
         c->win2 = c->up_f32(win2);
     }

@@ -110,6 +110,7 @@ struct athd_ctx {
     float* flast = nullptr;          // folded last freq level + freq_out (dec_last.hip)
     float* tlast = nullptr;          // folded last time level + time_out
     float2* tw = nullptr;
+    double2* tw64 = nullptr;       // FFT twiddles in double (f32 parity mode, spectral.hip)
     float* win = nullptr;
     float* win2 = nullptr;
 

@@ -249,7 +249,7 @@ void encode(Run& r, const Dims& d, const Bufs& b, const float* wav) {
         pp.ext_left = epl;
         pp.Lx = d.T + epl + epr;
     }
-    stft_launch(wav, (int)B, d.T, pp, (int)Ts, c->tw, c->win, b.spec, b.specT, r.s);
+    stft_launch(wav, (int)B, d.T, pp, (int)Ts, c->tw, r.actbf ? nullptr : c->tw64, c->win, b.spec, b.specT, r.s);
     wav_interleave_launch(wav, (int)B, d.T, b.wavT, r.s);
     double* st_spec = r.stats(B);
     double* st_wav = r.stats(B);
@@ -549,7 +549,7 @@ void decode_chunk(Run& r, const Dims& d, const Bufs& b, int64_t s0, int64_t Bc, 
         }
     }
     // ---- mask + iSTFT frames (ATHTDemucs_v2.py:297-310) ----
-    istft_frames_launch(b.FO, NI, (int)Ts, P, b.specT + s0 * 2048 * Ts * 4, c->tw, c->win, b.frames, r.s);
+    istft_frames_launch(b.FO, NI, (int)Ts, P, b.specT + s0 * 2048 * Ts * 4, c->tw, r.actbf ? nullptr : c->tw64, c->win, b.frames, r.s);
 
     // ---- time decoder (ATHTDemucs_v2.py:125-139, 313-321) ----
     float* xt2 = nullptr;                            // time_out(time decoder) [NI][T][2]

@@ -15,11 +15,12 @@ struct PadPlan {
 
 // spectral.hip
 // spec [b][f][t][4] (encoder layout) and specT [b][t][f][4] (frame-major, for the iSTFT)
+// tw64 != nullptr (f32 parity mode): the FFT runs in double (spectral.hip)
 void stft_launch(const float* wav, int nb, int64_t T, const PadPlan& pp, int Tspec, const float2* tw,
-                 const float* win, float* spec, float* specT, hipStream_t s);
+                 const double2* tw64, const float* win, float* spec, float* specT, hipStream_t s);
 // fo: FO^T [item][t][row][2] (dec_merge_proj_kernel output); specT as above
 void istft_frames_launch(const float* fo, int NI, int Tspec, int P, const float* specT, const float2* tw,
-                         const float* win, float* frames, hipStream_t s);
+                         const double2* tw64, const float* win, float* frames, hipStream_t s);
 // out[item][c][n] = OLA(frames)/env + xt2[item][n][c] * stdt[b] + meant[b]   (xt2: tdec_last_launch output)
 void combine_launch(const float* frames, int NI, int Tspec, int64_t T, const float* win2, const float* xt2,
                     const float* tnorm, int P, float* out, hipStream_t s);

@@ -1,8 +1,8 @@
 // Spectral front/back end for gfx950.
 //
 // STFT: one workgroup per (sample, kept frame).  Both audio channels go through ONE 4096-point complex FFT
-// (z = x_L + i x_R), radix-4 Stockham (6 stages) ping-ponging between two 32 KiB LDS buffers, twiddles from
-// a 4096-entry table; the two real spectra are split as X_L = (Z_k + conj Z_-k)/2, X_R = (Z_k - conj Z_-k)/2i.
+// (z = x_L + i x_R), three radix-16 Stockham passes in registers with two padded-LDS exchanges, twiddles
+// from a 4096-entry table; the two real spectra are split as X_L = (Z_k + conj Z_-k)/2, X_R = (Z_k - conj Z_-k)/2i.
 // The reflect padding of HTDemucs._spec (demucs pad1d, incl. its zero-extension for inputs shorter than the
 // pad) is folded into the frame gather; torch.stft's own centre padding is never reached by the kept frames
 // 2..le+1, so it needs no code.  Output is the CaC tensor channels-last: spec[b][f][t][4] = {Re L, Im L, Re R,
@@ -23,42 +23,116 @@ namespace athd {
 constexpr int NFFT = 4096;
 constexpr int HOP = 1024;
 
-struct cpx { float x, y; };
-ATHD_DEV cpx cadd(cpx a, cpx b) { return {a.x + b.x, a.y + b.y}; }
-ATHD_DEV cpx csub(cpx a, cpx b) { return {a.x - b.x, a.y - b.y}; }
-ATHD_DEV cpx cmul(cpx a, cpx b) { return {a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x}; }
+template <typename R>
+struct cx { R x, y; };
+using cpx = cx<float>;
+template <typename R> ATHD_DEV cx<R> cadd(cx<R> a, cx<R> b) { return {a.x + b.x, a.y + b.y}; }
+template <typename R> ATHD_DEV cx<R> csub(cx<R> a, cx<R> b) { return {a.x - b.x, a.y - b.y}; }
+template <typename R> ATHD_DEV cx<R> cmul(cx<R> a, cx<R> b) { return {a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x}; }
 
-// In-LDS radix-4 Stockham FFT (forward, e^{-2 pi i}) of 4096 points with 256 threads.  Result in the buffer
-// returned (a or b).
-ATHD_DEV cpx* fft4096(cpx* a, cpx* b, const float2* __restrict__ tw) {
-    const int tid = threadIdx.x;
-    for (int L = 1; L < NFFT; L *= 4) {
-        const int tstride = NFFT / (4 * L);
+// 4096-point forward FFT (e^{-2 pi i}) with 256 threads as three radix-16 Stockham passes (4096 = 16^3).  Each
+// thread keeps 16 points in registers; a pass is twiddle -> 16-point DFT in registers, and only the two
+// exchanges between passes go through LDS (vs six LDS round trips for radix-4).  Pass Ns (1, 16, 256): thread j
+// holds a[j + 256 r], multiplies by tw[(j mod Ns) r 4096/(16 Ns)] and writes its DFT output q to
+// (j / Ns) 16 Ns + (j mod Ns) + q Ns.  After the last pass thread j holds X[j + 256 q] with no store needed.
+// LDS slots are padded (one per 16) so that the stride-16 stores of the first exchange are conflict-free.
+//
+// R = float in throughput (bf16) mode.  R = double in the f32 parity mode: the spectrum is then the correctly
+// rounded fp32 value.  That matters because the reference's phase term z / (Re z_L + 1e-8)
+// (ATHTDemucs_v2.py:308) is singular: at a bin with Re z_L within a few 1e-8 of -1e-8 the output depends on the
+// last bits of the FFT, and an fp32 FFT whose rounding differs from torch's (another summation order) can move
+// the whole-output SDR by tens of dB on the reference fixtures.  A correctly rounded spectrum stays within
+// ~90 dB of the reference output on all of them.
+constexpr int FPAD = NFFT + NFFT / 16;
+ATHD_DEV int pidx(int i) { return i + (i >> 4); }
+
+// in-place forward radix-4: (x0, x1, x2, x3) <- DFT4
+template <typename R>
+ATHD_DEV void r4(cx<R>& x0, cx<R>& x1, cx<R>& x2, cx<R>& x3) {
+    const cx<R> s02 = cadd(x0, x2), d02 = csub(x0, x2), s13 = cadd(x1, x3), d13 = csub(x1, x3);
+    const cx<R> md13 = {d13.y, -d13.x};                  // -i * d13
+    x0 = cadd(s02, s13);
+    x1 = cadd(d02, md13);
+    x2 = csub(s02, s13);
+    x3 = csub(d02, md13);
+}
+
+// 16-point DFT as 4 x 4: v[r] (r = 4 r1 + r0) in; output bin q = k0 + 4 k1 is left in v[4 k0 + k1] (see vq)
+template <typename R>
+ATHD_DEV void dft16(cx<R> (&v)[16]) {
+    constexpr R C1 = (R)0.92387953251128675613, S1 = (R)0.38268343236508977173, C2 = (R)0.70710678118654752440;
 #pragma unroll
-        for (int it = 0; it < 4; ++it) {
-            const int j = tid + 256 * it;
-            const int k = j & (L - 1);
-            cpx a0 = a[j], a1 = a[j + NFFT / 4], a2 = a[j + NFFT / 2], a3 = a[j + 3 * NFFT / 4];
-            if (L > 1) {
-                float2 w1 = tw[(k * tstride) & (NFFT - 1)];
-                float2 w2 = tw[(2 * k * tstride) & (NFFT - 1)];
-                float2 w3 = tw[(3 * k * tstride) & (NFFT - 1)];
-                a1 = cmul(a1, {w1.x, w1.y});
-                a2 = cmul(a2, {w2.x, w2.y});
-                a3 = cmul(a3, {w3.x, w3.y});
-            }
-            cpx s02 = cadd(a0, a2), d02 = csub(a0, a2), s13 = cadd(a1, a3), d13 = csub(a1, a3);
-            cpx md13 = {d13.y, -d13.x};                    // -i * d13
-            const int base = (j - k) * 4 + k;
-            b[base] = cadd(s02, s13);
-            b[base + L] = cadd(d02, md13);
-            b[base + 2 * L] = csub(s02, s13);
-            b[base + 3 * L] = csub(d02, md13);
-        }
+    for (int r0 = 0; r0 < 4; ++r0) r4(v[r0], v[4 + r0], v[8 + r0], v[12 + r0]);
+    // a[r0][k0] sits in v[r0 + 4 k0]; multiply by W16^(r0 k0)
+    v[1 + 4] = cmul(v[5], {C1, -S1});      // W^1
+    v[1 + 8] = cmul(v[9], {C2, -C2});      // W^2
+    v[1 + 12] = cmul(v[13], {S1, -C1});    // W^3
+    v[2 + 4] = cmul(v[6], {C2, -C2});      // W^2
+    v[2 + 8] = {v[10].y, -v[10].x};        // W^4 = -i
+    v[2 + 12] = cmul(v[14], {-C2, -C2});   // W^6
+    v[3 + 4] = cmul(v[7], {S1, -C1});      // W^3
+    v[3 + 8] = cmul(v[11], {-C2, -C2});    // W^6
+    v[3 + 12] = cmul(v[15], {-C1, S1});    // W^9
+#pragma unroll
+    for (int k0 = 0; k0 < 4; ++k0) r4(v[4 * k0], v[4 * k0 + 1], v[4 * k0 + 2], v[4 * k0 + 3]);
+}
+// register holding DFT16 output bin q
+ATHD_DEV constexpr int vq(int q) { return 4 * (q & 3) + (q >> 2); }
+
+// One LDS exchange: DFT output q of this thread goes to slot dst(q), then v[r] = slot j + 256 r.  `lds` holds
+// FPAD 8-byte words: complex floats, or the real and then the imaginary parts of complex doubles.  Ends synced.
+template <typename R, typename Dst>
+ATHD_DEV void exchange(cx<R> (&v)[16], void* lds, Dst dst) {
+    const int j = threadIdx.x;
+    if constexpr (sizeof(R) == 4) {
+        cpx* b = reinterpret_cast<cpx*>(lds);
+#pragma unroll
+        for (int q = 0; q < 16; ++q) b[pidx(dst(q))] = v[vq(q)];
         __syncthreads();
-        cpx* t = a; a = b; b = t;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r] = b[pidx(j + 256 * r)];
+        __syncthreads();
+    } else {
+        R* b = reinterpret_cast<R*>(lds);
+        R t[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) b[pidx(dst(q))] = v[vq(q)].x;
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < 16; ++r) t[r] = b[pidx(j + 256 * r)];
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < 16; ++q) b[pidx(dst(q))] = v[vq(q)].y;
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r] = {t[r], b[pidx(j + 256 * r)]};
+        __syncthreads();
     }
-    return a;
+}
+
+// v[r] = x[threadIdx.x + 256 r] on entry; X[threadIdx.x + 256 q] = v[vq(q)] on exit.  tw[m] = e^{-2 pi i m/4096}.
+template <typename R, typename TW>
+ATHD_DEV void fft4096(cx<R> (&v)[16], void* lds, const TW* __restrict__ tw) {
+    const int j = threadIdx.x;
+    dft16(v);                                                       // Ns = 1: no twiddles
+    exchange(v, lds, [j](int q) { return 16 * j + q; });
+    {                                                               // Ns = 16
+        const int k = j & 15;
+#pragma unroll
+        for (int r = 1; r < 16; ++r) {
+            const TW w = tw[k * r * 16];
+            v[r] = cmul(v[r], {w.x, w.y});
+        }
+        dft16(v);
+        const int base = (j >> 4) * 256 + k;
+        exchange(v, lds, [base](int q) { return base + 16 * q; });
+    }
+#pragma unroll
+    for (int r = 1; r < 16; ++r) {                                  // Ns = 256
+        const TW w = tw[j * r];
+        v[r] = cmul(v[r], {w.x, w.y});
+    }
+    dft16(v);
 }
 
 ATHD_DEV float pad_sample(const float* __restrict__ x, int64_t p, const PadPlan& pp) {
@@ -69,26 +143,31 @@ ATHD_DEV float pad_sample(const float* __restrict__ x, int64_t p, const PadPlan&
     return (i >= 0 && i < pp.L) ? x[i] : 0.f;
 }
 
+template <typename R, typename TW>
 __global__ __launch_bounds__(256) void stft_kernel(const float* __restrict__ wav, int64_t T, PadPlan pp, int Tspec,
-                                                   const float2* __restrict__ tw, const float* __restrict__ win,
+                                                   const TW* __restrict__ tw, const float* __restrict__ win,
                                                    float* __restrict__ spec, float* __restrict__ specT) {
-    __shared__ cpx bufA[NFFT];
-    __shared__ cpx bufB[NFFT];
+    __shared__ cpx buf[FPAD];
     const int t = blockIdx.x;
     const int64_t b = blockIdx.y;
     const float* xl = wav + b * 2 * T;
     const float* xr = xl + T;
     const int64_t p0 = (int64_t)t * HOP;     // kept frame t = stft frame t+2, starts at 1024 t in the pad1d'ed signal
-    for (int n = threadIdx.x; n < NFFT; n += 256) {
+    cx<R> v[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int n = threadIdx.x + 256 * r;
         const float w = win[n];
-        bufA[n] = {pad_sample(xl, p0 + n, pp) * w, pad_sample(xr, p0 + n, pp) * w};
+        v[r] = {(R)(pad_sample(xl, p0 + n, pp) * w), (R)(pad_sample(xr, p0 + n, pp) * w)};
     }
+    fft4096(v, buf, tw);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) buf[pidx(threadIdx.x + 256 * q)] = {(float)v[vq(q)].x, (float)v[vq(q)].y};
     __syncthreads();
-    cpx* Z = fft4096(bufA, bufB, tw);
     float* out = spec + ((b * 2048) * Tspec + t) * 4;
     float* outT = specT + (b * Tspec + t) * 2048LL * 4;      // frame-major copy for the iSTFT (contiguous)
     for (int k = threadIdx.x; k < 2048; k += 256) {
-        cpx zk = Z[k], zn = Z[(NFFT - k) & (NFFT - 1)];
+        cpx zk = buf[pidx(k)], zn = buf[pidx((NFFT - k) & (NFFT - 1))];
         // X_L = (zk + conj zn)/2, X_R = (zk - conj zn)/(2i); scaled by 1/64 (normalized=True)
         const float s = 0.5f / 64.f;
         float4 v;
@@ -102,20 +181,25 @@ __global__ __launch_bounds__(256) void stft_kernel(const float* __restrict__ wav
 }
 
 void stft_launch(const float* wav, int nb, int64_t T, const PadPlan& pp, int Tspec, const float2* tw,
-                 const float* win, float* spec, float* specT, hipStream_t s) {
+                 const double2* tw64, const float* win, float* spec, float* specT, hipStream_t s) {
     KScope ks(s);
     if (ks.on()) ks.begin("stft_kernel", 0.0, (double)nb * 2 * T * 4 + 2.0 * nb * 2048 * Tspec * 4 * 4);
-    hipLaunchKernelGGL(stft_kernel, dim3(Tspec, nb), dim3(256), 0, s, wav, T, pp, Tspec, tw, win, spec, specT);
+    if (tw64)
+        hipLaunchKernelGGL((stft_kernel<double, double2>), dim3(Tspec, nb), dim3(256), 0, s, wav, T, pp, Tspec, tw64, win,
+                           spec, specT);
+    else
+        hipLaunchKernelGGL((stft_kernel<float, float2>), dim3(Tspec, nb), dim3(256), 0, s, wav, T, pp, Tspec, tw, win,
+                           spec, specT);
 }
 
 // ---------------------------------------------------------------------------------------------------------
+template <typename R, typename TW>
 __global__ __launch_bounds__(256) void istft_frames_kernel(const float* __restrict__ fo, int Tspec, int P,
                                                            const float* __restrict__ specT,
-                                                           const float2* __restrict__ tw,
+                                                           const TW* __restrict__ tw,
                                                            const float* __restrict__ win,
                                                            float* __restrict__ frames) {
-    __shared__ cpx bufA[NFFT];
-    __shared__ cpx bufB[NFFT];
+    __shared__ cpx buf[FPAD];
     const int t = blockIdx.x;
     const int64_t item = blockIdx.y;
     const int64_t b = item / P;
@@ -138,30 +222,44 @@ __global__ __launch_bounds__(256) void istft_frames_kernel(const float* __restri
         // Z = X0 + i X1 (k), and its Hermitian mirror at N-k: conj(X0) + i conj(X1); conj() for the inverse
         // (ifft(Z) = conj(fft(conj(Z))))
         cpx Zk = {X0.x - X1.y, X0.y + X1.x};
-        bufA[k] = {Zk.x, -Zk.y};
+        buf[pidx(k)] = {Zk.x, -Zk.y};
         if (k > 0) {
             cpx Zm = {X0.x + X1.y, -X0.y + X1.x};
-            bufA[NFFT - k] = {Zm.x, -Zm.y};
+            buf[pidx(NFFT - k)] = {Zm.x, -Zm.y};
         }
     }
-    if (threadIdx.x == 0) bufA[2048] = {0.f, 0.f};    // Nyquist bin padded with zero (HTDemucs._ispec)
+    if (threadIdx.x == 0) buf[pidx(2048)] = {0.f, 0.f};    // Nyquist bin padded with zero (HTDemucs._ispec)
     __syncthreads();
-    cpx* Z = fft4096(bufA, bufB, tw);
+    cx<R> v[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const cpx z = buf[pidx(threadIdx.x + 256 * r)];
+        v[r] = {(R)z.x, (R)z.y};
+    }
+    __syncthreads();
+    fft4096(v, buf, tw);
     float* o = frames + (item * Tspec + t) * 2LL * NFFT;
-    for (int n = threadIdx.x; n < NFFT; n += 256) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        const int n = threadIdx.x + 256 * q;
         const float w = win[n] * (1.f / 64.f);
-        o[n] = Z[n].x * w;             // conj(fft(conj Z)) -> real part unchanged
-        o[NFFT + n] = -Z[n].y * w;     // imag part negated
+        o[n] = (float)v[vq(q)].x * w;             // conj(fft(conj Z)) -> real part unchanged
+        o[NFFT + n] = -(float)v[vq(q)].y * w;     // imag part negated
     }
 }
 
 void istft_frames_launch(const float* fo, int NI, int Tspec, int P, const float* spec, const float2* tw,
-                         const float* win, float* frames, hipStream_t s) {
+                         const double2* tw64, const float* win, float* frames, hipStream_t s) {
     KScope ks(s);
     if (ks.on())
         ks.begin("istft_frames_kernel", 0.0, (double)NI * Tspec * Tspec * 2 * 4 + (double)(NI / P) * 2048 * Tspec * 4 * 4 +
                                                  (double)NI * Tspec * 2 * 4096 * 4);
-    hipLaunchKernelGGL(istft_frames_kernel, dim3(Tspec, NI), dim3(256), 0, s, fo, Tspec, P, spec, tw, win, frames);
+    if (tw64)
+        hipLaunchKernelGGL((istft_frames_kernel<double, double2>), dim3(Tspec, NI), dim3(256), 0, s, fo, Tspec, P, spec,
+                           tw64, win, frames);
+    else
+        hipLaunchKernelGGL((istft_frames_kernel<float, float2>), dim3(Tspec, NI), dim3(256), 0, s, fo, Tspec, P, spec, tw,
+                           win, frames);
 }
 
 // out[item][c][n] = OLA(frames)/env + xt2[item][n][c] * stdt[b] + meant[b]   (ATHTDemucs_v2.py:310-324; xt2 is

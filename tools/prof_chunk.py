@@ -8,7 +8,7 @@ d = sys.argv[1]
 which = int(sys.argv[2]) if len(sys.argv) > 2 else 1
 kt = glob.glob(os.path.join(d, "*kernel_trace.csv"))[0]
 tr = sorted(csv.DictReader(open(kt)), key=lambda r: int(r["Start_Timestamp"]))
-idx = [i for i, r in enumerate(tr) if r["Kernel_Name"].startswith("athd::stft_kernel")]
+idx = [i for i, r in enumerate(tr) if "stft_kernel" in r["Kernel_Name"]]
 last = tr[idx[-1]:]
 tv = [i for i, r in enumerate(last) if r["Kernel_Name"].startswith("athd::text_vec")] + [len(last)]
 tot = 0.0

@@ -9,7 +9,7 @@ import sys
 d = sys.argv[1]
 kt = glob.glob(os.path.join(d, "*kernel_trace.csv"))[0]
 tr = sorted(csv.DictReader(open(kt)), key=lambda r: int(r["Start_Timestamp"]))
-idx = [i for i, r in enumerate(tr) if r["Kernel_Name"].startswith("athd::stft_kernel")]
+idx = [i for i, r in enumerate(tr) if "stft_kernel" in r["Kernel_Name"]]
 sec = "encoder"
 tot = collections.OrderedDict()
 for r in tr[idx[-1]:]:

@@ -17,7 +17,7 @@ def main(d, seq=False, top=25):
     if seq:
         kt = glob.glob(os.path.join(d, "*kernel_trace.csv"))[0]
         tr = sorted(csv.DictReader(open(kt)), key=lambda r: int(r["Start_Timestamp"]))
-        idx = [i for i, r in enumerate(tr) if r["Kernel_Name"].startswith("athd::stft_kernel")]
+        idx = [i for i, r in enumerate(tr) if "stft_kernel" in r["Kernel_Name"]]
         for r in tr[idx[-1]:]:
             dur = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
             print(f"{dur:9.1f}us grid={r['Grid_Size_X']:>8}x{r['Grid_Size_Y']:>4}x{r['Grid_Size_Z']:>3} "
