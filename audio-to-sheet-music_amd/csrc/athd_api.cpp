@@ -196,6 +196,14 @@ int athd_finalize(athd_ctx* c) {
             e.cout = C;
             e.conv = c->conv_gemm(p + ".conv.weight", p + ".conv.bias", C, e.cin, 8);
             e.rewrite = c->conv_gemm(p + ".rewrite.weight", p + ".rewrite.bias", 2 * C, C, 1, true);
+            if (br == 1 && i == 0) {                      // tconv0_kernel: [C][2][8] -> [C][tap * 2 + ci]
+                const auto& w0 = c->W(p + ".conv.weight").v;
+                std::vector<float> t0((size_t)C * 16);
+                for (int n = 0; n < C; ++n)
+                    for (int ci = 0; ci < 2; ++ci)
+                        for (int t = 0; t < 8; ++t) t0[(size_t)n * 16 + t * 2 + ci] = w0[((size_t)n * 2 + ci) * 8 + t];
+                e.conv_f32 = c->up_f32(t0);
+            }
             for (int d = 0; d < 2; ++d) {
                 const std::string q = p + ".dconv.layers." + std::to_string(d);
                 e.dc.c3[d] = c->conv_gemm(q + ".0.weight", q + ".0.bias", C / 8, C, 3);

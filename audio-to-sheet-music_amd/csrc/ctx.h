@@ -35,6 +35,7 @@ struct DConvW {
 struct EncW {
     int cin = 0, cout = 0;
     GemmW conv, rewrite;
+    float* conv_f32 = nullptr;     // time level 0 only: [cout][tap * cin + ci] fp32 (tconv0.hip)
     DConvW dc;
 };
 

@@ -46,9 +46,7 @@ Dims make_dims(int64_t B, int64_t T, int P) {
 }
 
 struct Bufs {
-    float* spec;
     float* specT;
-    float* wavT;
     double* stats;
     int64_t nstats;     // number of double pairs
     float *snorm, *tnorm_div, *tnorm_std;
@@ -81,9 +79,7 @@ size_t plan(Arena& ar, const Dims& d, Bufs& b, bool actbf) {
     ns += d.chunks * 6 * d.Bc * d.P;
     b.nstats = ns;
     b.stats = ar.take<double>(2 * ns);
-    b.spec = ar.take<float>(B * 2048 * Ts * 4);
     b.specT = ar.take<float>(B * 2048 * Ts * 4);
-    b.wavT = ar.take<float>(B * d.T * 2);
     b.snorm = ar.take<float>(2 * B);
     b.tnorm_div = ar.take<float>(2 * B);
     b.tnorm_std = ar.take<float>(2 * B);
@@ -249,11 +245,9 @@ void encode(Run& r, const Dims& d, const Bufs& b, const float* wav) {
         pp.ext_left = epl;
         pp.Lx = d.T + epl + epr;
     }
-    stft_launch(wav, (int)B, d.T, pp, (int)Ts, c->tw, r.actbf ? nullptr : c->tw64, c->win, b.spec, b.specT, r.s);
-    wav_interleave_launch(wav, (int)B, d.T, b.wavT, r.s);
     double* st_spec = r.stats(B);
     double* st_wav = r.stats(B);
-    stats_launch(b.spec, (int)B, 2048LL * Ts * 4, st_spec, r.s);
+    stft_launch(wav, (int)B, d.T, pp, (int)Ts, c->tw, r.actbf ? nullptr : c->tw64, c->win, b.specT, st_spec, r.s);
     stats_launch(wav, (int)B, 2 * d.T, st_wav, r.s);
     input_norm_params_launch(st_spec, (int)B, 2048LL * Ts * 4, b.snorm, nullptr, r.s);
     input_norm_params_launch(st_wav, (int)B, 2 * d.T, b.tnorm_div, b.tnorm_std, r.s);
@@ -312,17 +306,18 @@ void encode(Run& r, const Dims& d, const Bufs& b, const float* wav) {
         KStage tstage(kTenc[i]);
         const EncW& et = c->tenc[i];
         const int64_t Li = d.L[i], Lo = d.L[i + 1];
-        GemmDesc gt;
         if (i == 0) {
-            gt.A = b.wavT; gt.a_ld = 2; gt.a_hs = 2; gt.a_bs = 2 * d.T; gt.a_norm = b.tnorm_div;   // (B, T, 2)
+            KSite site("tenc.conv");
+            tconv0_launch(wav, (int)B, d.T, Lo, et.conv_f32, et.conv.bias, b.tnorm_div, b.ybuf, eab, r.s);
         } else {
+            GemmDesc gt;
             gt.A = b.saved_t[i - 1]; gt.a_bf16 = eab; gt.a_ld = et.cin;
+            gt.nb = (int)B; gt.H_in = (int)Li; gt.W = 1; gt.C_in = et.cin;
+            gt.ntaps = 8; gt.in_stride = 4; gt.in_off = -2; gt.dil = 1; gt.H_out = (int)Lo;
+            gt.Wp = et.conv.w; gt.N = C; gt.K = et.conv.K; gt.Kp = et.conv.Kp; gt.bias = et.conv.bias;
+            gt.C = b.ybuf; gt.c_bf16 = eab; gt.H_out_total = (int)Lo; gt.ldo = C; gt.act = ACT_GELU;
+            r.gemm(gt, "tenc.conv");
         }
-        gt.nb = (int)B; gt.H_in = (int)Li; gt.W = 1; gt.C_in = et.cin;
-        gt.ntaps = 8; gt.in_stride = 4; gt.in_off = -2; gt.dil = 1; gt.H_out = (int)Lo;
-        gt.Wp = et.conv.w; gt.N = C; gt.K = et.conv.K; gt.Kp = et.conv.Kp; gt.bias = et.conv.bias;
-        gt.C = b.ybuf; gt.c_bf16 = eab; gt.H_out_total = (int)Lo; gt.ldo = C; gt.act = ACT_GELU;
-        r.gemm(gt, "tenc.conv");
         dconv(r, et, b, b.ybuf, B, Lo);
         GemmDesc grt;
         grt.A = b.ybuf; grt.a_bf16 = eab; grt.nb = (int)B; grt.H_in = (int)Lo; grt.W = 1; grt.C_in = C; grt.a_ld = C; grt.H_out = (int)Lo;
@@ -616,7 +611,6 @@ void dump_all(const Dims& d, const Bufs& b, hipStream_t s) {
     const int64_t B = d.B, Ts = d.Tspec, NI = std::min(d.B, d.Bc) * d.P;
     struct E { std::string name; const void* p; int64_t n; std::string shape; };
     std::vector<E> es = {
-        {"spec", b.spec, B * 2048 * Ts * 4, "B,2048,Ts,4"},
         {"specT", b.specT, B * Ts * 2048 * 4, "B,Ts,2048,4"},
         {"frames", b.frames, NI * Ts * 2 * 4096, "NI,Ts,2,4096"},
         {"snorm", b.snorm, 2 * B, "B,2"},

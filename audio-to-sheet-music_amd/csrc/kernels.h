@@ -13,11 +13,15 @@ struct PadPlan {
     int64_t Lx;         // zero-extended length
 };
 
+// tconv0.hip: time encoder level-0 conv + GELU on the raw waveform, normalisation on load; w = [48][tap*2 + c] f32
+void tconv0_launch(const float* wav, int nb, int64_t T, int64_t Lo, const float* w, const float* bias,
+                   const float* tnorm, void* out, int out_bf16, hipStream_t s);
+
 // spectral.hip
-// spec [b][f][t][4] (encoder layout) and specT [b][t][f][4] (frame-major, for the iSTFT)
+// specT [b][t][f][4] (frame-major: level-0 encoder and iSTFT) + per-batch {sum, sumsq} of it into stats (zeroed)
 // tw64 != nullptr (f32 parity mode): the FFT runs in double (spectral.hip)
 void stft_launch(const float* wav, int nb, int64_t T, const PadPlan& pp, int Tspec, const float2* tw,
-                 const double2* tw64, const float* win, float* spec, float* specT, hipStream_t s);
+                 const double2* tw64, const float* win, float* specT, double* stats, hipStream_t s);
 // fo: FO^T [item][t][row][2] (dec_merge_proj_kernel output); specT as above
 void istft_frames_launch(const float* fo, int NI, int Tspec, int P, const float* specT, const float2* tw,
                          const double2* tw64, const float* win, float* frames, hipStream_t s);

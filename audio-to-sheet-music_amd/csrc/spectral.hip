@@ -5,7 +5,7 @@
 // from a 4096-entry table; the two real spectra are split as X_L = (Z_k + conj Z_-k)/2, X_R = (Z_k - conj Z_-k)/2i.
 // The reflect padding of HTDemucs._spec (demucs pad1d, incl. its zero-extension for inputs shorter than the
 // pad) is folded into the frame gather; torch.stft's own centre padding is never reached by the kept frames
-// 2..le+1, so it needs no code.  Output is the CaC tensor channels-last: spec[b][f][t][4] = {Re L, Im L, Re R,
+// 2..le+1, so it needs no code.  Output is the CaC tensor frame-major: specT[b][t][f][4] = {Re L, Im L, Re R,
 // Im R} with the 1/sqrt(4096) "normalized" scale (exactly 1/64).
 //
 // iSTFT: per (item, frame) the decoder's freq map is resized 2048 rows (PyTorch fp32 bilinear index math),
@@ -146,7 +146,7 @@ ATHD_DEV float pad_sample(const float* __restrict__ x, int64_t p, const PadPlan&
 template <typename R, typename TW>
 __global__ __launch_bounds__(256) void stft_kernel(const float* __restrict__ wav, int64_t T, PadPlan pp, int Tspec,
                                                    const TW* __restrict__ tw, const float* __restrict__ win,
-                                                   float* __restrict__ spec, float* __restrict__ specT) {
+                                                   float* __restrict__ specT, double* __restrict__ st) {
     __shared__ cpx buf[FPAD];
     const int t = blockIdx.x;
     const int64_t b = blockIdx.y;
@@ -164,8 +164,8 @@ __global__ __launch_bounds__(256) void stft_kernel(const float* __restrict__ wav
 #pragma unroll
     for (int q = 0; q < 16; ++q) buf[pidx(threadIdx.x + 256 * q)] = {(float)v[vq(q)].x, (float)v[vq(q)].y};
     __syncthreads();
-    float* out = spec + ((b * 2048) * Tspec + t) * 4;
-    float* outT = specT + (b * Tspec + t) * 2048LL * 4;      // frame-major copy for the iSTFT (contiguous)
+    float* outT = specT + (b * Tspec + t) * 2048LL * 4;
+    double s1 = 0.0, s2 = 0.0;                                // CaC normalisation statistics (A3), fused
     for (int k = threadIdx.x; k < 2048; k += 256) {
         cpx zk = buf[pidx(k)], zn = buf[pidx((NFFT - k) & (NFFT - 1))];
         // X_L = (zk + conj zn)/2, X_R = (zk - conj zn)/(2i); scaled by 1/64 (normalized=True)
@@ -175,21 +175,32 @@ __global__ __launch_bounds__(256) void stft_kernel(const float* __restrict__ wav
         v.y = (zk.y - zn.y) * s;
         v.z = (zk.y + zn.y) * s;
         v.w = -(zk.x - zn.x) * s;
-        *reinterpret_cast<float4*>(out + (int64_t)k * Tspec * 4) = v;
         *reinterpret_cast<float4*>(outT + (int64_t)k * 4) = v;
+        s1 += (double)v.x + (double)v.y + (double)v.z + (double)v.w;
+        s2 += (double)v.x * v.x + (double)v.y * v.y + (double)v.z * v.z + (double)v.w * v.w;
+    }
+    s1 = wave_sum_d(s1);
+    s2 = wave_sum_d(s2);
+    __shared__ double red[2][4];
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) { red[0][w] = s1; red[1][w] = s2; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        atomicAdd(&st[2 * b], red[0][0] + red[0][1] + red[0][2] + red[0][3]);
+        atomicAdd(&st[2 * b + 1], red[1][0] + red[1][1] + red[1][2] + red[1][3]);
     }
 }
 
 void stft_launch(const float* wav, int nb, int64_t T, const PadPlan& pp, int Tspec, const float2* tw,
-                 const double2* tw64, const float* win, float* spec, float* specT, hipStream_t s) {
+                 const double2* tw64, const float* win, float* specT, double* stats, hipStream_t s) {
     KScope ks(s);
-    if (ks.on()) ks.begin("stft_kernel", 0.0, (double)nb * 2 * T * 4 + 2.0 * nb * 2048 * Tspec * 4 * 4);
+    if (ks.on()) ks.begin("stft_kernel", 0.0, (double)nb * 2 * T * 4 + (double)nb * 2048 * Tspec * 4 * 4);
     if (tw64)
         hipLaunchKernelGGL((stft_kernel<double, double2>), dim3(Tspec, nb), dim3(256), 0, s, wav, T, pp, Tspec, tw64, win,
-                           spec, specT);
+                           specT, stats);
     else
         hipLaunchKernelGGL((stft_kernel<float, float2>), dim3(Tspec, nb), dim3(256), 0, s, wav, T, pp, Tspec, tw, win,
-                           spec, specT);
+                           specT, stats);
 }
 
 // ---------------------------------------------------------------------------------------------------------

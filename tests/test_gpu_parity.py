@@ -188,7 +188,6 @@ def test_intermediates_f32(models, oracle_model, text_table, T):
 
     z = cap["z"]
     spec = torch.view_as_real(z).permute(0, 2, 3, 1, 4).reshape(B, 2048, Ts, 4).numpy()
-    cmp("spec", spec, dump["spec"])
     cmp("specT", spec.transpose(0, 2, 1, 3), dump["specT"])
     # iSTFT frames: masked spectrum (ATHTDemucs_v2.py:300-309), Nyquist bin zero (HTDemucs._ispec), inverse real
     # FFT, periodic Hann window, normalized=True (x sqrt(4096) / 4096 per frame)
@@ -204,7 +203,7 @@ def test_intermediates_f32(models, oracle_model, text_table, T):
     if os.environ.get("ATHD_TEST_SAVE"):
         np.savez(os.path.join(REPO, "gpurun_out", f"frames_T{T}.npz"), ref=fr.transpose(0, 3, 1, 2).astype(np.float32),
                  got=dump["frames"].reshape(fr.shape[0], fr.shape[3], 2, 4096), mask=mask.astype(np.float32),
-                 fo=dump["FO"], spec=dump["spec"])
+                 fo=dump["FO"], specT=dump["specT"])
     for i in range(4):
         cmp(f"saved{i}", cap["saved"][i].permute(0, 2, 3, 1).numpy(), dump[f"saved{i}"])
         cmp(f"saved_t{i}", cap["saved_t"][i].permute(0, 2, 1).numpy(), dump[f"saved_t{i}"])
