@@ -6,9 +6,9 @@
 //   c1stat: y = b1 + W1 * GELU(GN(h))   (2C outputs, never stored)  -> GroupNorm statistics of y per group
 //   c1app:  x += scale * GLU(GN(y))     (y recomputed: K = H is tiny)
 // A "group" is the GroupNorm(1) sample: one nb row of L positions (freq rows (b,f) along time, or time samples).
-// Access pattern: c3 stages its x tile (+ dilation halo) in LDS with 16-B coalesced loads; c1app maps a lane to
-// (position, 32-B chunk of x), so x is read and written in consecutive 32-B chunks.  Per-group GroupNorm
-// parameters are finalised once per block into LDS.
+// Access pattern: c3 stages its x tile (+ dilation halo) in LDS with 16-B coalesced loads; the 1x1 passes map a
+// lane to one position.  Every weight is read at a wave-uniform address (scalar loads, SGPR operands of the FMAs:
+// no LDS traffic for weights).  Per-group GroupNorm parameters are finalised once per block into LDS.
 #include <algorithm>
 
 #include "common.h"
@@ -24,6 +24,21 @@ template <> struct XS<float> {
 template <> struct XS<bf16_t> {
     static ATHD_DEV float ld(const bf16_t* p, int64_t i) { return bf2f(p[i]); }
 };
+
+// 16 B of x -> EPC floats
+template <typename TS>
+ATHD_DEV void unpack16(const uint4 q, float* v) {
+    if constexpr (sizeof(TS) == 2) {
+        const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            v[2 * i] = __uint_as_float(w[i] << 16);
+            v[2 * i + 1] = __uint_as_float(w[i] & 0xFFFF0000u);
+        }
+    } else {
+        v[0] = __uint_as_float(q.x); v[1] = __uint_as_float(q.y); v[2] = __uint_as_float(q.z); v[3] = __uint_as_float(q.w);
+    }
+}
 
 // Block-level {sum, sumsq} per group.  Blocks cover <= 256 consecutive positions, so with L >= 256 a block spans
 // at most two groups (g0 and g0 + 1).  Shorter rows fall back to per-thread atomics.
@@ -72,11 +87,9 @@ __global__ __launch_bounds__(256) void dconv_c3_kernel(const TS* __restrict__ x,
     constexpr int EPC = 16 / sizeof(TS);                    // elements per 16-B chunk
     constexpr int CPR = C / EPC;                             // chunks per row
     __shared__ __attribute__((aligned(16))) TS xs[ROWS * C];
-    __shared__ float wl[H * K];
     __shared__ double sh[16];
     const int64_t P = nb * L;
     const int64_t p0 = (int64_t)blockIdx.x * TILE;
-    for (int i = threadIdx.x; i < H * K; i += 256) wl[i] = W[i];
     for (int i = threadIdx.x; i < ROWS * CPR; i += 256) {
         const int r = i / CPR, ch = i - r * CPR;
         const int64_t pp = p0 - HALO + r;
@@ -99,11 +112,14 @@ __global__ __launch_bounds__(256) void dconv_c3_kernel(const TS* __restrict__ x,
             const int64_t tt = t + (tap - 1) * dil;
             if (tt < 0 || tt >= L) continue;                 // zero padding of the group row
             const TS* xr = &xs[(lp + HALO + (tap - 1) * dil) * C];
-#pragma unroll 4
-            for (int c = 0; c < C; ++c) {
-                const float v = XS<TS>::ld(xr, c);
+#pragma unroll 2
+            for (int c0 = 0; c0 < C; c0 += EPC) {
+                float v[EPC];
+                unpack16<TS>(*reinterpret_cast<const uint4*>(xr + c0), v);
 #pragma unroll
-                for (int j = 0; j < HJ; ++j) acc[j] += wl[(sub * HJ + j) * K + tap * C + c] * v;
+                for (int e = 0; e < EPC; ++e)
+#pragma unroll
+                    for (int j = 0; j < HJ; ++j) acc[j] += W[(sub * HJ + j) * K + tap * C + c0 + e] * v[e];
             }
         }
         float* hr = h + p * H + sub * HJ;
@@ -149,15 +165,11 @@ __global__ __launch_bounds__(256) void dconv_c1_stats_kernel(const float* __rest
                                                              const float* __restrict__ W, const float* __restrict__ bias,
                                                              double* __restrict__ st_y) {
     constexpr int H = C / 8, N = 2 * C;
-    __shared__ float wl[N * H];
-    __shared__ float bl[N], gw[H], gb[H], tm[GN_TAB], tr[GN_TAB];
+    __shared__ float tm[GN_TAB], tr[GN_TAB];
     __shared__ double sh[16];
     const int64_t P = nb * L;
     const int64_t p0 = (int64_t)blockIdx.x * 256;
     const int64_t gf = p0 / L, ng = (std::min<int64_t>(p0 + 255, P - 1)) / L - gf + 1;
-    for (int i = threadIdx.x; i < N * H; i += 256) wl[i] = W[i];
-    for (int i = threadIdx.x; i < N; i += 256) bl[i] = bias[i];
-    if (threadIdx.x < H) { gw[threadIdx.x] = g1w[threadIdx.x]; gb[threadIdx.x] = g1b[threadIdx.x]; }
     gn_table(st_h, (double)L * H, gf, ng, tm, tr);
     __syncthreads();
     const int64_t p = p0 + threadIdx.x;
@@ -167,12 +179,12 @@ __global__ __launch_bounds__(256) void dconv_c1_stats_kernel(const float* __rest
         float mean, rstd;
         gn_lookup(st_h, (double)L * H, p / L, gf, ng, tm, tr, mean, rstd);
         float hv[H];
-        load_hg<H, FAST>(h, p, mean, rstd, gw, gb, hv);
+        load_hg<H, FAST>(h, p, mean, rstd, g1w, g1b, hv);
 #pragma unroll 4
         for (int n = 0; n < N; ++n) {
-            float y = bl[n];
+            float y = bias[n];
 #pragma unroll
-            for (int j = 0; j < H; ++j) y += wl[n * H + j] * hv[j];
+            for (int j = 0; j < H; ++j) y += W[n * H + j] * hv[j];
             s1 += y;
             s2 += y * y;
         }
@@ -180,7 +192,8 @@ __global__ __launch_bounds__(256) void dconv_c1_stats_kernel(const float* __rest
     group_stats_add(st_y, p0, p, valid, L, s1, s2, sh);
 }
 
-// ---- c1app: one thread per (position, 32-B chunk of x = CPT channels): x[p][c..c+CPT) += scale * GLU(GN(y))
+// ---- c1app: one thread per position, all C channels: x[p][:] += scale * GLU(GN(y)); every weight / affine read is
+// wave-uniform (scalar loads), x moves in 16-B chunks
 template <int C, typename TS, bool FAST>
 __global__ __launch_bounds__(256) void dconv_c1_apply_kernel(TS* __restrict__ x, const float* __restrict__ h, int64_t nb,
                                                              int64_t L, const double* __restrict__ st_h,
@@ -190,58 +203,48 @@ __global__ __launch_bounds__(256) void dconv_c1_apply_kernel(TS* __restrict__ x,
                                                              const float* __restrict__ g2w, const float* __restrict__ g2b,
                                                              const float* __restrict__ scale) {
     constexpr int H = C / 8, N = 2 * C;
-    constexpr int CPT = 32 / sizeof(TS), CV = C / CPT;
-    __shared__ float wl[N * H];
-    __shared__ float bl[N], gw2[N], gb2[N], scl[C], gw[H], gb[H];
+    constexpr int EPC = 16 / sizeof(TS);
     __shared__ float tm1[GN_TAB], tr1[GN_TAB], tm2[GN_TAB], tr2[GN_TAB];
     const int64_t P = nb * L;
-    const int64_t q0 = (int64_t)blockIdx.x * 256;
-    const int64_t pf = q0 / CV, pl = std::min<int64_t>((q0 + 255) / CV, P - 1);
-    const int64_t gf = pf / L, ng = pl / L - gf + 1;
-    for (int i = threadIdx.x; i < N * H; i += 256) wl[i] = W[i];
-    for (int i = threadIdx.x; i < N; i += 256) { bl[i] = bias[i]; gw2[i] = g2w[i]; gb2[i] = g2b[i]; }
-    for (int i = threadIdx.x; i < C; i += 256) scl[i] = scale[i];
-    if (threadIdx.x < H) { gw[threadIdx.x] = g1w[threadIdx.x]; gb[threadIdx.x] = g1b[threadIdx.x]; }
+    const int64_t p0 = (int64_t)blockIdx.x * 256;
+    const int64_t gf = p0 / L, ng = (std::min<int64_t>(p0 + 255, P - 1)) / L - gf + 1;
     gn_table(st_h, (double)L * H, gf, ng, tm1, tr1);
     gn_table(st_y, (double)L * N, gf, ng, tm2, tr2);
     __syncthreads();
-    const int64_t gi = q0 + threadIdx.x;
-    if (gi >= P * CV) return;
-    const int64_t p = gi / CV;
-    const int c0 = (int)(gi - p * CV) * CPT;
+    const int64_t p = p0 + threadIdx.x;
+    if (p >= P) return;
     const int64_t g = p / L;
     float m1, r1, m2, r2;
     gn_lookup(st_h, (double)L * H, g, gf, ng, tm1, tr1, m1, r1);
     gn_lookup(st_y, (double)L * N, g, gf, ng, tm2, tr2, m2, r2);
     float hv[H];
-    load_hg<H, FAST>(h, p, m1, r1, gw, gb, hv);
-    float o[CPT];
+    load_hg<H, FAST>(h, p, m1, r1, g1w, g1b, hv);
+    TS* xp = x + p * C;
+#pragma unroll 2
+    for (int c0 = 0; c0 < C; c0 += EPC) {
+        uint4 q = *reinterpret_cast<const uint4*>(xp + c0);
+        float e[EPC];
+        unpack16<TS>(q, e);
 #pragma unroll
-    for (int q = 0; q < CPT; ++q) {
-        const int c = c0 + q;
-        float a = bl[c], gt = bl[C + c];
+        for (int k = 0; k < EPC; ++k) {
+            const int c = c0 + k;
+            float a = bias[c], gt = bias[C + c];
 #pragma unroll
-        for (int j = 0; j < H; ++j) {
-            a += wl[c * H + j] * hv[j];
-            gt += wl[(C + c) * H + j] * hv[j];
+            for (int j = 0; j < H; ++j) {
+                a += W[c * H + j] * hv[j];
+                gt += W[(C + c) * H + j] * hv[j];
+            }
+            a = (a - m2) * r2 * g2w[c] + g2b[c];
+            gt = (gt - m2) * r2 * g2w[C + c] + g2b[C + c];
+            const float o = scale[c] * (a * sigmoid<FAST>(gt));
+            e[k] += o;                                // rounded once below (pack2bf: RNE, as f2bf)
         }
-        a = (a - m2) * r2 * gw2[c] + gb2[c];
-        gt = (gt - m2) * r2 * gw2[C + c] + gb2[C + c];
-        o[q] = scl[c] * (a * sigmoid<FAST>(gt));
+        if constexpr (sizeof(TS) == 2)
+            q = make_uint4(pack2bf(e[0], e[1]), pack2bf(e[2], e[3]), pack2bf(e[4], e[5]), pack2bf(e[6], e[7]));
+        else
+            q = make_uint4(__float_as_uint(e[0]), __float_as_uint(e[1]), __float_as_uint(e[2]), __float_as_uint(e[3]));
+        *reinterpret_cast<uint4*>(xp + c0) = q;
     }
-    uint4* xp = reinterpret_cast<uint4*>(x + p * C + c0);
-    uint4 v[2] = {xp[0], xp[1]};
-    if constexpr (sizeof(TS) == 2) {
-        bf16_t* e = reinterpret_cast<bf16_t*>(v);
-#pragma unroll
-        for (int q = 0; q < CPT; ++q) e[q] = f2bf(bf2f(e[q]) + o[q]);
-    } else {
-        float* e = reinterpret_cast<float*>(v);
-#pragma unroll
-        for (int q = 0; q < CPT; ++q) e[q] += o[q];
-    }
-    xp[0] = v[0];
-    xp[1] = v[1];
 }
 
 template <int C, typename TS, bool FAST>
@@ -268,8 +271,7 @@ static void dconv_small_t(void* x, float* h, int64_t nb, int64_t L, int dil, con
     {
         KScope ks(s);
         if (ks.on()) ks.begin(klabel("dconv_c1_apply_kernel<%d,%s>", C, tn), 2.0 * px * 2 * C * H, px * (H * 4 + 2 * C * xb));
-        const int64_t n = P * (C / (32 / (int)sizeof(TS)));
-        hipLaunchKernelGGL((dconv_c1_apply_kernel<C, TS, FAST>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
+        hipLaunchKernelGGL((dconv_c1_apply_kernel<C, TS, FAST>), dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s,
                            (TS*)x, h, nb, L, st_h, g1w, g1b, w1, b1, st_y, g2w, g2b, scale);
     }
 }
