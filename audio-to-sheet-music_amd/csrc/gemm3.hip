@@ -178,7 +178,8 @@ static void launch3(const GemmDesc& d, hipStream_t s) {
 }
 
 // variant: 0 = auto, 1 = 256x128 (8 waves, 3 stages), 2 = 128x128 (4 waves, 3 stages), 3 = 256x192 (8 waves, 2 st),
-// 4 = 128x192 (4 waves, 2 stages: 80 KB LDS, 2 blocks/CU), 5 = 128x192 (4 waves, 3 stages), 6 = 128x96 (4 waves, 3 st)
+// 4 = 128x192 (4 waves, 2 stages: 80 KB LDS, 2 blocks/CU), 5 = 128x192 (4 waves, 3 stages), 6 = 128x96 (4 waves, 3 st),
+// 7 = 192x192 (8 waves, 3 stages: 144 KB LDS)
 int gemm3_launch(const GemmDesc& d, hipStream_t s, int variant) {
     if (variant == 0) variant = (d.N % 192 == 0 && d.N % 128 != 0) ? 3 : 1;
     if (variant == 1) launch3<256, 128, 4, 2, 3>(d, s);
@@ -186,6 +187,7 @@ int gemm3_launch(const GemmDesc& d, hipStream_t s, int variant) {
     else if (variant == 4) launch3<128, 192, 2, 2, 2>(d, s);
     else if (variant == 5) launch3<128, 192, 2, 2, 3>(d, s);
     else if (variant == 6) launch3<128, 96, 2, 2, 3>(d, s);
+    else if (variant == 7) launch3<192, 192, 4, 2, 3>(d, s);
     else launch3<256, 192, 4, 2, 2>(d, s);
     return (int)hipGetLastError();
 }
