@@ -62,6 +62,7 @@ struct Bufs {
     // decode (per chunk)
     float* avec;
     float *U, *Yb, *x_cond, *xt_cond;
+    uint16_t* Ub;       // bf16 copy of U (throughput mode: A operand of text.mlp0)
     void* Hm;
     float *G, *D, *FO, *frames;
     void *S, *Z, *Zs;   // freq level 1 re-associated (fdec_lr.hip): per-tap products of the 32 / 8 source rows
@@ -109,6 +110,7 @@ size_t plan(Arena& ar, const Dims& d, Bufs& b, bool actbf) {
     const int64_t NI = d.Bc * d.P;
     b.avec = ar.take<float>(NI * 384);
     b.U = ar.take<float>(NI * d.Nmax * 384);
+    b.Ub = actbf ? ar.take<uint16_t>(NI * d.Nmax * 384) : nullptr;
     b.Hm = act(NI * d.Nmax * 384);
     b.Yb = ar.take<float>(NI * d.Nmax * 384);
     b.x_cond = ar.take<float>(NI * d.Nf * 384);
@@ -475,8 +477,8 @@ void decode_chunk(Run& r, const Dims& d, const Bufs& b, int64_t s0, int64_t Bc, 
                     c->ta_ivb, c->ta_ow, c->ta_ob, b.avec, r.s);
     auto text_attn = [&](const float* enc, int64_t ntok, float* cond) {
         KStage kst(ntok == d.Nf ? "text_attn.freq" : "text_attn.time");
-        add_rowvec_launch(enc, b.avec, NI, P, ntok, 384, b.U, r.s);
-        GemmDesc g = r.lin(c->mlp0, b.U, 0, NI, ntok, 384);
+        add_rowvec_launch(enc, b.avec, NI, P, ntok, 384, b.U, b.Ub, r.s);
+        GemmDesc g = b.Ub ? r.lin(c->mlp0, b.Ub, 1, NI, ntok, 384) : r.lin(c->mlp0, b.U, 0, NI, ntok, 384);
         g.C = b.Hm; g.c_bf16 = ab; g.act = ACT_GELU;
         r.gemm(g, "text.mlp0");
         GemmDesc g2 = r.lin(c->mlp2, b.Hm, ab, NI, ntok, 384);

@@ -55,7 +55,8 @@ struct LnDesc {
 };
 void layernorm_launch(const LnDesc& d, hipStream_t s);
 // U[item][tok][c] = X[item / P][tok][c] + a[item][c]
-void add_rowvec_launch(const float* X, const float* a, int NI, int P, int64_t ntok, int C, float* U, hipStream_t s);
+void add_rowvec_launch(const float* X, const float* a, int NI, int P, int64_t ntok, int C, float* U, uint16_t* Ub,
+                       hipStream_t s);
 // a[item] = out_proj(in_v(v_proj(text[item])))   (TextCrossAttention closed form, 384 <- 512)
 void text_vec_launch(const float* text, int NI, int P, int text_per_item, const float* wv, const float* bv,
                      const float* wiv, const float* biv, const float* wo, const float* bo, float* a, hipStream_t s);

@@ -192,24 +192,35 @@ void layernorm_launch(const LnDesc& d, hipStream_t s) {
 }
 
 // --------------------------------------------------------------------------------------------- text conditioning
+// U[item] = X[item / P] + a[item] (row vector over C); float4 lanes.  Ub (optional, throughput mode): a bf16 copy of U,
+// the A operand of the text MLP's first GEMM (U itself stays f32 for the residual of the second)
 __global__ __launch_bounds__(256) void add_rowvec_kernel(const float* __restrict__ X, const float* __restrict__ a,
-                                                         int P, int64_t ntok, int C, float* __restrict__ U) {
+                                                         int P, int64_t ntok, int C, float* __restrict__ U,
+                                                         uint16_t* __restrict__ Ub) {
     const int64_t item = blockIdx.y;
     const int64_t b = item / P;
-    const int n = (int)(ntok * C);
-    const float* xp = X + b * n;
-    float* up = U + item * n;
+    const int n4 = (int)(ntok * C / 4);
+    const float4* xp = reinterpret_cast<const float4*>(X + b * ntok * C);
+    float4* up = reinterpret_cast<float4*>(U + item * ntok * C);
+    uint2* ubp = Ub ? reinterpret_cast<uint2*>(Ub + item * ntok * C) : nullptr;
     const float* ap = a + item * C;
-    for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256)
-        up[i] = xp[i] + ap[i % C];
+    const int C4 = C / 4;
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < n4; i += gridDim.x * 256) {
+        const float4 x = xp[i];
+        const float4 av = *reinterpret_cast<const float4*>(ap + 4 * (i % C4));
+        const float4 u = make_float4(x.x + av.x, x.y + av.y, x.z + av.z, x.w + av.w);
+        up[i] = u;
+        if (ubp) ubp[i] = make_uint2(pack2bf(u.x, u.y), pack2bf(u.z, u.w));
+    }
 }
 
-void add_rowvec_launch(const float* X, const float* a, int NI, int P, int64_t ntok, int C, float* U, hipStream_t s) {
-    int blocks = (int)((ntok * C + 255) / 256);
+void add_rowvec_launch(const float* X, const float* a, int NI, int P, int64_t ntok, int C, float* U, uint16_t* Ub,
+                       hipStream_t s) {
+    int blocks = (int)((ntok * C / 4 + 255) / 256);
     if (blocks > 1024) blocks = 1024;
     KScope ks(s);
-    if (ks.on()) ks.begin("add_rowvec_kernel", 0.0, (double)(NI / P + NI) * ntok * C * 4);
-    hipLaunchKernelGGL(add_rowvec_kernel, dim3(blocks, NI), dim3(256), 0, s, X, a, P, ntok, C, U);
+    if (ks.on()) ks.begin("add_rowvec_kernel", 0.0, (double)(NI / P + NI) * ntok * C * 4 + (Ub ? (double)NI * ntok * C * 2 : 0.0));
+    hipLaunchKernelGGL(add_rowvec_kernel, dim3(blocks, NI), dim3(256), 0, s, X, a, P, ntok, C, U, Ub);
 }
 
 __global__ __launch_bounds__(256) void text_vec_kernel(const float* __restrict__ text, int P, int per_item,
