@@ -440,6 +440,7 @@ void conv_t(Run& r, const DecW& w, const void* A, int a_bf16, int nb, int H_in, 
         g.ntaps = 3; g.in_stride = 1; g.in_off = -1; g.dil = 1; g.H_out = H_in;
         g.Wp = w.quad.w; g.N = w.quad.N; g.K = w.quad.K; g.Kp = w.quad.Kp; g.bias = w.quad.bias;
         g.C = out; g.c_bf16 = out_bf16; g.ldo = w.cout; g.stats = st; g.col_split = w.cout; g.hi_row_off = 1;
+        if (w.cin % 32 == 0) g.k_blk = w.cin;       // skip the zero third of K per residue pair (gemm3)
         if (keep < 0) {
             g.H_out_total = 4 * H_in; g.o_stride = 4; g.o_off = 0; g.store_mask = 15;
         } else {                                    // residues 1, 2 -> slots 2u, 2u+1; 0 and 3 feed the statistics

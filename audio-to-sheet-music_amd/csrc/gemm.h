@@ -43,6 +43,8 @@ struct GemmDesc {
     int col_split = 0;        // >0: column group g = n / col_split goes to output row + g * hi_row_off, column
     int hi_row_off = 1;       //     n - g * col_split (ConvTranspose residue classes computed by one GEMM)
     int store_mask = 3;       //     bit g: store column group g
+    int k_blk = 0;            // >0 (with col_split): the four-residue ConvT's zero blocks - column groups 0/1 read
+                              //     only K [0, 2 k_blk), groups 2/3 only K [k_blk, 3 k_blk); k_blk % 32 == 0
     // epilogue
     int act = ACT_NONE;       // ACT_GLU: packed pairs [a(16) | gate(16)] per 32 columns, output N/2 channels
     const void* res = nullptr;        // residual (same layout as C; f32, or bf16 with res_bf16); out = res + rs[n]*v

@@ -115,6 +115,14 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm3_kernel(const GemmDesc d) {
     else wait_vm<0>();
     __builtin_amdgcn_s_barrier();
 
+    // K sub-steps (32 wide) this wave multiplies: the zero K padding beyond K is skipped everywhere, and with k_blk
+    // the residue groups' zero blocks (the wave's BN/WN columns lie in one residue pair; wave-uniform branch)
+    int s_lo = 0, s_hi = (d.K + 31) / 32;
+    if (d.k_blk > 0) {
+        const int ga = (n0 + wn0) / d.col_split, gb = (n0 + wn0 + BN / WN - 1) / d.col_split;
+        if (gb < 2) s_hi = min(s_hi, 2 * d.k_blk / 32);
+        else if (ga >= 2) s_lo = d.k_blk / 32;
+    }
     const int fr = lane & 15, g = lane >> 4;
     int cur = 0;
     for (int kt = 0; kt < nk; ++kt) {
@@ -124,6 +132,7 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm3_kernel(const GemmDesc d) {
         const char* sB = sA + BM * ROWB;
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
+            if (2 * kt + ks < s_lo || 2 * kt + ks >= s_hi) continue;
             const int slot = ((4 * ks + g) ^ (fr & 7)) * 16;
             bf16v8 af[TM], bfr[TN];
 #pragma unroll
@@ -149,7 +158,7 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm3_kernel(const GemmDesc d) {
 }
 
 bool gemm3_supported(const GemmDesc& d) {
-    return d.a_bf16 && !d.a_norm && d.C_in % 8 == 0 && d.a_ld % 8 == 0 && d.a_cs == 1 && d.Kp % 64 == 0 && d.N >= 96 && d.col_split % 4 == 0 &&
+    return (d.k_blk == 0 || (d.k_blk % 32 == 0 && d.col_split > 0)) && d.a_bf16 && !d.a_norm && d.C_in % 8 == 0 && d.a_ld % 8 == 0 && d.a_cs == 1 && d.Kp % 64 == 0 && d.N >= 96 && d.col_split % 4 == 0 &&
            (d.act != ACT_GLU || d.N % 32 == 0);
 }
 

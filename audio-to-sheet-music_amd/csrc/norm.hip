@@ -137,9 +137,18 @@ void gn_apply_launch(float* x, int nb, int64_t N, int C, const double* stats, co
 }
 
 // --------------------------------------------------------------------------------------------- LayerNorm
+// One wave per token row of C = 64 * PER channels.  PER == 8 (C = 512): each lane owns 8 consecutive channels, so a
+// row is read as two float4 per lane (one 2 KB coalesced row per instruction pair) and the bf16 output leaves as one
+// 16-B store per lane; other PER: strided channels lane + 64 j.
+ATHD_DEV void ld8(const float* p, float* o) {
+    const float4 a = reinterpret_cast<const float4*>(p)[0], b = reinterpret_cast<const float4*>(p)[1];
+    o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = a.w; o[4] = b.x; o[5] = b.y; o[6] = b.z; o[7] = b.w;
+}
+
 template <int PER>
 __global__ __launch_bounds__(256) void layernorm_kernel(const LnDesc d) {
     constexpr int C = PER * 64;
+    constexpr bool VEC = PER == 8;
     const int lane = threadIdx.x & 63;
     const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     const int64_t rows = (int64_t)d.nb * d.N;
@@ -147,17 +156,33 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const LnDesc d) {
     const int64_t b = row / d.N;
     const int64_t tok = row % d.N;
     float* xr = d.x + row * C;
+    auto chan = [&](int j) { return VEC ? 8 * lane + j : lane + 64 * j; };
     float v[PER];
+    if (VEC) {
+        ld8(xr + 8 * lane, v);
+    } else {
 #pragma unroll
-    for (int j = 0; j < PER; ++j) v[j] = xr[lane + 64 * j];
+        for (int j = 0; j < PER; ++j) v[j] = xr[chan(j)];
+    }
     if (d.gn_stats) {
         float gm, gr;
         gn_params(d.gn_stats, b, d.N * (int64_t)C, gm, gr);
+        if (VEC) {
+            float gw[8], gb[8];
+            ld8(d.gn_w + 8 * lane, gw);
+            ld8(d.gn_b + 8 * lane, gb);
 #pragma unroll
-        for (int j = 0; j < PER; ++j) {
-            const int c = lane + 64 * j;
-            v[j] = (v[j] - gm) * gr * d.gn_w[c] + d.gn_b[c];
-            xr[c] = v[j];
+            for (int j = 0; j < 8; ++j) v[j] = (v[j] - gm) * gr * gw[j] + gb[j];
+            float4* xo = reinterpret_cast<float4*>(xr + 8 * lane);
+            xo[0] = make_float4(v[0], v[1], v[2], v[3]);
+            xo[1] = make_float4(v[4], v[5], v[6], v[7]);
+        } else {
+#pragma unroll
+            for (int j = 0; j < PER; ++j) {
+                const int c = chan(j);
+                v[j] = (v[j] - gm) * gr * d.gn_w[c] + d.gn_b[c];
+                xr[c] = v[j];
+            }
         }
     }
     float s = 0.f;
@@ -168,13 +193,36 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const LnDesc d) {
 #pragma unroll
     for (int j = 0; j < PER; ++j) { const float t = v[j] - mean; q += t * t; }
     const float rstd = 1.f / sqrtf(wave_sum(q) * (1.f / C) + 1e-5f);
+    float y[PER];
+    if (VEC) {                                   // affine and positional rows as float4 pairs too
+        float wv[8], bv[8], pv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        ld8(d.w + 8 * lane, wv);
+        ld8(d.b + 8 * lane, bv);
+        if (d.pos) ld8(d.pos + tok * C + 8 * lane, pv);
 #pragma unroll
-    for (int j = 0; j < PER; ++j) {
-        const int c = lane + 64 * j;
-        float y = (v[j] - mean) * rstd * d.w[c] + d.b[c];
-        if (d.pos) y += d.pos[tok * C + c];
-        if (d.out_bf16) ((bf16_t*)d.out)[row * C + c] = f2bf(y);
-        else ((float*)d.out)[row * C + c] = y;
+        for (int j = 0; j < 8; ++j) y[j] = (v[j] - mean) * rstd * wv[j] + bv[j] + pv[j];
+    } else {
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            const int c = chan(j);
+            y[j] = (v[j] - mean) * rstd * d.w[c] + d.b[c];
+            if (d.pos) y[j] += d.pos[tok * C + c];
+        }
+    }
+    if (VEC && d.out_bf16) {
+        reinterpret_cast<uint4*>((bf16_t*)d.out + row * C)[lane] =
+            make_uint4(pack2bf(y[0], y[1]), pack2bf(y[2], y[3]), pack2bf(y[4], y[5]), pack2bf(y[6], y[7]));
+    } else if (VEC) {
+        float4* o = reinterpret_cast<float4*>((float*)d.out + row * C);
+        o[2 * lane] = make_float4(y[0], y[1], y[2], y[3]);
+        o[2 * lane + 1] = make_float4(y[4], y[5], y[6], y[7]);
+    } else {
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            const int c = chan(j);
+            if (d.out_bf16) ((bf16_t*)d.out)[row * C + c] = f2bf(y[j]);
+            else ((float*)d.out)[row * C + c] = y[j];
+        }
     }
 }
 

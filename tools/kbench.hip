@@ -43,6 +43,19 @@ int kb_convt(int variant, const void* A, const void* W, const float* bias, void*
     if (variant >= 30) return gemm3_launch(d, (hipStream_t)stream, variant - 30);
     return gemm_launch(d, 1, (hipStream_t)stream);
 }
+// four-residue ConvT GEMM as the decoder runs it for level 2 (kept mode): K = rows u-1 | u | u+1, N = 4*Cout split
+// at Cout, residues 1, 2 stored into slots 2u, 2u+1; kskip = 1 sets k_blk (zero-block skip)
+int kb_convt_quad(int variant, int kskip, const void* A, const void* W, const float* bias, void* C, double* stats,
+                  int nb, int H, int Wd, int Cin, int Cout, int Kp, void* stream) {
+    GemmDesc d;
+    d.A = A; d.a_bf16 = 1; d.nb = nb; d.H_in = H; d.W = Wd; d.C_in = Cin; d.a_ld = Cin;
+    d.ntaps = 3; d.in_stride = 1; d.in_off = -1; d.dil = 1; d.H_out = H;
+    d.Wp = W; d.N = 4 * Cout; d.K = 3 * Cin; d.Kp = Kp; d.bias = bias;
+    d.C = C; d.c_bf16 = 1; d.ldo = Cout; d.stats = stats; d.col_split = Cout; d.hi_row_off = 1;
+    d.H_out_total = 2 * H; d.o_stride = 2; d.o_off = -1; d.store_mask = 6;
+    if (kskip) d.k_blk = Cin;
+    return gemm3_launch(d, (hipStream_t)stream, variant);
+}
 int kb_attn(const void* qkv, int nb, int N, void* out, void* stream) {
     AttnDesc a;
     a.nb = nb; a.Nq = N; a.Nk = N; a.heads = 8; a.scale = 0.125f;

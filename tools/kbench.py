@@ -76,6 +76,40 @@ def convt_case(nb, H, Wd, Cin, Cout, variants):
     print(f"CONVT nb={nb} H={H} W={Wd} Cin={Cin} Cout={Cout}: " + "  ".join(out), flush=True)
 
 
+def quad_case(nb, H, Wd, Cin, Cout, variants):
+    dev = "cuda"
+    A = (torch.randn(nb, H, Wd, Cin, device=dev) * 0.5).to(torch.bfloat16)
+    K = 3 * Cin
+    Kp = (K + 63) // 64 * 64
+    W = torch.zeros(4 * Cout, Kp, device=dev, dtype=torch.bfloat16)
+    W[:, :K] = (torch.randn(4 * Cout, K, device=dev) * 0.05).to(torch.bfloat16)
+    W[:2 * Cout, 2 * Cin:K] = 0          # residues 0/1 never read row u+1, 2/3 never row u-1
+    W[2 * Cout:, :Cin] = 0
+    bias = torch.randn(4 * Cout, device=dev) * 0.1
+    C = torch.zeros(nb, 2 * H, Wd, Cout, device=dev, dtype=torch.bfloat16)
+    st = torch.zeros(2 * nb, device=dev, dtype=torch.float64)
+    s = torch.cuda.current_stream().cuda_stream
+    flops = 2.0 * nb * H * Wd * 4 * Cout * K
+    z = torch.zeros_like(A[:, :1])
+    X = torch.cat([torch.cat([z, A[:, :-1]], 1), A, torch.cat([A[:, 1:], z], 1)], dim=-1).float()
+    ref = X @ W[:, :K].float().t() + bias                                     # (nb, H, Wd, 4 Cout)
+    r1, r2 = ref[..., Cout:2 * Cout], ref[..., 2 * Cout:3 * Cout]
+    rs = torch.stack([ref[..., i * Cout:(i + 1) * Cout] for i in range(4)]).double()
+    out = []
+    for v, ksk in variants:
+        st.zero_()
+        f = lambda: lib.kb_convt_quad(v, ksk, vp(A.data_ptr()), vp(W.data_ptr()), vp(bias.data_ptr()),
+                                      vp(C.data_ptr()), vp(st.data_ptr()), nb, H, Wd, Cin, Cout, Kp, vp(s))
+        st.zero_(); f(); torch.cuda.synchronize()
+        sref = rs.sum(dim=(0, 2, 3, 4)).cpu()
+        serr = ((st.view(nb, 2)[:, 0].cpu() - sref).abs().max() / sref.abs().max()).item()
+        us = timeit(f)
+        err = max((C[:, 0::2].float() - r1).abs().max().item(), (C[:, 1::2].float() - r2).abs().max().item())
+        err /= ref.abs().max().item()
+        out.append(f"v{v}{'s' if ksk else ''}: {us:8.1f}us {flops / us / 1e6:6.1f}TF err={err:.1e} serr={serr:.1e}")
+    print(f"QUAD nb={nb} H={H} W={Wd} Cin={Cin} Cout={Cout}: " + "  ".join(out), flush=True)
+
+
 def attn_case(B, N):
     qkv = (torch.randn(B, N, 1536, device="cuda")).to(torch.bfloat16)
     out = torch.empty(B, N, 512, device="cuda", dtype=torch.bfloat16)
@@ -159,6 +193,11 @@ if __name__ == "__main__":
         sys.exit(0)
     if "tr" in sys.argv[1:]:
         tr_probe()
+    if "quad" in sys.argv[1:]:
+        vs = [(3, 0), (3, 1), (4, 1), (5, 1), (6, 1), (7, 1)]
+        quad_case(64, 259, 259, 96, 48, vs)
+        quad_case(64, 16538, 1, 96, 48, vs)
+        sys.exit(0)
     if "convt" in sys.argv[1:]:
         convt_case(64, 259, 259, 192, 96, (2, 33, 34, 35))
         convt_case(64, 259, 259, 96, 48, (2, 34, 35, 36))
