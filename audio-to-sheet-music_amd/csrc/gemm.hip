@@ -291,7 +291,7 @@ int gemm_launch(const GemmDesc& d, int mode, hipStream_t s) {
     // other N >= 192: 256x192 or 192x192 tile, 8 waves (gemm3.hip)
     // (K >= 384: 192x192 tiles with a 3-stage ring, two K-tiles in flight across each barrier; measured per call
     // site 2-20 % faster there.  Shorter K, e.g. the K=288 four-residue ConvT, keeps 256x192 x 2 stages.)
-    if (mode == 1 && gemm3_supported(d) && d.N >= 192) return gemm3_launch(d, s, d.K >= 384 ? 7 : 3);
+    if (mode == 1 && gemm3_supported(d) && d.N >= 192) return gemm3_launch(d, s, 100 + (d.K >= 384 ? 7 : 3));   // persistent grid
     if (mode == 1 && gemm2_supported(d)) return gemm2_launch(d, s);
     if (mode == 1) launch_mode<1>(d, s);
     else launch_mode<0>(d, s);

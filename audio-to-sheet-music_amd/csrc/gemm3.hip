@@ -45,35 +45,48 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm3_kernel(const GemmDesc d) {
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm0 = (wave / WN) * (BM / WM), wn0 = (wave % WN) * (BN / WN);
     const int64_t M = (int64_t)d.nb * d.H_out * d.W;
-    const int64_t m0 = (int64_t)xcd_remap(blockIdx.x, gridDim.x) * BM;
+    const int ntm = (int)((M + BM - 1) / BM);
     const int n0 = blockIdx.y * BN;
+    if ((int)blockIdx.x >= ntm) return;           // (the launch never sizes gridDim.x above ntm)
     const int64_t a_bs = d.a_bs >= 0 ? d.a_bs : (int64_t)d.H_in * d.W * d.a_ld;
     const int64_t rowpitch = d.a_hs >= 0 ? d.a_hs : (int64_t)d.W * d.a_ld;
     const int lrow = lane >> 3;
     const int chunk = (lane & 7) ^ lrow;
 
+    // Tile loop: block x takes M tiles x, x + gridDim.x, ... (one tile when gridDim.x == ntm; persistent when the
+    // launch sizes the grid to the resident blocks, gridDim.x % 8 == 0 so every tile of a block maps to its XCD's
+    // contiguous range).  The next tile's first STAGES-1 K-tiles are issued BEFORE this tile's epilogue, so their
+    // load latency hides under the epilogue's VALU work and stores.
+    int tile = blockIdx.x;
+    int64_t m0 = 0;
     int64_t a_base[AQ];
     int a_h0[AQ];
     bool a_ok[AQ];
+    int k_cur = 0, tap = 0, ci = 0;
+    auto setup = [&](int t) {
+        m0 = (int64_t)xcd_remap(t, ntm) * BM;
 #pragma unroll
-    for (int q = 0; q < AQ; ++q) {
-        const uint32_t m = (uint32_t)(m0 + 8 * (wave + NW * q) + lrow);
-        a_ok[q] = m < (uint32_t)M;
-        const uint32_t mm = a_ok[q] ? m : 0u;
-        const uint32_t w = mm % (uint32_t)d.W;
-        const uint32_t t = mm / (uint32_t)d.W;
-        const uint32_t ho = t % (uint32_t)d.H_out;
-        const uint32_t b = t / (uint32_t)d.H_out;
-        a_base[q] = (int64_t)b * a_bs + (int64_t)w * d.a_ld;
-        a_h0[q] = (int)ho * d.in_stride + d.in_off;
-    }
+        for (int q = 0; q < AQ; ++q) {
+            const uint32_t m = (uint32_t)(m0 + 8 * (wave + NW * q) + lrow);
+            a_ok[q] = m < (uint32_t)M;
+            const uint32_t mm = a_ok[q] ? m : 0u;
+            const uint32_t w = mm % (uint32_t)d.W;
+            const uint32_t tt = mm / (uint32_t)d.W;
+            const uint32_t ho = tt % (uint32_t)d.H_out;
+            const uint32_t bb = tt / (uint32_t)d.H_out;
+            a_base[q] = (int64_t)bb * a_bs + (int64_t)w * d.a_ld;
+            a_h0[q] = (int)ho * d.in_stride + d.in_off;
+        }
+        k_cur = 8 * chunk;
+        tap = k_cur / d.C_in;
+        ci = k_cur - tap * d.C_in;
+    };
     const char* bptr[BQ];
 #pragma unroll
     for (int q = 0; q < BQ; ++q) {
         const int n = n0 + 8 * (wave + NW * q) + lrow;
         bptr[q] = n < d.N ? (const char*)d.Wp + ((int64_t)n * d.Kp + 8 * chunk) * 2 : nullptr;
     }
-    int k_cur = 8 * chunk, tap = k_cur / d.C_in, ci = k_cur - tap * d.C_in;
     const char* zero = reinterpret_cast<const char*>(g_zero_page3);
     const int nk = d.Kp / 64;
 
@@ -107,14 +120,6 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm3_kernel(const GemmDesc d) {
     float4 bias4[TN];                             // loaded before the main loop (gemm_epi.h: load_bias4)
     load_bias4<TN>(d, n0, wn0, lane, bias4);
 
-    // prologue: STAGES-1 tiles in flight, wait for tile 0
-#pragma unroll
-    for (int s = 0; s < STAGES - 1; ++s)
-        if (s < nk) issue(s, s);
-    if (nk >= STAGES - 1) wait_vm<(STAGES - 2) * LPT>();
-    else wait_vm<0>();
-    __builtin_amdgcn_s_barrier();
-
     // K sub-steps (32 wide) this wave multiplies: the zero K padding beyond K is skipped everywhere, and with k_blk
     // the residue groups' zero blocks (the wave's BN/WN columns lie in one residue pair; wave-uniform branch)
     int s_lo = 0, s_hi = (d.K + 31) / 32;
@@ -124,37 +129,65 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm3_kernel(const GemmDesc d) {
         else if (ga >= 2) s_lo = d.k_blk / 32;
     }
     const int fr = lane & 15, g = lane >> 4;
-    int cur = 0;
-    for (int kt = 0; kt < nk; ++kt) {
-        const int nxt = kt + STAGES - 1;
-        if (nxt < nk) issue(nxt, nxt % STAGES);
-        const char* sA = smem + cur * STAGE;
-        const char* sB = sA + BM * ROWB;
+
+    // prologue of the first tile: STAGES-1 K-tiles in flight, wait for K-tile 0
+    setup(tile);
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-            if (2 * kt + ks < s_lo || 2 * kt + ks >= s_hi) continue;
-            const int slot = ((4 * ks + g) ^ (fr & 7)) * 16;
-            bf16v8 af[TM], bfr[TN];
-#pragma unroll
-            for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const bf16v8*>(sA + (wm0 + 16 * i + fr) * ROWB + slot);
-#pragma unroll
-            for (int j = 0; j < TN; ++j) bfr[j] = *reinterpret_cast<const bf16v8*>(sB + (wn0 + 16 * j + fr) * ROWB + slot);
-#pragma unroll
-            for (int i = 0; i < TM; ++i)
-#pragma unroll
-                for (int j = 0; j < TN; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
-        }
-        // tile kt+1 must have landed before the next iteration; tiles issued after it may stay in flight
-        if (nxt < nk) wait_vm<(STAGES - 2) * LPT>();
-        else wait_vm<0>();
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    for (int s = 0; s < STAGES - 1; ++s)
+        if (s < nk) issue(s, s);
+    if (nk >= STAGES - 1) wait_vm<(STAGES - 2) * LPT>();
+    else wait_vm<0>();
+    for (;;) {
         __builtin_amdgcn_s_barrier();
-        cur = cur + 1 == STAGES ? 0 : cur + 1;
-    }
+        int cur = 0;
+        for (int kt = 0; kt < nk; ++kt) {
+            const int nxt = kt + STAGES - 1;
+            if (nxt < nk) issue(nxt, nxt % STAGES);
+            const char* sA = smem + cur * STAGE;
+            const char* sB = sA + BM * ROWB;
 #pragma unroll
-    for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(bias4[j].x), "v"(bias4[j].y), "v"(bias4[j].z), "v"(bias4[j].w));
-    gemm_epilogue<TM, TN, F, true>(d, acc, m0, n0, wm0, wn0, lane, st_lds, BM, bias4);
+            for (int ks = 0; ks < 2; ++ks) {
+                if (2 * kt + ks < s_lo || 2 * kt + ks >= s_hi) continue;
+                const int slot = ((4 * ks + g) ^ (fr & 7)) * 16;
+                bf16v8 af[TM], bfr[TN];
+#pragma unroll
+                for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const bf16v8*>(sA + (wm0 + 16 * i + fr) * ROWB + slot);
+#pragma unroll
+                for (int j = 0; j < TN; ++j) bfr[j] = *reinterpret_cast<const bf16v8*>(sB + (wn0 + 16 * j + fr) * ROWB + slot);
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+            }
+            // K-tile kt+1 must have landed before the next iteration; K-tiles issued after it may stay in flight
+            if (nxt < nk) wait_vm<(STAGES - 2) * LPT>();
+            else wait_vm<0>();
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            cur = cur + 1 == STAGES ? 0 : cur + 1;
+        }
+        // every wave's LDS reads of this tile retired (barrier above): stage the next tile's first K-tiles now
+        const int64_t m0_done = m0;
+        const int next = tile + (int)gridDim.x;
+        if (next < ntm) {
+            setup(next);
+#pragma unroll
+            for (int s = 0; s < STAGES - 1; ++s)
+                if (s < nk) issue(s, s);
+        }
+#pragma unroll
+        for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(bias4[j].x), "v"(bias4[j].y), "v"(bias4[j].z), "v"(bias4[j].w));
+        gemm_epilogue<TM, TN, F, true>(d, acc, m0_done, n0, wm0, wn0, lane, st_lds, BM, bias4);
+        if (next >= ntm) break;
+        tile = next;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+        // the epilogue's stores sit behind the staged K-tiles on the VM counter: drain all before the barrier
+        wait_vm<0>();
+    }
 }
 
 bool gemm3_supported(const GemmDesc& d) {
@@ -162,10 +195,29 @@ bool gemm3_supported(const GemmDesc& d) {
            (d.act != ACT_GLU || d.N % 32 == 0);
 }
 
+// Persistent grid: resident blocks per CU (occupancy API, once per instantiation) x CUs, split over the N tiles,
+// rounded down to a multiple of 8 (XCD count) and capped at the M tile count.
 template <int BM, int BN, int WM, int WN, int ST, unsigned F>
-static void launch3f(const GemmDesc& d, hipStream_t s) {
+static unsigned resident_grid_x(int ntm, int ntn) {
+    static int resident = 0;
+    if (resident == 0) {
+        int per_cu = 0, cus = 0, dev = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, gemm3_kernel<BM, BN, WM, WN, ST, F>, WM * WN * 64, 0);
+        resident = per_cu > 0 && cus > 0 ? per_cu * cus : -1;
+    }
+    if (resident < 0) return (unsigned)ntm;
+    int gx = resident / ntn / 8 * 8;
+    if (gx < 8) gx = 8;
+    return (unsigned)(gx < ntm ? gx : ntm);
+}
+
+template <int BM, int BN, int WM, int WN, int ST, unsigned F>
+static void launch3f(const GemmDesc& d, hipStream_t s, bool persist) {
     const int64_t M = (int64_t)d.nb * d.H_out * d.W;
-    dim3 grid((unsigned)((M + BM - 1) / BM), (unsigned)((d.N + BN - 1) / BN));
+    const int ntm = (int)((M + BM - 1) / BM), ntn = (d.N + BN - 1) / BN;
+    dim3 grid(persist ? resident_grid_x<BM, BN, WM, WN, ST, F>(ntm, ntn) : (unsigned)ntm, (unsigned)ntn);
     KScope ks(s);
     if (ks.on()) {
         double fl, by;
@@ -176,28 +228,30 @@ static void launch3f(const GemmDesc& d, hipStream_t s) {
 }
 
 template <int BM, int BN, int WM, int WN, int ST>
-static void launch3(const GemmDesc& d, hipStream_t s) {
+static void launch3(const GemmDesc& d, hipStream_t s, bool persist) {
     switch (epi_flags(d)) {
 #define ATHD_CASE(FL) \
-    case (FL): launch3f<BM, BN, WM, WN, ST, (FL)>(d, s); return;
+    case (FL): launch3f<BM, BN, WM, WN, ST, (FL)>(d, s, persist); return;
         ATHD_EPI_LIST(ATHD_CASE)
 #undef ATHD_CASE
-        default: launch3f<BM, BN, WM, WN, ST, F_ALL>(d, s); return;
+        default: launch3f<BM, BN, WM, WN, ST, F_ALL>(d, s, persist); return;
     }
 }
 
 // variant: 0 = auto, 1 = 256x128 (8 waves, 3 stages), 2 = 128x128 (4 waves, 3 stages), 3 = 256x192 (8 waves, 2 st),
 // 4 = 128x192 (4 waves, 2 stages: 80 KB LDS, 2 blocks/CU), 5 = 128x192 (4 waves, 3 stages), 6 = 128x96 (4 waves, 3 st),
-// 7 = 192x192 (8 waves, 3 stages: 144 KB LDS)
+// 7 = 192x192 (8 waves, 3 stages: 144 KB LDS); + 100: persistent grid (resident blocks walk the M tiles)
 int gemm3_launch(const GemmDesc& d, hipStream_t s, int variant) {
+    const bool persist = variant >= 100;
+    if (persist) variant -= 100;
     if (variant == 0) variant = (d.N % 192 == 0 && d.N % 128 != 0) ? 3 : 1;
-    if (variant == 1) launch3<256, 128, 4, 2, 3>(d, s);
-    else if (variant == 2) launch3<128, 128, 2, 2, 3>(d, s);
-    else if (variant == 4) launch3<128, 192, 2, 2, 2>(d, s);
-    else if (variant == 5) launch3<128, 192, 2, 2, 3>(d, s);
-    else if (variant == 6) launch3<128, 96, 2, 2, 3>(d, s);
-    else if (variant == 7) launch3<192, 192, 4, 2, 3>(d, s);
-    else launch3<256, 192, 4, 2, 2>(d, s);
+    if (variant == 1) launch3<256, 128, 4, 2, 3>(d, s, persist);
+    else if (variant == 2) launch3<128, 128, 2, 2, 3>(d, s, persist);
+    else if (variant == 4) launch3<128, 192, 2, 2, 2>(d, s, persist);
+    else if (variant == 5) launch3<128, 192, 2, 2, 3>(d, s, persist);
+    else if (variant == 6) launch3<128, 96, 2, 2, 3>(d, s, persist);
+    else if (variant == 7) launch3<192, 192, 4, 2, 3>(d, s, persist);
+    else launch3<256, 192, 4, 2, 2>(d, s, persist);
     return (int)hipGetLastError();
 }
 

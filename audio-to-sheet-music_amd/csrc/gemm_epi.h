@@ -43,6 +43,15 @@ inline unsigned epi_flags(const GemmDesc& d) {
     X(F_SPLIT | F_STATS | F_CBF16) X(F_SPLIT | F_CBF16) X(F_GLU | F_CBF16) X(F_GLU | F_ROWADD | F_CBF16)         \
     X(F_GN | F_GLU | F_RES | F_CBF16)
 
+// Publishes the LDS statistics partials before the per-block flush: the LDS atomics retired (lgkmcnt) + s_barrier.
+// Not __syncthreads(): that also waits vmcnt(0), i.e. for every output store of the tile to be acknowledged,
+// which holds the block (and, at one block per CU, the CU) for the store latency.
+ATHD_DEV void stats_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
 template <unsigned F>
 ATHD_DEV bool on(unsigned flag) { return (F & flag) != 0; }
 
@@ -275,7 +284,7 @@ ATHD_DEV void gemm_epilogue(const GemmDesc& d, const f32x4_t (&acc)[TM][TN], int
         }
     }
     if (f_stats) {
-        __syncthreads();
+        stats_barrier();
         if (threadIdx.x < EPI_MAXG) {
             const double a = st_lds[2 * threadIdx.x], q = st_lds[2 * threadIdx.x + 1];
             st_lds[2 * threadIdx.x] = 0.0;          // ready for the next tile of a persistent kernel
@@ -397,7 +406,7 @@ ATHD_DEV void gemm_epilogue_res(const GemmDesc& d, const f32x4_t (&acc)[TM][TN],
                 }
             }
         }
-        __syncthreads();
+        stats_barrier();
         if (threadIdx.x < EPI_MAXG) {
             const double a = st_lds[2 * threadIdx.x], q = st_lds[2 * threadIdx.x + 1];
             st_lds[2 * threadIdx.x] = 0.0;

@@ -54,6 +54,8 @@ int kb_convt_quad(int variant, int kskip, const void* A, const void* W, const fl
     d.C = C; d.c_bf16 = 1; d.ldo = Cout; d.stats = stats; d.col_split = Cout; d.hi_row_off = 1;
     d.H_out_total = 2 * H; d.o_stride = 2; d.o_off = -1; d.store_mask = 6;
     if (kskip) d.k_blk = Cin;
+    if (kskip == 2) d.store_mask = 0;       // probe: no stores
+    if (kskip == 3) d.stats = nullptr;      // probe: no statistics
     return gemm3_launch(d, (hipStream_t)stream, variant);
 }
 int kb_attn(const void* qkv, int nb, int N, void* out, void* stream) {

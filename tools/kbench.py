@@ -194,9 +194,12 @@ if __name__ == "__main__":
     if "tr" in sys.argv[1:]:
         tr_probe()
     if "quad" in sys.argv[1:]:
-        vs = [(3, 0), (3, 1), (4, 1), (5, 1), (6, 1), (7, 1)]
+        vs = [(3, 1), (103, 1), (7, 1), (107, 1), (3, 3), (103, 3)]
         quad_case(64, 259, 259, 96, 48, vs)
         quad_case(64, 16538, 1, 96, 48, vs)
+        if "contention" in sys.argv[1:]:    # same rows, statistics groups of 1 / 64 / 2368 batches
+            quad_case(1, 64 * 259, 259, 96, 48, [(3, 1), (3, 3)])
+            quad_case(2368, 7, 259, 96, 48, [(3, 1), (3, 3)])
         sys.exit(0)
     if "convt" in sys.argv[1:]:
         convt_case(64, 259, 259, 192, 96, (2, 33, 34, 35))
@@ -208,6 +211,14 @@ if __name__ == "__main__":
         attn_case(64, 2072)
         sys.exit(0)
     M = 64 * 2072
+    if "persist" in sys.argv[1:]:
+        VARIANTS = (33, 133, 37, 137)
+        gemm_case(M, 1536, 512)
+        gemm_case(M, 512, 2048)
+        gemm_case(M, 512, 512)
+        gemm_case(64 * 259 * 259, 192, 384)
+        gemm_case(64 * 259 * 259, 96, 192)
+        sys.exit(0)
     if "nostore" in sys.argv[1:]:
         VARIANTS = (40, 41, 42)
         gemm_case(M, 1536, 512)
