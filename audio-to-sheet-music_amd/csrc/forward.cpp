@@ -55,6 +55,7 @@ struct Bufs {
     void* saved_t[4];
     void* ybuf;
     float* hbuf;
+    uint16_t* hbuf_b;                 // bf16 mode: GELU(GN(hbuf)) as bf16, the A operand of the wide DConv 1x1 GEMMs
     int ea = 4;
     float *X, *XT;
     void *H[4], *QKV, *O, *F1;
@@ -96,6 +97,7 @@ size_t plan(Arena& ar, const Dims& d, Bufs& b, bool actbf) {
     b.ybuf = act(ymax);
     b.ea = (int)ab;
     b.hbuf = ar.take<float>(hmax);
+    b.hbuf_b = ab == 2 ? ar.take<uint16_t>(hmax) : nullptr;
     b.X = ar.take<float>(B * d.Nf * 512);
     b.XT = ar.take<float>(B * d.Nt * 512);
     for (int i = 0; i < 4; ++i) b.H[i] = act(B * d.Nmax * 512);
@@ -207,12 +209,16 @@ void dconv(Run& r, const EncW& e, const Bufs& b, void* x, int64_t nb, int64_t L)
         g.Wp = e.dc.c3[dd].w; g.N = Hh; g.K = e.dc.c3[dd].K; g.Kp = e.dc.c3[dd].Kp; g.bias = e.dc.c3[dd].bias;
         g.C = b.hbuf; g.H_out_total = (int)L; g.ldo = Hh; g.stats = st_h;
         r.gemm(g, "dconv.conv3");
+        // bf16 mode: GELU(GN(h)) written once as bf16, so both 1x1 passes read half the bytes and run on the bf16
+        // MFMA GEMMs (gemm3 / gemm4) instead of converting fp32 A on load
+        const bool hb = r.actbf && b.hbuf_b && Hh % 8 == 0;
         {
             KSite site("dconv.gn_gelu");
-            gn_gelu_launch(b.hbuf, (int)nb, L * Hh, Hh, st_h, e.dc.g1w[dd], e.dc.g1b[dd], r.s, r.actbf);
+            if (hb) gn_gelu_bf16_launch(b.hbuf, b.hbuf_b, (int)nb, L * Hh, Hh, st_h, e.dc.g1w[dd], e.dc.g1b[dd], r.s);
+            else gn_gelu_launch(b.hbuf, (int)nb, L * Hh, Hh, st_h, e.dc.g1w[dd], e.dc.g1b[dd], r.s, r.actbf);
         }
         GemmDesc g2;
-        g2.A = b.hbuf; g2.nb = (int)nb; g2.H_in = (int)L; g2.W = 1; g2.C_in = Hh; g2.a_ld = Hh; g2.H_out = (int)L;
+        g2.A = hb ? (const void*)b.hbuf_b : (const void*)b.hbuf; g2.a_bf16 = hb ? 1 : 0; g2.nb = (int)nb; g2.H_in = (int)L; g2.W = 1; g2.C_in = Hh; g2.a_ld = Hh; g2.H_out = (int)L;
         g2.Wp = e.dc.c1[dd].w; g2.N = 2 * C; g2.K = Hh; g2.Kp = e.dc.c1[dd].Kp; g2.bias = e.dc.c1[dd].bias;
         g2.C = x; g2.c_bf16 = ab; g2.H_out_total = (int)L; g2.ldo = C;
         GemmDesc g1 = g2;
