@@ -481,6 +481,9 @@ const char* athd_last_error(athd_ctx* c) { return c ? c->err.c_str() : "null con
 void athd_destroy(athd_ctx* c) {
     if (!c) return;
     for (void* p : c->allocs) hipFree(p);
+    if (c->ev_f) (void)hipEventDestroy(c->ev_f);
+    if (c->ev_t) (void)hipEventDestroy(c->ev_t);
+    if (c->s_time) (void)hipStreamDestroy(c->s_time);
     delete c->prof;
     delete c;
 }

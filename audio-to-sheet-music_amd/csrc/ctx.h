@@ -91,6 +91,9 @@ using namespace athd;
 
 struct athd_ctx {
     int device = 0;
+    // second stream + fork/join events: the transformer's time branch runs beside the frequency branch (forward.cpp)
+    hipStream_t s_time = nullptr;
+    hipEvent_t ev_f = nullptr, ev_t = nullptr;
     int mode = 1;
     bool finalized = false;
     std::string err;

@@ -59,6 +59,7 @@ struct Bufs {
     int ea = 4;
     float *X, *XT;
     void *H[4], *QKV, *O, *F1;
+    void *QKVt, *Ot, *F1t;            // the time branch's scratch (it runs on its own stream beside the freq branch)
     float *pos2d, *pos1d, *x_enc, *xt_enc;
     // decode (per chunk)
     float* avec;
@@ -104,6 +105,9 @@ size_t plan(Arena& ar, const Dims& d, Bufs& b, bool actbf) {
     b.QKV = act(B * d.Nmax * 1536);
     b.O = act(B * d.Nmax * 512);
     b.F1 = act(B * d.Nmax * 2048);
+    b.QKVt = act(B * d.Nmax * 1536);
+    b.Ot = act(B * d.Nt * 512);
+    b.F1t = act(B * d.Nt * 2048);
     b.pos2d = ar.take<float>(d.Nf * 512);
     b.pos1d = ar.take<float>(d.Nt * 512);
     b.x_enc = ar.take<float>(B * d.Nf * 384);
@@ -364,18 +368,21 @@ void encode(Run& r, const Dims& d, const Bufs& b, const float* wav) {
         layernorm_launch(l, r.s);
     };
     // attention + FFN of one branch given LN'ed query rows Hq and key/value source (projected inside)
-    auto block = [&](const TLayerW& L, float* X, int64_t N, void* Hq, void* Hkv, int64_t Nk, Pending* pend) {
+    auto block = [&](const TLayerW& L, float* X, int64_t N, void* Hq, void* Hkv, int64_t Nk, Pending* pend, bool tb) {
+        void* const sQKV = tb ? b.QKVt : b.QKV;
+        void* const sO = tb ? b.Ot : b.O;
+        void* const sF1 = tb ? b.F1t : b.F1;
         AttnDesc a;
         a.nb = (int)B; a.Nq = (int)N; a.Nk = (int)Nk; a.heads = 8; a.scale = 0.125f;
         if (!L.cross) {
             GemmDesc g = r.lin(L.qkv, Hq, ab, (int)B, N, 512);
-            g.C = b.QKV; g.c_bf16 = ab;
+            g.C = sQKV; g.c_bf16 = ab;
             r.gemm(g, "qkv");
-            a.Q = b.QKV; a.q_bf16 = ab; a.q_bs = N * 1536; a.q_ld = 1536; a.q_off = 0;
-            a.K = b.QKV; a.k_bf16 = ab; a.k_bs = N * 1536; a.k_ld = 1536; a.k_off = 512;
-            a.V = b.QKV; a.v_bf16 = ab; a.v_bs = N * 1536; a.v_ld = 1536; a.v_off = 1024;
+            a.Q = sQKV; a.q_bf16 = ab; a.q_bs = N * 1536; a.q_ld = 1536; a.q_off = 0;
+            a.K = sQKV; a.k_bf16 = ab; a.k_bs = N * 1536; a.k_ld = 1536; a.k_off = 512;
+            a.V = sQKV; a.v_bf16 = ab; a.v_bs = N * 1536; a.v_ld = 1536; a.v_off = 1024;
         } else {
-            char* Qb = (char*)b.QKV;
+            char* Qb = (char*)sQKV;
             char* KVb = Qb + (size_t)B * d.Nmax * 512 * (ab ? 2 : 4);
             GemmDesc gq = r.lin(L.q, Hq, ab, (int)B, N, 512);
             gq.C = Qb; gq.c_bf16 = ab;
@@ -387,41 +394,72 @@ void encode(Run& r, const Dims& d, const Bufs& b, const float* wav) {
             a.K = KVb; a.k_bf16 = ab; a.k_bs = Nk * 1024; a.k_ld = 1024; a.k_off = 0;
             a.V = KVb; a.v_bf16 = ab; a.v_bs = Nk * 1024; a.v_ld = 1024; a.v_off = 512;
         }
-        a.O = b.O; a.o_bf16 = ab; a.o_bs = N * 512; a.o_ld = 512;
+        a.O = sO; a.o_bf16 = ab; a.o_bs = N * 512; a.o_ld = 512;
         r.check(attn_launch(a, r.mode, r.s), "attention");
-        GemmDesc go = r.lin(L.out, b.O, ab, (int)B, N, 512);
+        GemmDesc go = r.lin(L.out, sO, ab, (int)B, N, 512);
         go.C = X; go.res = X; go.res_scale = L.g1;
         r.gemm(go, "out_proj");
         ln(X, N, L.cross ? L.n3w : L.n2w, L.cross ? L.n3b : L.n2b, nullptr, Hq);
         GemmDesc g1 = r.lin(L.l1, Hq, ab, (int)B, N, 512);
-        g1.C = b.F1; g1.c_bf16 = ab; g1.act = ACT_GELU;
+        g1.C = sF1; g1.c_bf16 = ab; g1.act = ACT_GELU;
         r.gemm(g1, "linear1");
         double* st = r.stats(B);
-        GemmDesc g2 = r.lin(L.l2, b.F1, ab, (int)B, N, 2048);
+        GemmDesc g2 = r.lin(L.l2, sF1, ab, (int)B, N, 2048);
         g2.C = X; g2.res = X; g2.res_scale = L.g2; g2.stats = st;
         r.gemm(g2, "linear2");
         pend->st = st; pend->w = L.now; pend->b = L.nob;
     };
+    // Two streams: the frequency branch on the caller's stream, the time branch on ctx.s_time.  Self-attention
+    // layers are independent per branch; a cross layer joins both streams (each waits for the other's previous
+    // layer: the key/value norms below overwrite buffers the other branch read), computes its four norms, joins
+    // again (each block reads the other branch's kv norm) and runs both blocks side by side.  Buffers: H[0] / H[1]
+    // written only on the freq stream, H[2] / H[3] only on the time stream; separate QKV / O / F1 scratch.
+    if (!c->s_time) {
+        r.check((int)hipStreamCreateWithFlags(&c->s_time, hipStreamNonBlocking), "stream");
+        r.check((int)hipEventCreateWithFlags(&c->ev_f, hipEventDisableTiming), "event");
+        r.check((int)hipEventCreateWithFlags(&c->ev_t, hipEventDisableTiming), "event");
+        if (r.err) return;
+    }
+    hipStream_t const s_f = r.s, s_t = c->s_time;
+    auto join = [&]() {
+        (void)hipEventRecord(c->ev_f, s_f);
+        (void)hipEventRecord(c->ev_t, s_t);
+        (void)hipStreamWaitEvent(s_t, c->ev_f, 0);
+        (void)hipStreamWaitEvent(s_f, c->ev_t, 0);
+    };
+    (void)hipEventRecord(c->ev_f, s_f);          // fork: the time stream starts after everything issued so far
+    (void)hipStreamWaitEvent(s_t, c->ev_f, 0);
     for (int idx = 0; idx < 5; ++idx) {
         const TLayerW& Lf = c->L[idx];
         const TLayerW& Lt = c->Lt[idx];
         if (!Lf.cross) {
+            r.s = s_f;
             ln(b.X, d.Nf, Lf.n1w, Lf.n1b, &pf, b.H[0]);
-            block(Lf, b.X, d.Nf, b.H[0], nullptr, d.Nf, &pf);
-            ln(b.XT, d.Nt, Lt.n1w, Lt.n1b, &pt, b.H[1]);
-            block(Lt, b.XT, d.Nt, b.H[1], nullptr, d.Nt, &pt);
+            block(Lf, b.X, d.Nf, b.H[0], nullptr, d.Nf, &pf, false);
+            r.s = s_t;
+            ln(b.XT, d.Nt, Lt.n1w, Lt.n1b, &pt, b.H[2]);
+            block(Lt, b.XT, d.Nt, b.H[2], nullptr, d.Nt, &pt, true);
         } else {
+            join();
             // all four norms read the pre-layer X / XT (time branch attends to old_x, demucs transformer.py)
+            r.s = s_f;
             ln(b.X, d.Nf, Lf.n1w, Lf.n1b, &pf, b.H[0]);      // applies pending GroupNorm to X
             ln(b.X, d.Nf, Lt.n2w, Lt.n2b, nullptr, b.H[1]);  // kv of the time branch = norm2_t(old_x)
+            r.s = s_t;
             ln(b.XT, d.Nt, Lt.n1w, Lt.n1b, &pt, b.H[2]);     // applies pending GroupNorm to XT
             ln(b.XT, d.Nt, Lf.n2w, Lf.n2b, nullptr, b.H[3]); // kv of the freq branch = norm2(xt)
-            block(Lf, b.X, d.Nf, b.H[0], b.H[3], d.Nt, &pf);
-            block(Lt, b.XT, d.Nt, b.H[2], b.H[1], d.Nf, &pt);
+            join();
+            r.s = s_f;
+            block(Lf, b.X, d.Nf, b.H[0], b.H[3], d.Nt, &pf, false);
+            r.s = s_t;
+            block(Lt, b.XT, d.Nt, b.H[2], b.H[1], d.Nf, &pt, true);
         }
     }
-    gn_apply_launch(b.X, (int)B, d.Nf, 512, pf.st, pf.w, pf.b, r.s);
-    gn_apply_launch(b.XT, (int)B, d.Nt, 512, pt.st, pt.w, pt.b, r.s);
+    r.s = s_f;
+    gn_apply_launch(b.X, (int)B, d.Nf, 512, pf.st, pf.w, pf.b, s_f);
+    gn_apply_launch(b.XT, (int)B, d.Nt, 512, pt.st, pt.w, pt.b, s_t);
+    (void)hipEventRecord(c->ev_t, s_t);          // join: the caller's stream continues after the time branch
+    (void)hipStreamWaitEvent(s_f, c->ev_t, 0);
     {
         GemmDesc g = r.lin(c->down, b.X, 0, (int)B, d.Nf, 512);
         g.C = b.x_enc;
