@@ -60,6 +60,7 @@ struct Bufs {
     float *X, *XT;
     void *H[4], *QKV, *O, *F1;
     void *QKVt, *Ot, *F1t;            // the time branch's scratch (it runs on its own stream beside the freq branch)
+    float *Gt, *Dt;                   // the time decoder's ConvT / merge buffers (second stream too)
     float *pos2d, *pos1d, *x_enc, *xt_enc;
     // decode (per chunk)
     float* avec;
@@ -132,6 +133,13 @@ size_t plan(Arena& ar, const Dims& d, Bufs& b, bool actbf) {
     dm = std::max(dm, d.L[2] * 96);
     dm = std::max(dm, d.L[1] * 48);
     b.D = ar.take<float>(NI * dm);
+    int64_t gt = std::max<int64_t>(4 * d.Nt * 192, 4 * d.L[3] * 96);
+    gt = std::max(gt, 4 * d.L[2] * 48);
+    gt = std::max(gt, d.T * 2);
+    b.Gt = ar.take<float>(NI * gt);
+    int64_t dmt = std::max<int64_t>(d.L[3] * 192, d.L[2] * 96);
+    dmt = std::max(dmt, d.L[1] * 48);
+    b.Dt = ar.take<float>(NI * dmt);
     b.S = act(NI * 32 * Ts * DEC_CH[1]);
     b.Z = act(NI * 32 * Ts * 8 * DEC_CH[2]);
     b.Zs = act(d.Bc * 8 * Ts * 8 * DEC_CH[2]);
@@ -193,6 +201,17 @@ struct Run {
 // Per layer: h = conv3(x) (+stats) -> GN+GELU in place -> 1x1 conv twice: pass 1 only accumulates the GroupNorm
 // statistics of its 2C outputs, pass 2 recomputes them (K = C/8 is tiny) and applies GN -> GLU -> LayerScale
 // -> residual in the epilogue, writing x in place.  The 2C-channel intermediate never touches HBM.
+// the second stream (time branch of the transformer and of the decoder) and its fork / join events, made once
+bool second_stream(Run& r) {
+    athd_ctx* c = r.c;
+    if (!c->s_time) {
+        r.check((int)hipStreamCreateWithFlags(&c->s_time, hipStreamNonBlocking), "stream");
+        r.check((int)hipEventCreateWithFlags(&c->ev_f, hipEventDisableTiming), "event");
+        r.check((int)hipEventCreateWithFlags(&c->ev_t, hipEventDisableTiming), "event");
+    }
+    return r.err == 0;
+}
+
 void dconv(Run& r, const EncW& e, const Bufs& b, void* x, int64_t nb, int64_t L) {
     const int ab = r.actbf ? 1 : 0;
     const int C = e.cout, Hh = C / 8;
@@ -414,12 +433,7 @@ void encode(Run& r, const Dims& d, const Bufs& b, const float* wav) {
     // layer: the key/value norms below overwrite buffers the other branch read), computes its four norms, joins
     // again (each block reads the other branch's kv norm) and runs both blocks side by side.  Buffers: H[0] / H[1]
     // written only on the freq stream, H[2] / H[3] only on the time stream; separate QKV / O / F1 scratch.
-    if (!c->s_time) {
-        r.check((int)hipStreamCreateWithFlags(&c->s_time, hipStreamNonBlocking), "stream");
-        r.check((int)hipEventCreateWithFlags(&c->ev_f, hipEventDisableTiming), "event");
-        r.check((int)hipEventCreateWithFlags(&c->ev_t, hipEventDisableTiming), "event");
-        if (r.err) return;
-    }
+    if (!second_stream(r)) return;
     hipStream_t const s_f = r.s, s_t = c->s_time;
     auto join = [&]() {
         (void)hipEventRecord(c->ev_f, s_f);
@@ -535,6 +549,12 @@ void decode_chunk(Run& r, const Dims& d, const Bufs& b, int64_t s0, int64_t Bc, 
     };
     text_attn(b.x_enc + s0 * d.Nf * 384, d.Nf, b.x_cond);
     text_attn(b.xt_enc + s0 * d.Nt * 384, d.Nt, b.xt_cond);
+    // fork: the time decoder (below, own Gt / Dt buffers) runs on the second stream beside the frequency decoder and
+    // the iSTFT frames; the branches join before combine_kernel, which reads both
+    if (!second_stream(r)) return;
+    hipStream_t const s_main = r.s, s_t = c->s_time;
+    (void)hipEventRecord(c->ev_f, s_main);
+    (void)hipStreamWaitEvent(s_t, c->ev_f, 0);
 
     // ---- frequency decoder (ATHTDemucs_v2.py:82-104, 293-297) ----
     const int ea = b.ea;
@@ -595,6 +615,7 @@ void decode_chunk(Run& r, const Dims& d, const Bufs& b, int64_t s0, int64_t Bc, 
 
     // ---- time decoder (ATHTDemucs_v2.py:125-139, 313-321) ----
     float* xt2 = nullptr;                            // time_out(time decoder) [NI][T][2]
+    r.s = s_t;
     {
         const void* svt[4] = {eoff(b.saved_t[0], s0 * d.L[1] * 48, ea), eoff(b.saved_t[1], s0 * d.L[2] * 96, ea),
                               eoff(b.saved_t[2], s0 * d.L[3] * 192, ea), eoff(b.saved_t[3], s0 * d.L[4] * 384, ea)};
@@ -604,46 +625,49 @@ void decode_chunk(Run& r, const Dims& d, const Bufs& b, int64_t s0, int64_t Bc, 
         for (int i = 0; i < 3; ++i) {
             const DecW& w = c->tdec[i];
             double* st = r.stats(NI);
-            conv_t(r, w, A, ab, NI, (int)Lin, 1, b.G, ab, st, -1, kT[i]);
+            conv_t(r, w, A, ab, NI, (int)Lin, 1, b.Gt, ab, st, -1, kT[i]);
             KStage kst(kT[i]);
             const int64_t target = d.L[3 - i];       // lengths_t reversed
             MergeDesc m;
-            m.src = b.G; m.src_bf16 = ab; m.H_src = (int)(4 * Lin); m.kept = 0; m.C = w.cout; m.fast_gelu = ab;
+            m.src = b.Gt; m.src_bf16 = ab; m.H_src = (int)(4 * Lin); m.kept = 0; m.C = w.cout; m.fast_gelu = ab;
             m.stats = st; m.gn_count = 4 * Lin * w.cout; m.gn_w = w.gnw; m.gn_b = w.gnb;
             m.skip = svt[3 - i]; m.skip_bf16 = ab; m.H_skip = (int)d.L[4 - i]; m.C_skip = ENC_CH[3 - i]; m.P = P;
-            m.out = b.D; m.out_bf16 = ab; m.H_out = (int)target; m.W = 1; m.NI = NI;
+            m.out = b.Dt; m.out_bf16 = ab; m.H_out = (int)target; m.W = 1; m.NI = NI;
             if (i == 2) {
                 // level 2's merge fused with level 3 + resize + skip + time_out 1x1 (4 -> 2) when 4 L1 == T
                 // (dec_last.hip::tdec_tail_kernel): one pass over the ConvT output, xt2 -> D
                 DecLastDesc dl;
-                dl.g = b.G; dl.g_bf16 = ab; dl.Hg = (int)(4 * Lin); dl.stats = st; dl.gn_count = m.gn_count;
+                dl.g = b.Gt; dl.g_bf16 = ab; dl.Hg = (int)(4 * Lin); dl.stats = st; dl.gn_count = m.gn_count;
                 dl.gn_w = w.gnw; dl.gn_b = w.gnb; dl.fast_gelu = ab;
                 dl.skip2 = svt[1]; dl.skip2_bf16 = ab; dl.H_skip2 = (int)d.L[2]; dl.C_skip2 = ENC_CH[1];
                 dl.NI = NI; dl.P = P; dl.H = (int)target; dl.T = d.T;
                 dl.fold = c->tlast; dl.skip = svt[0]; dl.skip_bf16 = ab; dl.H_skip = (int)d.L[1]; dl.C_skip = ENC_CH[0];
-                dl.out = b.D;
+                dl.out = b.Dt;
                 if (tdec_tail_supported(dl)) {
                     KStage kst3("tdec3");
                     r.check(tdec_tail_launch(dl, r.s), "tdec_tail");
-                    xt2 = b.D;
+                    xt2 = b.Dt;
                     break;
                 }
             }
             r.check(dec_merge_launch(m, r.s), "dec_merge");
-            A = b.D;
+            A = b.Dt;
             Lin = target;
         }
         if (!xt2) {
             // ragged T: level 3 + resize + skip + time_out 1x1 (4 -> 2) over the merged 48-channel input (dec_last.hip)
             KStage kst("tdec3");
             DecLastDesc dl;
-            dl.in = b.D; dl.in_bf16 = ab; dl.NI = NI; dl.P = P; dl.H = (int)Lin; dl.T = d.T;
+            dl.in = b.Dt; dl.in_bf16 = ab; dl.NI = NI; dl.P = P; dl.H = (int)Lin; dl.T = d.T;
             dl.fold = c->tlast; dl.skip = svt[0]; dl.skip_bf16 = ab; dl.H_skip = (int)d.L[1]; dl.C_skip = ENC_CH[0];
-            dl.out = b.G;
+            dl.out = b.Gt;
             r.check(tdec_last_launch(dl, r.s), "tdec_last");
-            xt2 = b.G;
+            xt2 = b.Gt;
         }
     }
+    (void)hipEventRecord(c->ev_t, s_t);              // join
+    (void)hipStreamWaitEvent(s_main, c->ev_t, 0);
+    r.s = s_main;
     // ---- iSTFT overlap-add + denorm + branch sum (ATHTDemucs_v2.py:310-324) ----
     b.xt2 = xt2;
     combine_launch(b.frames, NI, (int)Ts, d.T, c->win2, xt2, b.tnorm_std + 2 * s0, P, out + s0 * P * 2 * d.T, r.s);
