@@ -434,7 +434,9 @@ void encode(Run& r, const Dims& d, const Bufs& b, const float* wav) {
     // again (each block reads the other branch's kv norm) and runs both blocks side by side.  Buffers: H[0] / H[1]
     // written only on the freq stream, H[2] / H[3] only on the time stream; separate QKV / O / F1 scratch.
     if (!second_stream(r)) return;
-    hipStream_t const s_f = r.s, s_t = c->s_time;
+    // (while a kernel profile is open the branches run serially on one stream, so per-kernel event times are the
+    // kernel's own and not shared with a concurrent one)
+    hipStream_t const s_f = r.s, s_t = c->prof ? r.s : c->s_time;
     auto join = [&]() {
         (void)hipEventRecord(c->ev_f, s_f);
         (void)hipEventRecord(c->ev_t, s_t);
@@ -552,7 +554,7 @@ void decode_chunk(Run& r, const Dims& d, const Bufs& b, int64_t s0, int64_t Bc, 
     // fork: the time decoder (below, own Gt / Dt buffers) runs on the second stream beside the frequency decoder and
     // the iSTFT frames; the branches join before combine_kernel, which reads both
     if (!second_stream(r)) return;
-    hipStream_t const s_main = r.s, s_t = c->s_time;
+    hipStream_t const s_main = r.s, s_t = c->prof ? r.s : c->s_time;   // serial while profiling (see encode)
     (void)hipEventRecord(c->ev_f, s_main);
     (void)hipStreamWaitEvent(s_t, c->ev_f, 0);
 
