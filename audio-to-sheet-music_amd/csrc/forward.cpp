@@ -202,6 +202,17 @@ struct Run {
 // statistics of its 2C outputs, pass 2 recomputes them (K = C/8 is tiny) and applies GN -> GLU -> LayerScale
 // -> residual in the epilogue, writing x in place.  The 2C-channel intermediate never touches HBM.
 // the second stream (time branch of the transformer and of the decoder) and its fork / join events, made once
+// ATHD_SERIAL=1: both branches on the caller's stream (profiling runs whose per-kernel times should be the kernel's
+// own; also the behaviour while an athd_profile window is open)
+bool serial_branches(const Run& r) {
+    static int env = -1;
+    if (env < 0) {
+        const char* e = std::getenv("ATHD_SERIAL");
+        env = (e && *e && *e != '0') ? 1 : 0;
+    }
+    return env == 1 || r.c->prof != nullptr;
+}
+
 bool second_stream(Run& r) {
     athd_ctx* c = r.c;
     if (!c->s_time) {
@@ -436,7 +447,7 @@ void encode(Run& r, const Dims& d, const Bufs& b, const float* wav) {
     if (!second_stream(r)) return;
     // (while a kernel profile is open the branches run serially on one stream, so per-kernel event times are the
     // kernel's own and not shared with a concurrent one)
-    hipStream_t const s_f = r.s, s_t = c->prof ? r.s : c->s_time;
+    hipStream_t const s_f = r.s, s_t = serial_branches(r) ? r.s : c->s_time;
     auto join = [&]() {
         (void)hipEventRecord(c->ev_f, s_f);
         (void)hipEventRecord(c->ev_t, s_t);
@@ -554,7 +565,7 @@ void decode_chunk(Run& r, const Dims& d, const Bufs& b, int64_t s0, int64_t Bc, 
     // fork: the time decoder (below, own Gt / Dt buffers) runs on the second stream beside the frequency decoder and
     // the iSTFT frames; the branches join before combine_kernel, which reads both
     if (!second_stream(r)) return;
-    hipStream_t const s_main = r.s, s_t = c->prof ? r.s : c->s_time;   // serial while profiling (see encode)
+    hipStream_t const s_main = r.s, s_t = serial_branches(r) ? r.s : c->s_time;   // (see encode)
     (void)hipEventRecord(c->ev_f, s_main);
     (void)hipStreamWaitEvent(s_t, c->ev_f, 0);
 

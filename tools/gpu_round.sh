@@ -16,6 +16,9 @@ tail -1 $O/bench_full.log
 step kernel-trace
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$TAG -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline > $O/prof_$TAG.log 2>&1 || { tail -20 $O/prof_$TAG.log; exit 1; }
 tail -1 $O/prof_$TAG.log
+step kernel-trace-serial
+ATHD_SERIAL=1 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_${TAG}_serial -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline > $O/prof_${TAG}_serial.log 2>&1 || { tail -20 $O/prof_${TAG}_serial.log; exit 1; }
+tail -1 $O/prof_${TAG}_serial.log | cut -c1-200
 step pmc-fetch
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch_$TAG -o run -- python bench.py --steps 1 --warmup 1 --no-cpu-baseline > $O/pmc_fetch_$TAG.log 2>&1 || { tail -20 $O/pmc_fetch_$TAG.log; exit 1; }
 step pmc-write

@@ -7,6 +7,9 @@ set -e
 cp $O/prof_$TAG/run_kernel_stats.csv $P/${TAG}_kernel_stats.csv
 python tools/prof_summary.py $O/prof_$TAG > $P/${TAG}_kernel_summary.txt
 python tools/prof_sections.py $O/prof_$TAG > $P/${TAG}_sections.txt
+cp $O/prof_${TAG}_serial/run_kernel_stats.csv $P/${TAG}_kernel_stats_serial.csv
+python tools/prof_summary.py $O/prof_${TAG}_serial > $P/${TAG}_kernel_summary_serial.txt
+python tools/prof_sections.py $O/prof_${TAG}_serial > $P/${TAG}_sections_serial.txt
 cp $O/pmc_traffic.json $P/pmc_traffic.json
 python tools/pmc_traffic.py $O/pmc_fetch_$TAG $O/pmc_write_$TAG --batch 64 --dtype bf16 -o /tmp/pmc_traffic.json > $P/${TAG}_pmc_traffic_top.txt
 tail -1 $O/bench_full.log > $P/${TAG}_bench.json
