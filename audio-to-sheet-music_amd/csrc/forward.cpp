@@ -54,6 +54,9 @@ struct Bufs {
     void* saved[4];
     void* saved_t[4];
     void* ybuf;
+    void* ybuf_t;                     // the time encoder's level buffers (it runs on the second stream)
+    float* hbuf_t;
+    uint16_t* hbuf_b_t;
     float* hbuf;
     uint16_t* hbuf_b;                 // bf16 mode: GELU(GN(hbuf)) as bf16, the A operand of the wide DConv 1x1 GEMMs
     int ea = 4;
@@ -87,15 +90,20 @@ size_t plan(Arena& ar, const Dims& d, Bufs& b, bool actbf) {
     b.snorm = ar.take<float>(2 * B);
     b.tnorm_div = ar.take<float>(2 * B);
     b.tnorm_std = ar.take<float>(2 * B);
-    int64_t ymax = 0, hmax = 0;
+    int64_t ymax = 0, hmax = 0, ymax_t = 0, hmax_t = 0;
     for (int i = 0; i < 4; ++i) {
         const int64_t C = ENC_CH[i];
         b.saved[i] = act(B * d.F[i + 1] * Ts * C);
         b.saved_t[i] = act(B * d.L[i + 1] * C);
-        const int64_t rows = std::max(B * d.F[i + 1] * Ts, B * d.L[i + 1]);
+        const int64_t rows = B * d.F[i + 1] * Ts, rows_t = B * d.L[i + 1];
         ymax = std::max(ymax, rows * C);
         hmax = std::max(hmax, rows * (C / 8));
+        ymax_t = std::max(ymax_t, rows_t * C);
+        hmax_t = std::max(hmax_t, rows_t * (C / 8));
     }
+    b.ybuf_t = act(ymax_t);
+    b.hbuf_t = ar.take<float>(hmax_t);
+    b.hbuf_b_t = ab == 2 ? ar.take<uint16_t>(hmax_t) : nullptr;
     b.ybuf = act(ymax);
     b.ea = (int)ab;
     b.hbuf = ar.take<float>(hmax);
@@ -223,7 +231,7 @@ bool second_stream(Run& r) {
     return r.err == 0;
 }
 
-void dconv(Run& r, const EncW& e, const Bufs& b, void* x, int64_t nb, int64_t L) {
+void dconv(Run& r, const EncW& e, void* x, int64_t nb, int64_t L, float* hbuf, uint16_t* hbuf_b) {
     const int ab = r.actbf ? 1 : 0;
     const int C = e.cout, Hh = C / 8;
     for (int dd = 0; dd < 2; ++dd) {
@@ -232,7 +240,7 @@ void dconv(Run& r, const EncW& e, const Bufs& b, void* x, int64_t nb, int64_t L)
         double* st_y = r.stats(nb);
         if (C <= 96) {   // narrow levels: HBM-bound VALU kernels (dconv.hip)
             KSite site(dd == 0 ? "dconv0" : "dconv1");
-            r.check(dconv_small_launch(x, ab, b.hbuf, nb, L, C, dil, e.dc.w3f[dd], e.dc.c3[dd].bias, e.dc.g1w[dd],
+            r.check(dconv_small_launch(x, ab, hbuf, nb, L, C, dil, e.dc.w3f[dd], e.dc.c3[dd].bias, e.dc.g1w[dd],
                                        e.dc.g1b[dd], e.dc.w1f[dd], e.dc.b1f[dd], e.dc.g2wf[dd], e.dc.g2bf[dd],
                                        e.dc.scale[dd], st_h, st_y, r.s, r.actbf), "dconv_small");
             continue;
@@ -241,18 +249,18 @@ void dconv(Run& r, const EncW& e, const Bufs& b, void* x, int64_t nb, int64_t L)
         g.A = x; g.a_bf16 = ab; g.nb = (int)nb; g.H_in = (int)L; g.W = 1; g.C_in = C; g.a_ld = C;
         g.ntaps = 3; g.in_stride = 1; g.in_off = -dil; g.dil = dil; g.H_out = (int)L;
         g.Wp = e.dc.c3[dd].w; g.N = Hh; g.K = e.dc.c3[dd].K; g.Kp = e.dc.c3[dd].Kp; g.bias = e.dc.c3[dd].bias;
-        g.C = b.hbuf; g.H_out_total = (int)L; g.ldo = Hh; g.stats = st_h;
+        g.C = hbuf; g.H_out_total = (int)L; g.ldo = Hh; g.stats = st_h;
         r.gemm(g, "dconv.conv3");
         // bf16 mode: GELU(GN(h)) written once as bf16, so both 1x1 passes read half the bytes and run on the bf16
         // MFMA GEMMs (gemm3 / gemm4) instead of converting fp32 A on load
-        const bool hb = r.actbf && b.hbuf_b && Hh % 8 == 0;
+        const bool hb = r.actbf && hbuf_b && Hh % 8 == 0;
         {
             KSite site("dconv.gn_gelu");
-            if (hb) gn_gelu_bf16_launch(b.hbuf, b.hbuf_b, (int)nb, L * Hh, Hh, st_h, e.dc.g1w[dd], e.dc.g1b[dd], r.s);
-            else gn_gelu_launch(b.hbuf, (int)nb, L * Hh, Hh, st_h, e.dc.g1w[dd], e.dc.g1b[dd], r.s, r.actbf);
+            if (hb) gn_gelu_bf16_launch(hbuf, hbuf_b, (int)nb, L * Hh, Hh, st_h, e.dc.g1w[dd], e.dc.g1b[dd], r.s);
+            else gn_gelu_launch(hbuf, (int)nb, L * Hh, Hh, st_h, e.dc.g1w[dd], e.dc.g1b[dd], r.s, r.actbf);
         }
         GemmDesc g2;
-        g2.A = hb ? (const void*)b.hbuf_b : (const void*)b.hbuf; g2.a_bf16 = hb ? 1 : 0; g2.nb = (int)nb; g2.H_in = (int)L; g2.W = 1; g2.C_in = Hh; g2.a_ld = Hh; g2.H_out = (int)L;
+        g2.A = hb ? (const void*)hbuf_b : (const void*)hbuf; g2.a_bf16 = hb ? 1 : 0; g2.nb = (int)nb; g2.H_in = (int)L; g2.W = 1; g2.C_in = Hh; g2.a_ld = Hh; g2.H_out = (int)L;
         g2.Wp = e.dc.c1[dd].w; g2.N = 2 * C; g2.K = Hh; g2.Kp = e.dc.c1[dd].Kp; g2.bias = e.dc.c1[dd].bias;
         g2.C = x; g2.c_bf16 = ab; g2.H_out_total = (int)L; g2.ldo = C;
         GemmDesc g1 = g2;
@@ -295,6 +303,12 @@ void encode(Run& r, const Dims& d, const Bufs& b, const float* wav) {
     input_norm_params_launch(st_wav, (int)B, 2 * d.T, b.tnorm_div, b.tnorm_std, r.s);
 
     // ---- encoders (ATHTDemucs_v2.py:197-217; HEncLayer + DConv) ----
+    // fork: the time encoder runs on the second stream (own ybuf_t / hbuf_t) beside the frequency encoder; the
+    // branches join before the transformer's up-projections
+    if (!second_stream(r)) return;
+    hipStream_t const s_enc = r.s, s_tenc = serial_branches(r) ? r.s : c->s_time;
+    (void)hipEventRecord(c->ev_f, s_enc);
+    (void)hipStreamWaitEvent(s_tenc, c->ev_f, 0);
     const int eab = r.actbf ? 1 : 0;       // encoder activations in bf16 (throughput mode)
     static const char* const kFenc[4] = {"fenc0", "fenc1", "fenc2", "fenc3"};
     static const char* const kTenc[4] = {"tenc0", "tenc1", "tenc2", "tenc3"};
@@ -335,7 +349,7 @@ void encode(Run& r, const Dims& d, const Bufs& b, const float* wav) {
         g.Wp = e.conv.w; g.N = C; g.K = e.conv.K; g.Kp = e.conv.Kp; g.bias = e.conv.bias;
         g.C = b.ybuf; g.c_bf16 = eab; g.H_out_total = Fo; g.ldo = C; g.act = ACT_GELU;
         r.gemm(g, "fenc.conv");
-        dconv(r, e, b, b.ybuf, B * Fo, Ts);
+        dconv(r, e, b.ybuf, B * Fo, Ts, b.hbuf, b.hbuf_b);
         GemmDesc gr;
         gr.A = b.ybuf; gr.a_bf16 = eab; gr.nb = (int)B; gr.H_in = Fo; gr.W = (int)Ts; gr.C_in = C; gr.a_ld = C; gr.H_out = Fo;
         gr.Wp = e.rewrite.w; gr.N = 2 * C; gr.K = C; gr.Kp = e.rewrite.Kp; gr.bias = e.rewrite.bias;
@@ -345,28 +359,32 @@ void encode(Run& r, const Dims& d, const Bufs& b, const float* wav) {
         }
 
         // time branch: right zero-pad to a multiple of 4 is implicit (rows >= L read as 0)
+        r.s = s_tenc;
         KStage tstage(kTenc[i]);
         const EncW& et = c->tenc[i];
         const int64_t Li = d.L[i], Lo = d.L[i + 1];
         if (i == 0) {
             KSite site("tenc.conv");
-            tconv0_launch(wav, (int)B, d.T, Lo, et.conv_f32, et.conv.bias, b.tnorm_div, b.ybuf, eab, r.s);
+            tconv0_launch(wav, (int)B, d.T, Lo, et.conv_f32, et.conv.bias, b.tnorm_div, b.ybuf_t, eab, r.s);
         } else {
             GemmDesc gt;
             gt.A = b.saved_t[i - 1]; gt.a_bf16 = eab; gt.a_ld = et.cin;
             gt.nb = (int)B; gt.H_in = (int)Li; gt.W = 1; gt.C_in = et.cin;
             gt.ntaps = 8; gt.in_stride = 4; gt.in_off = -2; gt.dil = 1; gt.H_out = (int)Lo;
             gt.Wp = et.conv.w; gt.N = C; gt.K = et.conv.K; gt.Kp = et.conv.Kp; gt.bias = et.conv.bias;
-            gt.C = b.ybuf; gt.c_bf16 = eab; gt.H_out_total = (int)Lo; gt.ldo = C; gt.act = ACT_GELU;
+            gt.C = b.ybuf_t; gt.c_bf16 = eab; gt.H_out_total = (int)Lo; gt.ldo = C; gt.act = ACT_GELU;
             r.gemm(gt, "tenc.conv");
         }
-        dconv(r, et, b, b.ybuf, B, Lo);
+        dconv(r, et, b.ybuf_t, B, Lo, b.hbuf_t, b.hbuf_b_t);
         GemmDesc grt;
-        grt.A = b.ybuf; grt.a_bf16 = eab; grt.nb = (int)B; grt.H_in = (int)Lo; grt.W = 1; grt.C_in = C; grt.a_ld = C; grt.H_out = (int)Lo;
+        grt.A = b.ybuf_t; grt.a_bf16 = eab; grt.nb = (int)B; grt.H_in = (int)Lo; grt.W = 1; grt.C_in = C; grt.a_ld = C; grt.H_out = (int)Lo;
         grt.Wp = et.rewrite.w; grt.N = 2 * C; grt.K = C; grt.Kp = et.rewrite.Kp; grt.bias = et.rewrite.bias;
         grt.C = b.saved_t[i]; grt.c_bf16 = eab; grt.H_out_total = (int)Lo; grt.ldo = C; grt.act = ACT_GLU;
         r.gemm(grt, "tenc.rewrite");
+        r.s = s_enc;
     }
+    (void)hipEventRecord(c->ev_t, s_tenc);        // join
+    (void)hipStreamWaitEvent(s_enc, c->ev_t, 0);
 
     // ---- cross-transformer (ATHTDemucs_v2.py:219-234) ----
     KStage xstage("transformer");
