@@ -11,6 +11,21 @@
 
 namespace athd {
 
+// Block -> (query block, head, batch), XCD-aware (cdna_hip_programming.md T1): block i runs on XCD i % 8, so the
+// tiles (bh-major, the ceil(Nq/128) query blocks of one (b, h) consecutive) are cut into 8 contiguous ranges, one
+// per XCD.  All query blocks of a (b, h) then run on one XCD at about the same time and its K / V come from HBM
+// once into that XCD's L2, instead of once per XCD they were spread over.
+ATHD_DEV void attn_tile(const AttnDesc& d, int& qb, int& h, int64_t& b) {
+    const int n = (int)gridDim.x, i = (int)blockIdx.x;
+    const int q = n / 8, r = n % 8, x = i % 8;
+    const int t = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i / 8;
+    const int gq = (d.Nq + 127) / 128;
+    qb = t % gq;
+    const int bh = t / gq;
+    h = bh % d.heads;
+    b = bh / d.heads;
+}
+
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16v8;
 typedef __attribute__((ext_vector_type(4))) __bf16 bf16v4;
 
@@ -40,9 +55,10 @@ __global__ __launch_bounds__(256) void attn_kernel(const AttnDesc d) {
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int g = lane >> 4, c16 = lane & 15;
-    const int h = blockIdx.y;
-    const int64_t b = blockIdx.z;
-    const int q0 = blockIdx.x * 128 + wave * 32;
+    int qblk, h;
+    int64_t b;
+    attn_tile(d, qblk, h, b);
+    const int q0 = qblk * 128 + wave * 32;
     const float sl2 = d.scale * 1.4426950408889634f;
 
     // Q^T fragments (B operand of S^T = K Q^T): lane holds Q[q][32c + 8g + j]
@@ -249,9 +265,10 @@ __global__ __launch_bounds__(256, 3) void attn_bf16_kernel(const AttnDesc d) {
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int g = lane >> 4, c16 = lane & 15;
-    const int h = blockIdx.y;
-    const int64_t b = blockIdx.z;
-    const int q0 = blockIdx.x * 128 + wave * 32;
+    int qblk, h;
+    int64_t b;
+    attn_tile(d, qblk, h, b);
+    const int q0 = qblk * 128 + wave * 32;
     const float sl2 = d.scale * 1.4426950408889634f;
 
     bf16v8 qb[2][2];
@@ -438,7 +455,7 @@ __global__ __launch_bounds__(256, 3) void attn_bf16_kernel(const AttnDesc d) {
 
 int attn_launch(const AttnDesc& d, int mode, hipStream_t s) {
     if (d.heads * 64 > d.o_ld && d.o_ld != 0) return -2;
-    dim3 grid((unsigned)((d.Nq + 127) / 128), (unsigned)d.heads, (unsigned)d.nb);
+    dim3 grid((unsigned)((d.Nq + 127) / 128) * (unsigned)d.heads * (unsigned)d.nb);   // attn_tile decodes it
     KScope ks(s);
     if (ks.on()) {
         const bool v2 = mode == 1 && d.q_bf16 && d.k_bf16 && d.v_bf16;
