@@ -39,7 +39,15 @@ Dims make_dims(int64_t B, int64_t T, int P) {
     d.Nf = 8LL * d.Tspec;
     d.Nt = d.L[4];
     d.Nmax = std::max(d.Nf, d.Nt);
-    int64_t items_per_chunk = 64;
+    // (segment, prompt) items per decode chunk; the decoder's buffers scale with it.  256 = the whole bench batch
+    // (64 segments x 4 prompts) in one chunk: a 51 GB workspace, sized for the 288 GB of HBM, and fewer, larger
+    // decoder launches (measured 32 / 64 / 128 / 256 items: 1203 / 1238 / 1263 / 1284 segments/s).
+    // ATHD_DECODE_ITEMS overrides (smaller GPUs or co-resident jobs).
+    int64_t items_per_chunk = 256;
+    if (const char* e = std::getenv("ATHD_DECODE_ITEMS")) {
+        const long v = std::strtol(e, nullptr, 10);
+        if (v > 0) items_per_chunk = v;
+    }
     d.Bc = std::max<int64_t>(1, std::min<int64_t>(B, items_per_chunk / P));
     d.chunks = cdiv(B, d.Bc);
     return d;

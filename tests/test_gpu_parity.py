@@ -154,6 +154,25 @@ def test_batch_independence(models):
     assert torch.allclose(full[1:2], one, atol=1e-5, rtol=1e-5)
 
 
+def test_bench_batch_one_chunk(models):
+    """The bench configuration (B=64 x 6 s x 4 prompts = 256 items, one decode chunk, the largest buffers and
+    launch grids of the path) agrees with the same segments run as a 2-segment batch (bf16: >= 40 dB, see
+    test_forward_prompts_matches_forward)."""
+    from athd.synth import synthetic_batch
+    prompts = ["drums", "bass", "other", "vocals"]
+    base = synthetic_batch(8, 264600, seed0=4242)
+    wav = torch.as_tensor(np.concatenate([base] * 8)).cuda()          # (64, 2, 264600)
+    m = models["bf16"]
+    full = m.forward_prompts(wav, prompts)
+    pick = [0, 63]
+    few = m.forward_prompts(wav[pick], prompts)
+    for i, j in enumerate(pick):
+        for p in range(len(prompts)):
+            assert sdr_db(few[i, p].cpu().numpy(), full[j, p].cpu().numpy()) >= 40.0, (j, prompts[p])
+    del full, few
+    torch.cuda.empty_cache()
+
+
 @pytest.mark.parametrize("T", [30000, 30001])
 def test_intermediates_f32(models, oracle_model, text_table, T):
     """Stage-by-stage parity (f32) via the ATHD_DUMP debug dump: localises any divergence.  T = 30001 runs the
