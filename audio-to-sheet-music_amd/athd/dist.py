@@ -1,20 +1,26 @@
 """Multi-GPU runner for the hot path: one process per GPU under torchrun, `torch.distributed`
 with backend "nccl" (RCCL over xGMI on MI355X).
 
-Units are independent, so sharding needs no data-path collective; the single exchange is north_star's gather of
-results to rank 0:
-  * `separate_segments`: N segments -> contiguous blocks of ceil(N/W) per rank; each rank runs
-    `forward_prompts` on its block (encode once, decode P times) and rank `dst` gathers (B_r, P, 2, T) from all
-    ranks with one `gather` per call.
-  * `separate_track_sharded`: the windows of one track (test_inference.py:92-141) -> contiguous window ranges per
-    rank; each rank overlap-adds its windows into a partial track span (athd_overlap_add with [k0, k1)); rank
-    `dst` gathers the spans and adds them in rank order.  Seams get window k-1 then window k, as in the
-    reference loop, and 0.0f + x = x elsewhere, so the result equals the single-GPU track bit-exactly.
-Span and block sizes follow from the plan, so no size exchange is needed; ragged blocks are padded for the
-gather and cut on rank `dst`.
+Units are independent, so sharding needs no data-path collective; the one exchange is north_star's gather of the
+separated waveforms to rank `dst`:
+  * `separate_segments`: N segments -> contiguous blocks of ceil(N/W) per rank.  Each rank runs `forward_prompts`
+    (encode once, decode P times) on batches of its block.  As soon as a batch is computed its (b, P, 2, T) result
+    is sent point-to-point to `dst`, which receives it straight into its slice of the preallocated (N, P, 2, T)
+    output (the block of rank r is rows [lo_r, hi_r), so every batch lands in one contiguous slice: no padding,
+    no `torch.cat`).  The sends run on RCCL's stream while the next batch computes on the compute stream; at most
+    two batches are in flight per rank.  xGMI is point to point, so a gather to one GPU is one direct link per
+    peer, never a ring.
+  * `separate_track_sharded`: the windows of one track -> contiguous window ranges per rank; each rank overlap-adds
+    its windows into a partial track span and sends it to `dst`, which adds the spans in rank order.  Protocols:
+      - "test_inference" (test_inference.py:92-141, Fade + additive OLA, athd_overlap_add): seams get window k-1
+        then window k as in the reference loop and 0.0f + x = x elsewhere, so the result equals the single-GPU
+        track bit for bit;
+      - "benchmark" (benchmark.py:155-204, weighted OLA, athd_overlap_add_weighted): the partial spans carry the
+        unnormalised sum and the weight sum, added in rank order the same way, then normalised once on `dst`.
+Block, batch and span sizes follow from (N, W) or the window plan, so no size exchange is needed.
 
-`window_fn` / `ola_fn` default to the native path (athd.inference.run_windows / overlap_add); tests substitute
-CPU stand-ins to exercise the sharding and gather logic with the gloo backend.
+`forward_fn` / `window_fn` / `ola_fn` default to the native path; tests substitute CPU stand-ins to exercise the
+sharding and exchange logic with the gloo backend.
 """
 from __future__ import annotations
 
@@ -39,50 +45,97 @@ def _world(group) -> Tuple[int, int]:
     return 1, 0
 
 
-def _gather_padded(t: torch.Tensor, sizes: List[int], dst: int, group) -> Optional[List[torch.Tensor]]:
-    """Gather tensors whose dim 0 is sizes[r] on rank r (padded to max(sizes)) -> list on dst, None elsewhere."""
-    world, rank = _world(group)
-    if world == 1:
-        return [t]
-    mx = max(sizes)
-    pad = torch.zeros((mx,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
-    if t.shape[0]:
-        pad[:t.shape[0]] = t
-    bufs = [torch.empty_like(pad) for _ in range(world)] if rank == dst else None
-    dist.gather(pad, bufs, dst=dst, group=group)
-    if rank != dst:
-        return None
-    return [b[:s] for b, s in zip(bufs, sizes)]
+def _global(group, r: int) -> int:
+    return dist.get_global_rank(group, r) if group is not None else r
+
+
+class PendingSends:
+    """Point-to-point transfers in flight; `limit` bounds how many are outstanding (the oldest is waited on, which
+    only makes the current stream wait for it on NCCL - no host synchronisation)."""
+
+    def __init__(self, limit: Optional[int] = 2):
+        self.limit = limit
+        self.works: List = []
+
+    def add(self, works, keep=None):
+        """works: the list batch_isend_irecv returned; keep: tensors that must stay alive until they complete."""
+        self.works.append((works, keep))
+        while self.limit is not None and len(self.works) > self.limit:
+            for w in self.works.pop(0)[0]:
+                w.wait()
+
+    def wait(self):
+        for ws, _ in self.works:
+            for w in ws:
+                w.wait()
+        self.works = []
 
 
 @torch.no_grad()
 def separate_segments(model, segments: torch.Tensor, prompts: Sequence[str] = STEMS, dst: int = 0, group=None,
-                      max_batch: int = 64, forward_fn: Optional[Callable] = None) -> Optional[torch.Tensor]:
-    """segments: (N, 2, T), the full list (every rank passes the same tensor, or a lazy view); rank r computes
-    block shard_range(N) -> returns (N, P, 2, T) on rank dst, None on the others."""
+                      max_batch: int = 64, forward_fn: Optional[Callable] = None, n_total: Optional[int] = None,
+                      out: Optional[torch.Tensor] = None, pending: Optional[PendingSends] = None
+                      ) -> Optional[torch.Tensor]:
+    """Separate N segments into P stems across the ranks of `group` -> (N, P, 2, T) on rank `dst`, None elsewhere.
+
+    segments: (N, 2, T), the full list on every rank (a host tensor or a lazy view is fine: only this rank's block
+    is read), or - with `n_total=N` - only this rank's block [lo, hi) of shard_range(N, W, rank), e.g. already
+    resident on the device.  `out`: optional preallocated (N, P, 2, T) result on `dst`.  `pending`: a PendingSends
+    to leave the transfers in flight in (the caller waits on it later, e.g. across bench steps); by default they
+    are completed before returning."""
     world, rank = _world(group)
-    N, P = segments.shape[0], len(prompts)
+    N = n_total if n_total is not None else segments.shape[0]
+    P, T = len(prompts), segments.shape[-1]
     lo, hi = shard_range(N, world, rank)
-    fwd = forward_fn or (lambda wav: model.forward_prompts(wav, list(prompts)))
+    if n_total is not None and segments.shape[0] != hi - lo:
+        raise ValueError(f"rank {rank}: expected its block of {hi - lo} segments, got {segments.shape[0]}")
+    base = 0 if n_total is None else lo          # segment index of row 0 of `segments`
+    fwd = forward_fn or (lambda wav, o: model.forward_prompts(wav, list(prompts), out=o))
     dev = model.device if forward_fn is None else segments.device
-    parts = []
-    for b0 in range(lo, hi, max_batch):
-        wav = segments[b0:min(hi, b0 + max_batch)].to(dev, non_blocking=True).contiguous()
-        parts.append(fwd(wav))
-    T = segments.shape[-1]
-    mine = torch.cat(parts) if parts else torch.empty((0, P, 2, T), dtype=torch.float32, device=dev)
-    sizes = [shard_range(N, world, r)[1] - shard_range(N, world, r)[0] for r in range(world)]
-    got = _gather_padded(mine, sizes, dst, group)
-    return torch.cat(got) if got is not None else None
+    if rank == dst:
+        if out is None:
+            out = torch.empty((N, P, 2, T), dtype=torch.float32, device=dev)
+        elif tuple(out.shape) != (N, P, 2, T) or not out.is_contiguous():
+            raise ValueError(f"out must be a contiguous {(N, P, 2, T)} tensor")
+    own = pending is None
+    pend = pending if pending is not None else PendingSends()
+    per = -(-N // world) if N else 0
+    for j in range(-(-per // max_batch) if per else 0):          # same batch count on every rank
+        recvs = []
+        if rank == dst:
+            for r in range(world):
+                a, b = shard_range(N, world, r)
+                b0, b1 = min(b, a + j * max_batch), min(b, a + (j + 1) * max_batch)
+                if r != dst and b1 > b0:
+                    recvs.append(dist.P2POp(dist.irecv, out[b0:b1], _global(group, r), group))
+        b0, b1 = min(hi, lo + j * max_batch), min(hi, lo + (j + 1) * max_batch)
+        if b1 > b0:
+            wav = segments[b0 - base:b1 - base].to(dev, non_blocking=True).contiguous()
+            if rank == dst:
+                res = fwd(wav, out[b0:b1])
+            else:
+                res = fwd(wav, None).contiguous()
+                pend.add(dist.batch_isend_irecv([dist.P2POp(dist.isend, res, _global(group, dst), group)]), res)
+        if recvs:
+            pend.add(dist.batch_isend_irecv(recvs), out)
+    if own:
+        pend.wait()
+    return out if rank == dst else None
 
 
 @torch.no_grad()
 def separate_track_sharded(model, mixture: torch.Tensor, stems: Sequence[str] = STEMS, sample_rate: int = 44100,
                            segment_seconds: float = 6.0, overlap: float = 0.1, dst: int = 0, group=None,
                            max_batch: int = 64, window_fn: Optional[Callable] = None,
-                           ola_fn: Optional[Callable] = None) -> Optional[torch.Tensor]:
-    """One track split by window ranges across ranks -> (S, 2, L) on rank dst (None elsewhere)."""
-    from .inference import overlap_add, run_windows, window_plan
+                           ola_fn: Optional[Callable] = None, protocol: str = "test_inference"
+                           ) -> Optional[torch.Tensor]:
+    """One track split by window ranges across ranks -> (S, 2, L) on rank dst (None elsewhere).
+
+    protocol "test_inference": test_inference.py:92-141 (overlap default 0.1 s); "benchmark": benchmark.py:155-204
+    (pass overlap=1.5 for its default).  window_fn(k0, k1) -> (k1-k0, S, 2, chunk) model outputs; ola_fn(win, k0, k1)
+    -> span (test_inference) or (span, weight sums) (benchmark)."""
+    if protocol not in ("test_inference", "benchmark"):
+        raise ValueError(f"unknown protocol {protocol!r}")
     world, rank = _world(group)
     if mixture.dim() == 3:
         mixture = mixture[0]
@@ -90,28 +143,72 @@ def separate_track_sharded(model, mixture: torch.Tensor, stems: Sequence[str] = 
     chunk_len = int(sample_rate * segment_seconds)
     ov = int(overlap * sample_rate)
     hop = chunk_len - ov
-    plan = window_plan(L, sample_rate, segment_seconds, overlap)
-    n, S = len(plan), len(stems)
+    n = -(-L // hop)
+    S = len(stems)
     ranges = [shard_range(n, world, r) for r in range(world)]
-
-    def span_len(k0, k1):
-        return 0 if k1 <= k0 else min((k1 - 1) * hop + chunk_len, L) - k0 * hop
-
     k0, k1 = ranges[rank]
-    wfn = window_fn or (lambda a, b: run_windows(model, mixture, plan, stems, chunk_len, a, b, max_batch))
-    ofn = ola_fn or (lambda win, a, b: overlap_add(win, L, chunk_len, ov, a, b))
+    bench = protocol == "benchmark"
+    if window_fn is None or ola_fn is None:
+        if bench:
+            from .benchmark import OurModel, overlap_add_weighted
+            om = OurModel(model, segment_seconds=segment_seconds, overlap=overlap, max_batch=max_batch)
+            wfn = lambda a, b: om.run_windows(mixture, stems, a, b)                         # noqa: E731
+            ofn = lambda win, a, b: overlap_add_weighted(win, L, chunk_len, ov, a, b, partial=True)  # noqa: E731
+        else:
+            from .inference import overlap_add, run_windows, window_plan
+            plan = window_plan(L, sample_rate, segment_seconds, overlap)
+            wfn = lambda a, b: run_windows(model, mixture, plan, stems, chunk_len, a, b, max_batch)  # noqa: E731
+            ofn = lambda win, a, b: overlap_add(win, L, chunk_len, ov, a, b)                 # noqa: E731
+        window_fn = window_fn or wfn
+        ola_fn = ola_fn or ofn
+
+    def span_len(a, b):
+        return 0 if b <= a else min((b - 1) * hop + chunk_len, L) - a * hop
+
+    dev = mixture.device
     if k1 > k0:
-        span = ofn(wfn(k0, k1), k0, k1)
+        res = ola_fn(window_fn(k0, k1), k0, k1)
+        span, wsum = res if bench else (res, None)
     else:
-        span = torch.empty((S, 2, 0), dtype=torch.float32, device=mixture.device)
-    # gather along the sample axis: move it to dim 0 for the padded gather
-    sizes = [span_len(a, b) for a, b in ranges]
-    got = _gather_padded(span.permute(2, 0, 1).contiguous(), sizes, dst, group)
-    if got is None:
+        span = torch.empty((S, 2, 0), dtype=torch.float32, device=dev)
+        wsum = torch.empty(0, dtype=torch.float32, device=dev)
+    # exchange: every non-empty span goes to dst point to point (sizes follow from the plan)
+    parts = {rank: (span, wsum)}
+    ops = []
+    for r, (a, b) in enumerate(ranges):
+        m = span_len(a, b)
+        if r == rank or m == 0 or world == 1:
+            continue
+        if rank == dst:
+            pr = (torch.empty((S, 2, m), dtype=torch.float32, device=dev),
+                  torch.empty(m, dtype=torch.float32, device=dev) if bench else None)
+            parts[r] = pr
+            ops.append(dist.P2POp(dist.irecv, pr[0], _global(group, r), group))
+            if bench:
+                ops.append(dist.P2POp(dist.irecv, pr[1], _global(group, r), group))
+    if rank != dst and world > 1 and k1 > k0:
+        ops.append(dist.P2POp(dist.isend, span.contiguous(), _global(group, dst), group))
+        if bench:
+            ops.append(dist.P2POp(dist.isend, wsum.contiguous(), _global(group, dst), group))
+    if ops:
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+    if rank != dst:
         return None
-    final = torch.zeros((S, 2, L), dtype=torch.float32, device=span.device)
-    for (a, b), part in zip(ranges, got):          # rank order = window order
-        if b > a:
-            s0 = a * hop
-            final[:, :, s0:s0 + part.shape[0]] += part.permute(1, 2, 0)
+    final = torch.zeros((S, 2, L), dtype=torch.float32, device=dev)
+    weight = torch.zeros(L, dtype=torch.float32, device=dev) if bench else None
+    for r, (a, b) in enumerate(ranges):                       # rank order = window order
+        if b <= a:
+            continue
+        sp, ws = parts[r]
+        s0 = a * hop
+        final[:, :, s0:s0 + sp.shape[-1]] += sp
+        if bench:
+            weight[s0:s0 + ws.shape[0]] += ws
+    if bench:
+        if weight.device.type == "cuda":
+            from .benchmark import ola_normalize
+            ola_normalize(final, weight)
+        else:                                                  # CPU stand-in runs (tests)
+            final /= weight.clamp(min=1e-8)
     return final

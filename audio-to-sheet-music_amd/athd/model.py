@@ -31,7 +31,8 @@ def _to_numpy(v) -> np.ndarray:
 class AudioTextHTDemucs:
     def __init__(self, htdemucs_model=None, clap_encoder=None, clap_tokenizer=None, model_dim: int = 384,
                  text_dim: int = 512, num_heads: int = 8, sample_rate: int = 44100, segment: float = 7.8,
-                 dtype: str = "bf16", text_table: Optional[Dict[str, np.ndarray]] = None):
+                 dtype: str = "bf16", text_table: Optional[Dict[str, np.ndarray]] = None,
+                 decode_items: Optional[int] = None):
         if (model_dim, text_dim, num_heads) != (384, 512, 8):
             raise ValueError("the native path is built for model_dim=384, text_dim=512, num_heads=8 "
                              "(config.yaml:15-17)")
@@ -40,6 +41,9 @@ class AudioTextHTDemucs:
         self.sample_rate = sample_rate
         self.segment = segment
         self.dtype = dtype
+        # (segment, prompt) items per decode chunk (athd_set_decode_items; None = the library default, 64).  256 puts
+        # a 64-segment x 4-prompt batch in one chunk (51 GB workspace, the bench setting).
+        self.decode_items = decode_items
         self.embedder = PromptEmbedder(clap_encoder, clap_tokenizer, text_table)
         self._weights: Dict[str, np.ndarray] = {}
         if htdemucs_model is not None:
@@ -109,8 +113,15 @@ class AudioTextHTDemucs:
         for k in native.required_keys():
             ctx.set_weight(k, self._weights[k])
         ctx.finalize()
+        if self.decode_items is not None:
+            ctx.set_decode_items(self.decode_items)
         self._ctx = ctx
         return ctx
+
+    def set_decode_items(self, items: Optional[int]):
+        self.decode_items = items
+        if self._ctx is not None:
+            self._ctx.set_decode_items(64 if items is None else items)
 
     def profile_start(self, kernel: Optional[str] = None):
         """Measurement aid (bench.py): HIP-event timing of one kernel (or all) in the following forwards."""

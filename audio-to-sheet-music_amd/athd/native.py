@@ -39,8 +39,17 @@ lib.athd_num_windows.restype = _c.c_int64
 lib.athd_overlap_add.argtypes = [_c.c_void_p, _c.c_int64, _c.c_int64, _c.c_int64, _c.c_int, _c.c_int64, _c.c_int64,
                                  _c.c_void_p, _c.c_void_p]
 lib.athd_overlap_add.restype = _c.c_int
+lib.athd_overlap_add_weighted.argtypes = [_c.c_void_p, _c.c_int64, _c.c_int64, _c.c_int64, _c.c_int, _c.c_int64,
+                                          _c.c_int64, _c.c_void_p, _c.c_void_p, _c.c_void_p]
+lib.athd_overlap_add_weighted.restype = _c.c_int
+lib.athd_ola_normalize.argtypes = [_c.c_void_p, _c.c_void_p, _c.c_int, _c.c_int64, _c.c_void_p]
+lib.athd_ola_normalize.restype = _c.c_int
 lib.athd_sdr.argtypes = [_c.c_void_p, _c.c_void_p, _c.c_int64, _c.c_int64, _c.c_void_p, _c.c_void_p, _c.c_void_p]
 lib.athd_sdr.restype = _c.c_int
+lib.athd_sisdr.argtypes = [_c.c_void_p, _c.c_void_p, _c.c_int64, _c.c_int64, _c.c_void_p, _c.c_void_p, _c.c_void_p]
+lib.athd_sisdr.restype = _c.c_int
+lib.athd_set_decode_items.argtypes = [_c.c_void_p, _c.c_int64]
+lib.athd_set_decode_items.restype = _c.c_int
 lib.athd_profile_start.argtypes = [_c.c_void_p, _c.c_char_p]
 lib.athd_profile_start.restype = _c.c_int
 lib.athd_profile_stop.argtypes = [_c.c_void_p]
@@ -56,8 +65,9 @@ lib.athd_destroy.argtypes = [_c.c_void_p]
 lib.athd_destroy.restype = None
 
 EXPORTED = ["athd_version", "athd_create", "athd_set_weight", "athd_num_required_keys", "athd_required_key",
-            "athd_finalize", "athd_workspace_bytes", "athd_forward", "athd_forward_prompts", "athd_num_windows",
-            "athd_overlap_add", "athd_sdr", "athd_profile_start",
+            "athd_finalize", "athd_set_decode_items", "athd_workspace_bytes", "athd_forward", "athd_forward_prompts",
+            "athd_num_windows", "athd_overlap_add", "athd_overlap_add_weighted", "athd_ola_normalize", "athd_sdr",
+            "athd_sisdr", "athd_profile_start",
             "athd_profile_stop", "athd_profile_count", "athd_profile_get", "athd_last_error", "athd_destroy"]
 
 F32, BF16 = 0, 1
@@ -95,6 +105,10 @@ class Context:
 
     def finalize(self):
         self._check(lib.athd_finalize(self.h), "finalize")
+
+    def set_decode_items(self, items: int):
+        """(segment, prompt) items per decode chunk (the decoder's workspace scales with it; library default 64)."""
+        self._check(lib.athd_set_decode_items(self.h, int(items)), "set_decode_items")
 
     def workspace_bytes(self, B: int, T: int, P: int = 1) -> int:
         return int(lib.athd_workspace_bytes(self.h, B, T, P))

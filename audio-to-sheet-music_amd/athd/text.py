@@ -34,16 +34,17 @@ class PromptEmbedder:
         if self.clap is None or self.tokenizer is None:
             raise KeyError(f"no embedding for prompts {prompts} and no CLAP model/tokenizer to compute one")
         inputs = self.tokenizer(prompts, padding=True, return_tensors="pt")
-        dev = next(self.clap.parameters()).device if hasattr(self.clap, "parameters") else "cpu"
+        params = getattr(self.clap, "parameters", None)
+        dev = next(params()).device if params is not None else "cpu"
         inputs = {k: v.to(dev) for k, v in inputs.items()}
         with torch.no_grad():
-            cls_name = type(self.clap).__name__
-            if cls_name == "ClapModel":
-                out = self.clap.get_text_features(**inputs)
-                if not isinstance(out, torch.Tensor):       # transformers >= 5 returns a ModelOutput
-                    out = getattr(out, "text_embeds", None) or out[0]
-            else:
+            if _is_clap_model(self.clap):
+                out = _text_features(self.clap.get_text_features(**inputs))
+            else:                                             # ClapTextModelWithProjection (:245-248)
                 out = self.clap.forward(**inputs).text_embeds
+        if not isinstance(out, torch.Tensor) or out.dim() != 2 or out.shape[0] != len(prompts):
+            raise ValueError(f"CLAP returned {type(out).__name__} {tuple(getattr(out, 'shape', ()))}, expected "
+                             f"({len(prompts)}, {TEXT_DIM})")
         return out.float().cpu()
 
     def rows(self, text: Union[str, List[str]], batch: int) -> torch.Tensor:
@@ -56,4 +57,38 @@ class PromptEmbedder:
             emb = self._clap_embed(missing)
             for p, e in zip(missing, emb):
                 self.table[p] = e
-        return torch.stack([self.table[p] for p in prompts])
+        out = torch.stack([self.table[p] for p in prompts])
+        if out.shape != (batch, TEXT_DIM):
+            raise ValueError(f"prompt embeddings must be {TEXT_DIM}-d (text_dim, config.yaml:16), got "
+                             f"{tuple(out.shape[1:])}")
+        return out
+
+
+TEXT_DIM = 512
+
+
+def _is_clap_model(m) -> bool:
+    """`isinstance(self.clap, ClapModel)` of ATHTDemucs_v2.py:241 (by class name when transformers is absent)."""
+    try:
+        from transformers import ClapModel
+        if isinstance(m, ClapModel):
+            return True
+    except ImportError:
+        pass
+    return any(c.__name__ == "ClapModel" for c in type(m).__mro__)
+
+
+def _text_features(out) -> torch.Tensor:
+    """`ClapModel.get_text_features` result -> (P, 512) projected, L2-normalised text features.  transformers 4.x
+    (the reference's pin, requirements.txt:14) returns that tensor directly; transformers >= 5 returns a
+    BaseModelOutputWithPooling whose `pooler_output` holds it (its `last_hidden_state` is the 768-d RoBERTa
+    output, not an embedding)."""
+    if isinstance(out, torch.Tensor):
+        return out
+    pooled = getattr(out, "pooler_output", None)
+    if isinstance(pooled, torch.Tensor):
+        return pooled
+    emb = getattr(out, "text_embeds", None)
+    if isinstance(emb, torch.Tensor):
+        return emb
+    raise TypeError(f"unrecognised get_text_features output {type(out).__name__}")

@@ -140,7 +140,7 @@ const std::vector<std::pair<std::string, std::vector<int64_t>>>& keys() {
 // =============================================================================================== ABI
 extern "C" {
 
-int athd_version(void) { return 100; }
+int athd_version(void) { return 101; }
 
 int athd_num_required_keys(void) { return (int)keys().size(); }
 
@@ -412,17 +412,33 @@ int athd_finalize(athd_ctx* c) {
             win2[k] = w * w;
         }
         c->tw = c->dalloc<float2>(4096);
-        hipMemcpy(c->tw, tw.data(), 4096 * sizeof(float2), hipMemcpyHostToDevice);
+        c->h2d(c->tw, tw.data(), 4096 * sizeof(float2));
         c->tw64 = c->dalloc<double2>(4096);
-        hipMemcpy(c->tw64, tw64.data(), 4096 * sizeof(double2), hipMemcpyHostToDevice);
+        c->h2d(c->tw64, tw64.data(), 4096 * sizeof(double2));
         c->win = c->up_f32(win);
         c->win2 = c->up_f32(win2);
     }
     for (void* p : c->allocs)
         if (!p) return c->fail(ATHD_EHIP, "device allocation failed");
+    if (c->upload_failed) return c->fail(ATHD_EHIP, "weight upload failed");
+    // the time branch's stream and the fork / join events, made here so that athd_forward* create nothing (they
+    // can then be captured in a HIP graph from the first call on)
+    if (!c->s_time && hipStreamCreateWithFlags(&c->s_time, hipStreamNonBlocking) != hipSuccess)
+        return c->fail(ATHD_EHIP, "stream creation failed");
+    if (!c->ev_f && hipEventCreateWithFlags(&c->ev_f, hipEventDisableTiming) != hipSuccess)
+        return c->fail(ATHD_EHIP, "event creation failed");
+    if (!c->ev_t && hipEventCreateWithFlags(&c->ev_t, hipEventDisableTiming) != hipSuccess)
+        return c->fail(ATHD_EHIP, "event creation failed");
     if (hipDeviceSynchronize() != hipSuccess) return c->fail(ATHD_EHIP, "upload failed");
     c->host.clear();
     c->finalized = true;
+    return ATHD_OK;
+}
+
+int athd_set_decode_items(athd_ctx* c, int64_t items) {
+    if (!c) return ATHD_EINVAL;
+    if (items < 1 || items > 4096) return c->fail(ATHD_EINVAL, "decode_items must be in [1, 4096]");
+    c->decode_items = items;
     return ATHD_OK;
 }
 
@@ -438,9 +454,26 @@ int athd_overlap_add(const float* windows, int64_t length, int64_t chunk_len, in
     return rc == 0 ? ATHD_OK : (rc == -1 ? ATHD_EINVAL : ATHD_EHIP);
 }
 
+int athd_overlap_add_weighted(const float* windows, int64_t length, int64_t chunk_len, int64_t overlap, int n_stems,
+                              int64_t k0, int64_t k1, float* out, float* weight, void* stream) {
+    const int rc = ola_launch(windows, length, chunk_len, overlap, n_stems, k0, k1, out, (hipStream_t)stream, 1, weight);
+    return rc == 0 ? ATHD_OK : (rc == -1 ? ATHD_EINVAL : ATHD_EHIP);
+}
+
+int athd_ola_normalize(float* out, const float* weight, int rows, int64_t n, void* stream) {
+    const int rc = ola_normalize_launch(out, weight, rows, n, (hipStream_t)stream);
+    return rc == 0 ? ATHD_OK : (rc == -1 ? ATHD_EINVAL : ATHD_EHIP);
+}
+
 int athd_sdr(const float* est, const float* target, int64_t rows, int64_t n, double* scratch, float* out,
              void* stream) {
     const int rc = sdr_launch(est, target, rows, n, scratch, out, (hipStream_t)stream);
+    return rc == 0 ? ATHD_OK : (rc == -1 ? ATHD_EINVAL : ATHD_EHIP);
+}
+
+int athd_sisdr(const float* est, const float* target, int64_t rows, int64_t n, double* scratch, float* out,
+               void* stream) {
+    const int rc = sisdr_launch(est, target, rows, n, scratch, out, (hipStream_t)stream);
     return rc == 0 ? ATHD_OK : (rc == -1 ? ATHD_EINVAL : ATHD_EHIP);
 }
 
@@ -480,7 +513,7 @@ const char* athd_last_error(athd_ctx* c) { return c ? c->err.c_str() : "null con
 
 void athd_destroy(athd_ctx* c) {
     if (!c) return;
-    for (void* p : c->allocs) hipFree(p);
+    for (void* p : c->allocs) (void)hipFree(p);
     if (c->ev_f) (void)hipEventDestroy(c->ev_f);
     if (c->ev_t) (void)hipEventDestroy(c->ev_t);
     if (c->s_time) (void)hipStreamDestroy(c->s_time);

@@ -95,6 +95,8 @@ struct athd_ctx {
     hipStream_t s_time = nullptr;
     hipEvent_t ev_f = nullptr, ev_t = nullptr;
     int mode = 1;
+    // (segment, prompt) items per decode chunk (athd_set_decode_items): the decoder's workspace scales with it
+    int64_t decode_items = 64;
     bool finalized = false;
     std::string err;
     std::map<std::string, HostT> host;
@@ -130,9 +132,13 @@ struct athd_ctx {
         return (T*)p;
     }
     const HostT& W(const std::string& k) { return host.at(k); }
+    bool upload_failed = false;
+    void h2d(void* dst, const void* src, size_t bytes) {
+        if (!dst || hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice) != hipSuccess) upload_failed = true;
+    }
     float* up_f32(const std::vector<float>& v) {
         float* p = dalloc<float>(v.size());
-        if (p) hipMemcpy(p, v.data(), v.size() * 4, hipMemcpyHostToDevice);
+        h2d(p, v.data(), v.size() * 4);
         return p;
     }
     float* up_key(const std::string& k) { return up_f32(W(k).v); }
@@ -150,7 +156,7 @@ struct athd_ctx {
             for (int n = 0; n < N; ++n)
                 for (int k = 0; k < K; ++k) p[(size_t)n * g.Kp + k] = host_f2bf(w[(size_t)n * K + k]);
             void* d = dalloc<uint16_t>(p.size());
-            hipMemcpy(d, p.data(), p.size() * 2, hipMemcpyHostToDevice);
+            h2d(d, p.data(), p.size() * 2);
             g.w = d;
         } else {
             std::vector<float> p((size_t)Nalloc * g.Kp, 0.f);

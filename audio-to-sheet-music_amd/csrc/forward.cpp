@@ -28,7 +28,7 @@ struct Dims {
     int64_t chunks = 0;
 };
 
-Dims make_dims(int64_t B, int64_t T, int P) {
+Dims make_dims(const athd_ctx* c, int64_t B, int64_t T, int P) {
     Dims d;
     d.B = B;
     d.T = T;
@@ -39,11 +39,11 @@ Dims make_dims(int64_t B, int64_t T, int P) {
     d.Nf = 8LL * d.Tspec;
     d.Nt = d.L[4];
     d.Nmax = std::max(d.Nf, d.Nt);
-    // (segment, prompt) items per decode chunk; the decoder's buffers scale with it.  256 = the whole bench batch
-    // (64 segments x 4 prompts) in one chunk: a 51 GB workspace, sized for the 288 GB of HBM, and fewer, larger
-    // decoder launches (measured 32 / 64 / 128 / 256 items: 1203 / 1238 / 1263 / 1284 segments/s).
-    // ATHD_DECODE_ITEMS overrides (smaller GPUs or co-resident jobs).
-    int64_t items_per_chunk = 256;
+    // (segment, prompt) items per decode chunk; the decoder's buffers scale with it.  Library default 64 (an 18 GB
+    // workspace at B=64 x P=4); bench.py sets 256 = the whole bench batch in one chunk (51 GB, sized for the 288 GB
+    // of HBM: fewer, larger decoder launches; measured 32 / 64 / 128 / 256 items: 1203 / 1238 / 1263 / 1284
+    // segments/s).  ATHD_DECODE_ITEMS overrides the context's setting.
+    int64_t items_per_chunk = c ? c->decode_items : 64;
     if (const char* e = std::getenv("ATHD_DECODE_ITEMS")) {
         const long v = std::strtol(e, nullptr, 10);
         if (v > 0) items_per_chunk = v;
@@ -229,13 +229,9 @@ bool serial_branches(const Run& r) {
     return env == 1 || r.c->prof != nullptr;
 }
 
+// (created by athd_finalize: a forward creates no HIP objects, so it can be graph-captured from the first call)
 bool second_stream(Run& r) {
-    athd_ctx* c = r.c;
-    if (!c->s_time) {
-        r.check((int)hipStreamCreateWithFlags(&c->s_time, hipStreamNonBlocking), "stream");
-        r.check((int)hipEventCreateWithFlags(&c->ev_f, hipEventDisableTiming), "event");
-        r.check((int)hipEventCreateWithFlags(&c->ev_t, hipEventDisableTiming), "event");
-    }
+    if (!r.c->s_time || !r.c->ev_f || !r.c->ev_t) r.check((int)hipErrorInvalidResourceHandle, "second stream");
     return r.err == 0;
 }
 
@@ -285,6 +281,7 @@ bool br_fused(const EncW& e, int Ts) { return e.dc.c3p[0].w && e.dc.c3p[1].w && 
 
 void encode(Run& r, const Dims& d, const Bufs& b, const float* wav) {
     athd_ctx* c = r.c;
+    KSection sec_enc("encoder");
     const int64_t B = d.B, Ts = d.Tspec;
     // ---- STFT + CaC, input normalisation statistics (ATHTDemucs_v2.py:261-275) ----
     PadPlan pp;
@@ -396,6 +393,7 @@ void encode(Run& r, const Dims& d, const Bufs& b, const float* wav) {
 
     // ---- cross-transformer (ATHTDemucs_v2.py:219-234) ----
     KStage xstage("transformer");
+    KSection sec_x("transformer");
     const int ab = r.actbf ? 1 : 0;
     {
         GemmDesc g = r.lin(c->up, b.saved[3], ab, (int)B, d.Nf, 384);
@@ -566,6 +564,7 @@ void conv_t(Run& r, const DecW& w, const void* A, int a_bf16, int nb, int H_in, 
 void decode_chunk(Run& r, const Dims& d, const Bufs& b, int64_t s0, int64_t Bc, const float* text, bool text_per_item,
                   float* out) {
     athd_ctx* c = r.c;
+    KSection sec_dec("decoder");
     const int P = d.P;
     const int NI = (int)(Bc * P);
     const int64_t Ts = d.Tspec;
@@ -756,7 +755,7 @@ int forward_impl(athd_ctx* c, const float* wav, int64_t B, int64_t T, const floa
     if (!wav || !text || !out || B <= 0 || T <= 0 || P <= 0) return c->fail(ATHD_EINVAL, "bad forward arguments");
     if (P > 256) return c->fail(ATHD_EINVAL, "at most 256 prompts per athd_forward_prompts call");
     if (T > (int64_t)1 << 26) return c->fail(ATHD_EINVAL, "segment too long");
-    const Dims d = make_dims(B, T, P);
+    const Dims d = make_dims(c, B, T, P);
     Bufs b;
     Arena sz;
     const size_t need = plan(sz, d, b, c->mode == 1);
@@ -799,7 +798,7 @@ size_t athd_workspace_bytes(athd_ctx* c, int64_t B, int64_t T, int P) {
     if (!c || B <= 0 || T <= 0 || P <= 0) return 0;
     Bufs b;
     Arena a;
-    return plan(a, make_dims(B, T, P), b, c->mode == 1);
+    return plan(a, make_dims(c, B, T, P), b, c->mode == 1);
 }
 
 int athd_forward(athd_ctx* c, const float* wav, int64_t B, int64_t T, const float* text_emb, float* out, void* ws,

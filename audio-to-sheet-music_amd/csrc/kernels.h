@@ -142,9 +142,13 @@ void wav_interleave_launch(const float* wav, int nb, int64_t T, float* out, hipS
 void pos2d_launch(float* out, int Fr, int T1, int C, hipStream_t s);   // out[(f*T1+t)][C]
 void pos1d_launch(float* out, int T2, int C, hipStream_t s);           // out[t][C]
 
-// track.hip: window overlap-add of test_inference.py:92-141 and sdr_loss (src/loss.py:9-30)
+// track.hip: window overlap-add of test_inference.py:92-141 (mode 0) and benchmark.py:155-204 (mode 1, weighted;
+// wsum != nullptr: unnormalised partial span + weight sums), sdr_loss / sisdr_loss (src/loss.py:9-68)
 int ola_launch(const float* win, int64_t L, int64_t chunk, int64_t overlap, int S, int64_t k0, int64_t k1, float* out,
-               hipStream_t s);
+               hipStream_t s, int mode = 0, float* wsum = nullptr);
+int ola_normalize_launch(float* out, const float* wsum, int rows, int64_t n, hipStream_t s);
 int sdr_launch(const float* est, const float* tgt, int64_t rows, int64_t n, double* sums, float* out, hipStream_t s);
+int sisdr_launch(const float* est, const float* tgt, int64_t rows, int64_t n, double* scratch, float* out,
+                 hipStream_t s);
 
 }  // namespace athd

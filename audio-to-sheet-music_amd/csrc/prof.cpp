@@ -8,6 +8,7 @@ namespace athd {
 thread_local KProf* t_kprof = nullptr;
 thread_local const char* t_ksite = nullptr;
 thread_local const char* t_kstage = nullptr;
+thread_local const char* t_ksection = nullptr;
 
 static bool sites_on() {
     static const bool on = [] {
@@ -21,13 +22,15 @@ void KScope::begin(const std::string& label0, double flops, double bytes) {
     KProf* p = t_kprof;
     if (!p) return;
     std::string label = label0;
-    if (sites_on() && (t_kstage || t_ksite)) {
+    if (p->only == "@section") {
+        label = t_ksection ? t_ksection : "other";
+    } else if (sites_on() && (t_kstage || t_ksite)) {
         label += "@";
         if (t_kstage) label += t_kstage;
         if (t_kstage && t_ksite) label += ".";
         if (t_ksite) label += t_ksite;
     }
-    if (!p->only.empty() && p->only != label) return;
+    if (!p->only.empty() && p->only != "@section" && p->only != label) return;
     hipEvent_t ev[2];
     for (auto& e : ev) {
         if (!p->pool.empty()) {

@@ -14,7 +14,8 @@
 namespace athd {
 
 struct KProf {
-    std::string only;                      // "" = every kernel, else one label
+    std::string only;                      // "" = every kernel, "@section" = every kernel aggregated per forward
+                                           // section (KSection), else one label
     struct Rec { std::string label; hipEvent_t a, b; double flops, bytes; };
     struct Agg { std::string label; long long n; double ms, flops, bytes; };
     std::vector<Rec> recs;
@@ -27,6 +28,12 @@ struct KProf {
 extern thread_local KProf* t_kprof;
 extern thread_local const char* t_ksite;    // call-site tags appended as "@stage.site" when ATHD_PROF_SITES=1
 extern thread_local const char* t_kstage;
+extern thread_local const char* t_ksection;  // "encoder" / "transformer" / "decoder" (profile mode "@section")
+struct KSection {
+    const char* saved;
+    explicit KSection(const char* s) : saved(t_ksection) { t_ksection = s; }
+    ~KSection() { t_ksection = saved; }
+};
 struct KStage {                               // RAII stage tag (e.g. "fenc2", "fdec1")
     const char* saved;
     explicit KStage(const char* s) : saved(t_kstage) { t_kstage = s; }

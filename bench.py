@@ -1,16 +1,23 @@
 """Throughput bench of the MI355X-native AudioTextHTDemucs hot path.
 
-Workload (BASELINE.json configs[2]): per GPU a batch of B=64 synthetic 6 s 44.1 kHz stereo segments, each
-separated into all 4 stems (drums/bass/other/vocals) - encode once, decode 4x (athd_forward_prompts).  A "step"
-is one such batch.  `value` = segments/s over all ranks (each segment fully separated into 4 stems).
-Multi-GPU: one process per GPU (torchrun), segments sharded across ranks (weak scaling), no data-path
-collective; timing = barrier + sync around K steps, max over ranks.
+Workload (BASELINE.json configs[2]): per GPU a batch of B=64 distinct synthetic 6 s 44.1 kHz stereo segments, each
+separated into all 4 stems (drums/bass/other/vocals) - encode once, decode 4x (athd_forward_prompts).  A "step" is
+one such batch per GPU.  `value` = segments/s over all ranks (each segment fully separated into 4 stems).
+Multi-GPU (configs[3] shape): one process per GPU (torchrun), segments sharded across ranks (weak scaling); every
+step runs athd.dist.separate_segments, so the point-to-point RCCL gather of all separated waveforms to rank 0
+(xGMI) is inside the timed region, overlapped with the next step's compute.  Timing = barrier + sync around K steps,
+max over ranks.
+
+Beside the headline (all outside the timed region, rank 0): the roofline of the dominant kernel (HIP events) and of
+each forward section, the whole-step MFMA fraction, the bf16 output's SDR against the fp32 oracle, an f32-mode
+(parity mode) throughput line, and the CPU baseline (the oracle on the host's cores).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--dtype bf16|f32] [--no-cpu-baseline]
 """
 import argparse
 import json
 import os
+import statistics
 import sys
 import time
 
@@ -28,14 +35,14 @@ ENC_GMAC, DEC_GMAC = 87.03, 10.31
 BF16_PEAK_TFLOPS = 2500.0     # MI355X dense bf16 MFMA (MI355X_MICROARCH.md chip table)
 F32_PEAK_TFLOPS = 157.3
 HBM_PEAK_GBS = 8000.0
-MFMA_KERNELS = ("gemm", "attn")   # kernel-name prefixes priced against the MFMA peak; the rest against HBM
+MFMA_KERNELS = ("gemm", "attn", "fenc_row")   # kernel-name prefixes priced against the MFMA peak; the rest HBM
 ROOF_STEPS = 2
 PMC_FILE = os.environ.get("ATHD_PMC_TRAFFIC", os.path.join(REPO, "profiles", "pmc_traffic.json"))
 
 
 def pmc_traffic(kernel, batch, dtype):
     """HBM bytes per launch of `kernel` measured by tools/pmc_traffic.py (rocprofv3 FETCH_SIZE / WRITE_SIZE in
-    separate passes, FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM) for this build and workload, else None."""
+    separate passes, corrected per MI355X_MICROARCH.md §HBM) for this build and workload, else None."""
     try:
         d = json.load(open(PMC_FILE))
     except (OSError, ValueError):
@@ -46,28 +53,89 @@ def pmc_traffic(kernel, batch, dtype):
     return (k["hbm_bytes_per_launch"], os.path.relpath(PMC_FILE, REPO)) if k else (None, None)
 
 
-def cpu_baseline(sd, table, budget_s=15.0):
-    """Oracle (PyTorch-CPU restatement of the reference forward) on the host cores, reference protocol:
-    one forward per (segment, prompt)."""
+def cpu_info():
+    """(threads usable by this process, host logical CPUs, CPU model).  Usable = the process's CPU affinity,
+    capped by the cgroup CPU quota (the GPU box grants each job a share of the host: os.cpu_count() there counts the
+    whole machine, and running that many threads on the share would oversubscribe it)."""
+    host = os.cpu_count() or 1
+    usable = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else host
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            usable = min(usable, max(1, int(int(q) / int(p))))
+    except (OSError, ValueError):
+        pass
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return usable, host, model
+
+
+def cpu_baseline(sd, table):
+    """The oracle (PyTorch-CPU restatement of the reference forward, same torch ops) on the host cores with the
+    reference protocol (one forward per (segment, prompt)), SURVEY.md §8(d): median of 5 timed forwards after 1
+    warm-up, at B=1 (test_inference's batch) and B=8."""
     from oracle.athtdemucs_ref import AudioTextHTDemucsRef
     from athd.synth import synthetic_batch
-    threads = min(16, os.cpu_count() or 1)
+    threads, host, model = cpu_info()
     torch.set_num_threads(threads)
     m = AudioTextHTDemucsRef(sd)
-    wav = torch.as_tensor(synthetic_batch(1, SEG, seed0=4242))
-    te = torch.as_tensor(table[3:4])
-    m.forward(wav, te)                       # warm-up
-    n, t0 = 0, time.perf_counter()
-    while True:
-        m.forward(wav, te)
-        n += 1
-        el = time.perf_counter() - t0
-        if el > budget_s or n >= 20:
-            break
-    per_fwd = el / n
-    return {"value": 1.0 / (4 * per_fwd), "unit": "6s-segments/s (4 stems each)", "cores": threads,
-            "kind": "port", "sample": f"{n} x forward(B=1, T=264600, 1 prompt) = {n} (segment,prompt) pairs, "
-                                      f"{per_fwd * 1e3:.0f} ms each; 4 forwards per segment"}
+    res = {}
+    for B in (1, 8):
+        wav = torch.as_tensor(synthetic_batch(B, SEG, seed0=4242))
+        te = torch.as_tensor(table[3:4]).expand(B, -1).contiguous()
+        m.forward(wav, te)                                  # warm-up
+        ts = []
+        for _ in range(5):
+            t0 = time.perf_counter()
+            m.forward(wav, te)
+            ts.append(time.perf_counter() - t0)
+        res[B] = statistics.median(ts)
+    per1, per8 = res[1], res[8] / 8
+    return {"value": round(1.0 / (4 * per1), 4), "unit": "6s-segments/s (4 stems each: 4 forwards per segment)",
+            "cores": threads, "host_cores": host, "cpu_model": model, "kind": "port",
+            "b8": {"value": round(1.0 / (4 * per8), 4), "ms_per_forward": round(res[8] * 1e3, 1)},
+            "sample": f"median of 5 (after 1 warm-up) forward(B=1, T=264600, 1 prompt) = {per1 * 1e3:.0f} ms; "
+                      f"forward(B=8) = {res[8] * 1e3:.0f} ms; {threads} torch threads"}
+
+
+def sdr_vs_oracle(model, sd, table, wav0):
+    """SDR (dB) of this model's output for one segment x 4 prompts against the fp32 oracle forward (north_star:
+    'SDR delta reported'); min and mean over the prompts."""
+    from oracle.athtdemucs_ref import AudioTextHTDemucsRef
+    got = model.forward_prompts(wav0, STEMS).cpu().double()[0]
+    ref = AudioTextHTDemucsRef(sd).forward_prompts(wav0.cpu(), torch.as_tensor(table)).double()[0]
+    s = [float(10 * torch.log10((ref[p] ** 2).sum() / ((ref[p] - got[p]) ** 2).sum())) for p in range(4)]
+    return {"min": round(min(s), 2), "mean": round(sum(s) / 4, 2), "per_prompt": [round(x, 2) for x in s],
+            "what": "SDR of the bench dtype's output vs the fp32 oracle, segment 0 x 4 prompts (unclamped)"}
+
+
+def f32_line(sd, table, wav, steps=3):
+    """Throughput of the f32 parity mode (fp32 MFMA everywhere) on the same batch, outside the headline."""
+    from athd.model import AudioTextHTDemucs
+    m = AudioTextHTDemucs(dtype="f32", text_table={s: table[i] for i, s in enumerate(STEMS)})
+    m.load_state_dict(sd)
+    m = m.to(wav.device).eval()
+    m.forward_prompts(wav, STEMS)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        m.forward_prompts(wav, STEMS)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    ms = el / steps * 1e3
+    tf = 2e9 * (ENC_GMAC + 4 * DEC_GMAC) * wav.shape[0] / (ms * 1e-3) / 1e12
+    out = {"value": round(wav.shape[0] * steps / el, 3), "unit": "segments/s", "ms_per_step": round(ms, 3),
+           "steps": steps, "warmup": 1, "step_essential_tflops": round(tf, 2),
+           "frac_of_f32_mfma_peak": round(tf / F32_PEAK_TFLOPS, 4)}
+    del m
+    torch.cuda.empty_cache()
+    return out
 
 
 def main():
@@ -78,6 +146,7 @@ def main():
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extras", action="store_true", help="skip the SDR, f32 and section measurements")
     ap.add_argument("--dump-kernels", default=None, help="write the warmup step's per-kernel profile (JSON)")
     ap.add_argument("--kernel", default=None, help="roofline kernel (default: largest summed time in warmup)")
     args = ap.parse_args()
@@ -91,21 +160,32 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=dev)
 
+    from athd.dist import PendingSends, separate_segments
     from athd.model import AudioTextHTDemucs
     from athd.synth import synthetic_batch
     from athd.weights import synthetic_state_dict, synthetic_text_table
 
     sd = synthetic_state_dict(seed=0)
     table = synthetic_text_table(4, seed=7)
-    model = AudioTextHTDemucs(dtype=args.dtype, text_table={s: table[i] for i, s in enumerate(STEMS)})
+    B = args.batch
+    # the whole per-GPU batch in one decode chunk (B x 4 items): fewer, larger decoder launches (51 GB workspace)
+    model = AudioTextHTDemucs(dtype=args.dtype, text_table={s: table[i] for i, s in enumerate(STEMS)},
+                              decode_items=B * len(STEMS))
     model.load_state_dict(sd)
     model = model.to(dev).eval()
-    B = args.batch
-    # distinct synthetic segments per rank (weak scaling: each rank owns its shard of segments)
-    base = synthetic_batch(min(B, 8), SEG, seed0=1000 + 64 * rank)
-    wav = torch.as_tensor(np.concatenate([base] * ((B + len(base) - 1) // len(base)))[:B]).to(dev)
+    # B distinct synthetic segments per rank, resident in HBM before timing (weak scaling: each rank owns its block)
+    wav = torch.as_tensor(synthetic_batch(B, SEG, seed0=1000 + B * rank)).to(dev)
+    N = B * world
+    out = torch.empty((N, len(STEMS), 2, SEG), dtype=torch.float32, device=dev) if rank == 0 else None
+    pending = PendingSends(limit=None)
 
     def step():
+        if world == 1:
+            return model.forward_prompts(wav, STEMS, out=out)
+        # shard + point-to-point gather of the separated waveforms to rank 0, transfers left in flight
+        return separate_segments(model, wav, STEMS, max_batch=B, n_total=N, out=out, pending=pending)
+
+    def fwd_only():
         return model.forward_prompts(wav, STEMS)
 
     # warmup; the last warmup step times every kernel (HIP events) to find the dominant one
@@ -113,6 +193,7 @@ def main():
         if i == args.warmup - 1:
             model.profile_start(None)
         step()
+    pending.wait()
     torch.cuda.synchronize()
     dominant = args.kernel
     if args.warmup > 0:
@@ -125,7 +206,7 @@ def main():
         if dominant is None:
             dominant = max(allk, key=lambda r: r["ms"])["kernel"]
     if dominant is None:
-        dominant = "gemm3_kernel<256,192,4,2,2,200>"
+        dominant = "attn_bf16_kernel"
 
     def barrier():
         if world > 1:
@@ -135,33 +216,40 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        out = step()
+        step()
+    pending.wait()
     torch.cuda.synchronize()
     barrier()
     el = time.perf_counter() - t0
     # roofline kernel: every launch of it bracketed with HIP events on its launch stream, over ROOF_STEPS further
-    # steps outside the timed region (with a profile open the library runs the freq / time branches serially on one
-    # stream, so the events time the kernel alone rather than sharing the chip with the other branch)
+    # forwards outside the timed region (with a profile open the library runs the freq / time branches serially on
+    # one stream, so the events time the kernel alone rather than sharing the chip with the other branch)
     model.profile_start(dominant)
     for _ in range(ROOF_STEPS):
-        step()
+        fwd_only()
     torch.cuda.synchronize()
     prof = model.profile_stop()
+    sections = None
+    if not args.no_extras:
+        model.profile_start("@section")
+        fwd_only()
+        torch.cuda.synchronize()
+        sections = model.profile_stop()
     if world > 1:
         t = torch.tensor([el], device=dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         el = float(t.item())
     ms = el / args.steps * 1e3
     value = B * world * args.steps / el
+    peak_mfma = BF16_PEAK_TFLOPS if args.dtype == "bf16" else F32_PEAK_TFLOPS
     flops_step = 2e9 * (ENC_GMAC + 4 * DEC_GMAC) * B
     step_tf = flops_step / (ms * 1e-3) / 1e12
     kp = next((r for r in prof if r["kernel"] == dominant), None)
     if kp is None or kp["launches"] == 0:
         raise RuntimeError(f"roofline kernel {dominant!r} was not launched in the timed region")
     per_launch_ms = kp["ms"] / kp["launches"]
-    roof_step_ms = ms
     if dominant.startswith(MFMA_KERNELS):
-        peak = BF16_PEAK_TFLOPS if args.dtype == "bf16" else F32_PEAK_TFLOPS
+        peak = peak_mfma
         ach = kp["flops"] / (kp["ms"] * 1e-3) / 1e12
         bound, unit = "mfma", "TFLOP/s"
     else:
@@ -171,12 +259,28 @@ def main():
     roofline = {"bound": bound, "achieved": round(ach, 2), "peak": peak, "unit": unit, "frac": round(ach / peak, 4),
                 "traffic": traffic, "kernel": dominant, "launches_per_step": kp["launches"] / ROOF_STEPS,
                 "avg_launch_us": round(per_launch_ms * 1e3, 2),
-                "share_of_step": round(kp["ms"] / ROOF_STEPS / roof_step_ms, 4),
+                "share_of_step": round(kp["ms"] / ROOF_STEPS / ms, 4),
                 "algorithmic_per_launch": {"flops": kp["flops"] / kp["launches"],
                                            "bytes": kp["bytes"] / kp["launches"]},
-                "timing": f"HIP events on the launch stream around every launch of the kernel, {ROOF_STEPS} steps after the timed region (branches serialised on one stream)"}
+                "timing": f"HIP events on the launch stream around every launch of the kernel, {ROOF_STEPS} forwards "
+                          "after the timed region (branches serialised on one stream)",
+                "step": {"achieved_tflops": round(step_tf, 2), "peak": peak_mfma, "frac": round(step_tf / peak_mfma, 4),
+                         "basis": "essential FLOPs per step (SURVEY.md §8(d): 256.5 GFLOP per segment x 4 stems) / "
+                                  "timed ms per step"}}
     if traffic_src:
         roofline["traffic_source"] = traffic_src
+    if sections:
+        sec = {}
+        for r in sections:
+            if not r["ms"]:
+                continue
+            tf = r["flops"] / (r["ms"] * 1e-3) / 1e12
+            sec[r["kernel"]] = {"ms": round(r["ms"], 3), "tflops": round(tf, 1), "frac_mfma": round(tf / peak_mfma, 4),
+                                "hbm_gbs": round(r["bytes"] / (r["ms"] * 1e-3) / 1e9, 1)}
+        roofline["sections"] = sec
+        roofline["sections_timing"] = ("one forward after the timed region, every kernel bracketed by HIP events "
+                                       "(branches serialised), summed per section; flops / bytes = the kernels' "
+                                       "algorithmic work")
     rec = {
         "metric": "6s-segments/sec (each separated into 4 stems; encode once, decode 4x)",
         "value": round(value, 3),
@@ -189,21 +293,29 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": args.dtype,
-        "data": "synthetic (seeded tones+noise 6 s stereo, seeded random weights of the htdemucs/AudioTextHTDemucs architecture)",
-        "config": {"workload": "BASELINE configs[2]: B=64 x 6 s segments x 4 prompts per GPU", "global_batch": B * world,
-                   "seq_len": SEG, "prompts": 4, "parallelism": f"segment-sharded dp{world}"},
+        "data": "synthetic (64 distinct seeded tones+noise 6 s stereo segments per GPU, seeded random weights of the "
+                "htdemucs/AudioTextHTDemucs architecture)",
+        "config": {"workload": "BASELINE configs[2]: B=64 x 6 s segments x 4 prompts per GPU"
+                               + ("; configs[3] shape: segments sharded over the GPUs, RCCL gather to rank 0 timed"
+                                  if world > 1 else ""),
+                   "global_batch": N, "seq_len": SEG, "prompts": 4, "parallelism": f"segment-sharded dp{world}",
+                   "gather_timed": world > 1},
         "stems_per_s": round(4 * value, 3),
         "roofline": roofline,
         "step_essential_tflops": round(step_tf, 2),
         "workspace_gb": round(model._ws.numel() / 1e9, 2) if model._ws is not None else None,
     }
+    if rank == 0 and not args.no_extras:
+        rec["sdr_db_vs_oracle"] = sdr_vs_oracle(model, sd, table, wav[:1].contiguous())
+        if world == 1 and args.dtype == "bf16":
+            rec["f32"] = f32_line(sd, table, wav)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         rec["cpu_baseline"] = cpu_baseline(sd, table)
     if rank == 0:
         print(json.dumps(rec), flush=True)
     if world > 1:
+        torch.distributed.barrier()
         torch.distributed.destroy_process_group()
-    del out
 
 
 if __name__ == "__main__":

@@ -12,8 +12,10 @@
  * the caller (wav, text embeddings, output, workspace); the context owns the packed weights.  Every call
  * returns 0 on success or a negative athd_status; the message is in athd_last_error().  Nothing is thrown
  * across the ABI.  Work is enqueued on the caller's stream (a hipStream_t passed as void*, NULL = default
- * stream); athd_forward* do not synchronise the host and do not allocate, so they can be captured in a graph.
- * One context per device; calls on one context must be serialised by the caller.
+ * stream); athd_forward* do not synchronise the host and create no memory, streams or events (the time branch's
+ * stream and the fork/join events are made by athd_finalize), so they can be captured in a graph.  One context
+ * per device; calls on one context must be serialised by the caller, even from different streams (the fork/join
+ * events are per context).
  */
 #ifndef ATHD_H
 #define ATHD_H
@@ -60,8 +62,15 @@ const char* athd_required_key(int i);
  * order, ConvTranspose residue split, bf16 conversion) and upload. */
 int athd_finalize(athd_ctx* ctx);
 
+/* (segment, prompt) items the decoder processes per chunk (default 64; 1..4096).  The encoder's buffers scale
+ * with B and the decoder's with this setting: at B = 64, T = 264600 (6 s), P = 4 the workspace is about 18 GB
+ * at 64 items and 51 GB at 256 (the whole batch in one decode chunk: fewer, larger launches, the bench setting).
+ * Takes effect for the next athd_workspace_bytes / athd_forward* calls; the environment variable
+ * ATHD_DECODE_ITEMS overrides it. */
+int athd_set_decode_items(athd_ctx* ctx, int64_t items);
+
 /* Workspace bytes needed by athd_forward (P = 1) / athd_forward_prompts (P prompts) for B segments of
- * T samples. */
+ * T samples (see athd_set_decode_items for the sizes at the bench configuration). */
 size_t athd_workspace_bytes(athd_ctx* ctx, int64_t B, int64_t T, int P);
 
 /* wav: (B,2,T) f32, text_emb: (B,512) f32 -> out: (B,2,T) f32.  == AudioTextHTDemucs.forward(wav, text). */
@@ -86,17 +95,41 @@ int64_t athd_num_windows(int64_t length, int64_t chunk_len, int64_t overlap);
 int athd_overlap_add(const float* windows, int64_t length, int64_t chunk_len, int64_t overlap, int n_stems,
                      int64_t k0, int64_t k1, float* out, void* stream);
 
+/* ---- Track level, benchmark.py protocol (OurModel._chunked_inference, benchmark.py:155-204) ----
+ * Same window starts (hop = chunk_len - overlap, while start < length); every window's model input is zero-padded
+ * to chunk_len, its first len_k = end_k - start_k outputs are used.  fade_len_k = min(overlap, len_k / 2); the
+ * window weight is 1 with linspace(0, 1, fade_len) over its first fade_len samples if start_k > 0 and
+ * linspace(1, 0, fade_len) over its last fade_len samples if end_k < length; output += out_k * w and
+ * weight += w in ascending k, then output / max(weight, 1e-8).
+ * windows: device (k1-k0, n_stems, 2, chunk_len) f32.  weight == NULL: out (n_stems, 2, span) = the normalised
+ * track span of windows [k0, k1) (the track itself for the full range).  weight != NULL (device, span floats):
+ * out = the unnormalised sum and weight = the weight sum of the span, for sharded runs that add spans of window
+ * ranges (the sum over ranks in rank order equals the single-range sum bit for bit) and then normalise with
+ * athd_ola_normalize. */
+int athd_overlap_add_weighted(const float* windows, int64_t length, int64_t chunk_len, int64_t overlap, int n_stems,
+                              int64_t k0, int64_t k1, float* out, float* weight, void* stream);
+/* out (rows, n) /= max(weight (n), 1e-8) in place (benchmark.py:201-202). */
+int athd_ola_normalize(float* out, const float* weight, int rows, int64_t n, void* stream);
+
 /* SDR of src/loss.py:9-30 with the sign of test_inference.py:153: est/target device (rows, n) f32 ->
  * *out (device f32) = mean over rows of clamp(10 log10((sum t^2 + 1e-8) / (sum (t-e)^2 + 1e-8)), -30, 30).
  * scratch: device, 2*rows doubles.  Sums are accumulated in fp64. */
 int athd_sdr(const float* est, const float* target, int64_t rows, int64_t n, double* scratch, float* out,
              void* stream);
 
+/* SI-SDR of src/loss.py:33-68 with the sign of benchmark.py:586: per row, zero-mean est e and target t,
+ * a = <e,t> / (|t|^2 + 1e-8), clamp(10 log10((|a t|^2 + 1e-8) / (|e - a t|^2 + 1e-8)), -30, 30), mean over
+ * rows -> *out (device f32).  scratch: device, 5*rows doubles.  fp64 sums. */
+int athd_sisdr(const float* est, const float* target, int64_t rows, int64_t n, double* scratch, float* out,
+               void* stream);
+
 /* Kernel timing (measurement aid for bench.py; not part of the reference interface).  Between
  * athd_profile_start and athd_profile_stop every launch of kernel `kernel` (its rocprofv3 symbol without
  * "void athd::", the argument list and 'u' suffixes, e.g. "attn_bf16_kernel"; NULL or "" = all kernels) made
  * by this context's forwards is bracketed by HIP events on the launch stream.  athd_profile_stop synchronises
- * those events and aggregates per kernel: launches, summed event time, summed ALGORITHMIC flops and bytes. */
+ * those events and aggregates per kernel: launches, summed event time, summed ALGORITHMIC flops and bytes.
+ * kernel = "@section": every kernel, aggregated per forward section ("encoder", "transformer", "decoder").
+ * While a profile is open the time branch runs on the caller's stream, so each event pair times one kernel. */
 int athd_profile_start(athd_ctx* ctx, const char* kernel);
 int athd_profile_stop(athd_ctx* ctx);
 int athd_profile_count(athd_ctx* ctx);

@@ -1,6 +1,6 @@
 """ORACLE (test infrastructure only) - CPU restatement of `AudioTextHTDemucs.forward`
-(`/root/reference/src/models/stem_separation/ATHTDemucs_v2.py:250-326`) and of the reference's metric
-(`src/loss.py:9-30`) and chunk loop (`test_inference.py:92-141`).
+(`/root/reference/src/models/stem_separation/ATHTDemucs_v2.py:250-326`), of the reference's metrics
+(`src/loss.py:9-68`: SDR, SI-SDR) and of its two chunk loops (`test_inference.py:92-141`; `benchmark.py:155-204`).
 
 Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this module.
 
@@ -242,3 +242,49 @@ def linear_fade(x: torch.Tensor, fade_in: int, fade_out: int) -> torch.Tensor:
     fi = torch.cat((torch.linspace(0, 1, fade_in, dtype=x.dtype), torch.ones(L - fade_in, dtype=x.dtype))).clamp_(0, 1)
     fo = torch.cat((torch.ones(L - fade_out, dtype=x.dtype), -torch.linspace(0, 1, fade_out, dtype=x.dtype) + 1)).clamp_(0, 1)
     return fi * fo * x
+
+
+def sisdr_db(estimated: torch.Tensor, target: torch.Tensor) -> float:
+    """`src/loss.py:33-68` with the sign flipped (benchmark.py:573-588), literally in fp32 torch ops."""
+    est_flat = estimated.reshape(estimated.shape[0], -1).float()
+    tgt_flat = target.reshape(target.shape[0], -1).float()
+    est_flat = est_flat - est_flat.mean(dim=-1, keepdim=True)
+    tgt_flat = tgt_flat - tgt_flat.mean(dim=-1, keepdim=True)
+    dot = torch.sum(est_flat * tgt_flat, dim=-1, keepdim=True)
+    s_target_norm_sq = torch.sum(tgt_flat ** 2, dim=-1, keepdim=True)
+    s_target = (dot / (s_target_norm_sq + 1e-8)) * tgt_flat
+    e_noise = est_flat - s_target
+    sisdr = 10 * torch.log10((torch.sum(s_target ** 2, dim=-1) + 1e-8) / (torch.sum(e_noise ** 2, dim=-1) + 1e-8))
+    return float(torch.clamp(sisdr, min=-30, max=30).mean())
+
+
+def benchmark_chunked_inference(model_fn, mixture: torch.Tensor, sample_rate: int = 44100,
+                                segment_seconds: float = 6.0, overlap: float = 1.5) -> torch.Tensor:
+    """`benchmark.py:155-204` (OurModel._chunked_inference) restated: model_fn((1, C, chunk_len)) -> (1, C, chunk_len).
+    Windows of chunk_len every chunk_len - overlap_frames samples; the last one zero-padded to chunk_len; linspace
+    fades of min(overlap_frames, len // 2) samples; weighted overlap-add normalised by the summed weights."""
+    C, T = mixture.shape
+    chunk_len = int(sample_rate * segment_seconds)
+    overlap_frames = int(overlap * sample_rate)
+    output = torch.zeros(C, T)
+    weight = torch.zeros(T)
+    start = 0
+    while start < T:
+        end = min(start + chunk_len, T)
+        chunk = mixture[:, start:end].unsqueeze(0)
+        if chunk.shape[-1] < chunk_len:
+            chunk = F.pad(chunk, (0, chunk_len - chunk.shape[-1]))
+        out = model_fn(chunk).squeeze(0)
+        actual_len = end - start
+        out = out[:, :actual_len]
+        fade_len = min(overlap_frames, actual_len // 2)
+        chunk_weight = torch.ones(actual_len)
+        if start > 0 and fade_len > 0:
+            chunk_weight[:fade_len] = torch.linspace(0, 1, fade_len)
+        if end < T and fade_len > 0:
+            chunk_weight[-fade_len:] = torch.linspace(1, 0, fade_len)
+        output[:, start:end] += out * chunk_weight
+        weight[start:end] += chunk_weight
+        start += chunk_len - overlap_frames
+    weight = weight.clamp(min=1e-8)
+    return output / weight
