@@ -86,17 +86,24 @@ def test_separate_track_sharded_300s(pg, model_f32, oracle_model, text_table):
     ref = separate_track(model_f32, mix, STEMS)
     assert got.shape == (4, 2, L)
     assert torch.equal(got, ref) or _sdr(ref.cpu().numpy(), got.cpu().numpy()) >= 120.0
-    # sample windows against the oracle forward (encode once, decode 4x on the CPU)
-    ks = [0, 25, 50]
-    res = {}
-    for k in ks:
+    # sample windows against the oracle forward (encode once, decode 4x on the CPU).  Windows whose spectrum has a
+    # bin near the reference mask's singularity (Re z_L ~ -1e-8, tests/test_gpu_parity.py::_phase_cond) are
+    # reported but not gated: there the output depends on the last bits of that STFT bin.
+    from test_gpu_parity import PHASE_COND_MIN, _phase_cond, _report
+    res, cond = {}, {}
+    for k in [0, 25, 50, 12, 37, 49, 1]:
+        if sum(1 for kk in cond if cond[kk] >= PHASE_COND_MIN) >= 3:
+            break
         w = plan[k]
-        win = run_windows(model_f32, mix, plan, STEMS, SEG, k, k + 1).cpu()[0]     # (4, 2, SEG)
         seg = mix[:, w.start:w.end].cpu()[None]
+        cond[k] = _phase_cond(oracle_model.prepare(seg)[0])
+        win = run_windows(model_f32, mix, plan, STEMS, SEG, k, k + 1).cpu()[0]     # (4, 2, SEG)
         o = oracle_model.forward_prompts(seg, torch.as_tensor(text_table))[0]
-        for si in range(4):
-            res[(k, si)] = _sdr(o[si].numpy(), win[si, :, :w.end - w.start].numpy())
-    assert min(res.values()) >= 70.0, res
+        res[k] = min(_sdr(o[si].numpy(), win[si, :, :w.end - w.start].numpy()) for si in range(4))
+    _report("track300s_windows_f32", {str(k): {"sdr_db_min_over_stems": res[k], "phase_cond": cond[k]} for k in res})
+    gated = [k for k in res if cond[k] >= PHASE_COND_MIN]
+    assert len(gated) >= 3, cond
+    assert min(res[k] for k in gated) >= 70.0, (res, cond)
     del got, ref
     torch.cuda.empty_cache()
 

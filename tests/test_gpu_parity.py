@@ -1,8 +1,12 @@
 """Parity of the HIP path (through the C-ABI) against the oracle and the reference's golden fixtures.
 
-Tolerances (stated per north_star's "stated fp32 tolerance (SDR delta reported)"):
-  * f32 mode (exact-f32 MFMA everywhere): SDR(athd vs reference) >= F32_SDR_DB and max|err| <= F32_MAXREL * RMS(ref)
-  * bf16 mode (bf16 MFMA operands, fp32 accumulation and norms): SDR(athd vs reference) >= BF16_SDR_DB
+Tolerances (stated per north_star's "stated fp32 tolerance (SDR delta reported)"), each within ~10-15 dB of the
+value measured on MI355X (profiles/r02_parity_report.json), so that a regression of that size fails:
+  * f32 mode (exact-f32 MFMA everywhere): max|err| <= F32_MAXREL * RMS(ref) (1e-4) and SDR >= 110 dB
+    wherever the input's spectrum keeps away from the reference mask's singularity (_phase_cond); on the reference
+    fixtures, whose spectra do not, per-fixture SDR gates F32_FIXTURE_DB (measured 80 / 98 / 127 dB);
+  * bf16 mode (bf16 MFMA operands, fp32 accumulation and norms): SDR >= BF16_SDR_DB = 40 dB (measured 49-54 dB);
+  * stage-by-stage (f32): SDR >= F32_STAGE_DB = 90 dB per intermediate (measured 103-135 dB).
 SDR here is 10 log10(sum ref^2 / sum (ref - out)^2) over the whole output (`src/loss.py:9-30` without clamp).
 """
 import json
@@ -17,9 +21,12 @@ from conftest import GOLDEN, REPO
 
 pytestmark = pytest.mark.gpu
 
-F32_SDR_DB = 70.0
-F32_MAXREL = 2e-3
-BF16_SDR_DB = 25.0
+F32_SDR_DB = 110.0          # f32, inputs away from the mask singularity (measured 124-127 dB)
+F32_MAXREL = 1e-4
+F32_FIXTURE_DB = {"b1_t44100_vocals": 70.0, "b2_t30000_drums_bass": 85.0, "b1_t1500_other": 110.0}
+F32_6S_DB = {"oracle": 85.0, "fixture": 75.0}   # measured 98.6 / 89.4 dB (phase-singular bins in the fixture)
+F32_STAGE_DB = 90.0
+BF16_SDR_DB = 40.0
 
 REPORT = os.path.join(REPO, "gpurun_out", "parity_report.json")
 
@@ -76,7 +83,9 @@ def test_golden_fixture(models, name, dt):
     rel = float(np.abs(out - ref).max() / np.sqrt(np.mean(ref ** 2)))
     _report(f"{name}/{dt}", {"sdr_db": s, "maxabs_over_rms": rel})
     if dt == "f32":
-        assert s >= F32_SDR_DB and rel <= F32_MAXREL, (s, rel)
+        assert s >= F32_FIXTURE_DB[name], (s, rel)
+        if F32_FIXTURE_DB[name] >= F32_SDR_DB:        # the fixture whose spectrum is away from the singularity
+            assert rel <= F32_MAXREL, rel
     else:
         assert s >= BF16_SDR_DB, s
 
@@ -92,8 +101,10 @@ def test_full_segment_6s(models, oracle_model, text_table, dt):
     ref = oracle_model.forward(wav, torch.as_tensor(text_table[3:4])).numpy()
     s = sdr_db(ref, out)
     _report(f"6s/{dt}", {"sdr_db_vs_oracle": s, "sdr_db_vs_fixture_stride97": s_fix})
-    thr = F32_SDR_DB if dt == "f32" else BF16_SDR_DB
-    assert s >= thr and s_fix >= thr, (s, s_fix)
+    if dt == "f32":
+        assert s >= F32_6S_DB["oracle"] and s_fix >= F32_6S_DB["fixture"], (s, s_fix)
+    else:
+        assert s >= BF16_SDR_DB and s_fix >= BF16_SDR_DB, (s, s_fix)
 
 
 PHASE_COND_MIN = 5e-8
@@ -122,8 +133,12 @@ def test_ragged_length(models, oracle_model, text_table, T):
         out = models[dt](wav.cuda(), "bass").cpu().numpy()
         assert out.shape == ref.shape
         s = sdr_db(ref, out)
-        _report(f"ragged_T{T}/{dt}", {"sdr_db_vs_oracle": s})
-        assert s >= (F32_SDR_DB if dt == "f32" else BF16_SDR_DB), (dt, s)
+        rel = float(np.abs(out - ref).max() / np.sqrt(np.mean(ref.astype(np.float64) ** 2)))
+        _report(f"ragged_T{T}/{dt}", {"sdr_db_vs_oracle": s, "maxabs_over_rms": rel})
+        if dt == "f32":
+            assert s >= F32_SDR_DB and rel <= F32_MAXREL, (s, rel)
+        else:
+            assert s >= BF16_SDR_DB, s
 
 
 def test_forward_prompts_matches_forward(models):
@@ -235,12 +250,12 @@ def test_intermediates_f32(models, oracle_model, text_table, T):
     cmp("freq_wav", cap["freq_wav"].numpy(), out - cap["xt_dec"].numpy())
     cmp("out", ref_out, out)
     _report(f"intermediates_f32_T{T}", res)
-    bad = {k: v for k, v in res.items() if v["sdr_db"] < F32_SDR_DB}
+    bad = {k: v for k, v in res.items() if v["sdr_db"] < F32_STAGE_DB}
     assert not bad, bad
 
 
 SHARP_SCALE = 6.0          # Q and K in-projection rows x6: logits x36, mean max softmax prob ~0.1-0.3 (vs ~0.005)
-SHARP_BF16_SDR_DB = 20.0   # bf16 logit rounding is amplified by the sharpening
+SHARP_BF16_SDR_DB = 35.0   # bf16 logit rounding is amplified by the sharpening (measured 47.6-48.2 dB)
 
 
 def test_sharp_attention_encoder(state_dict, text_table):
@@ -280,4 +295,4 @@ def test_sharp_attention_encoder(state_dict, text_table):
                 res[f"{dt}/{name}"] = sdr_db(ref[name].reshape(-1), got)
     _report("sharp_attention", res)
     for key, v in res.items():
-        assert v >= (F32_SDR_DB if key.startswith("f32") else SHARP_BF16_SDR_DB), res
+        assert v >= (F32_STAGE_DB if key.startswith("f32") else SHARP_BF16_SDR_DB), res
