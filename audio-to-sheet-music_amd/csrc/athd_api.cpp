@@ -263,11 +263,14 @@ int athd_finalize(athd_ctx* c) {
             l.cross = idx % 2 == 1;
             const std::string p = ctp + (br == 0 ? ".layers." : ".layers_t.") + std::to_string(idx);
             const std::string a = p + (l.cross ? ".cross_attn" : ".self_attn");
+            // bf16 mode: the query projection is prescaled by (1/sqrt(64)) * log2(e) so that the attention kernel's
+            // scores come out in log2 units (attn.hip, attn32_kernel); f32 mode keeps the reference weights
+            const float qs = c->mode == 1 ? ATTN_Q_PRESCALE : 1.f;
             if (l.cross) {
-                l.q = c->lin_gemm(a + ".in_proj_weight", a + ".in_proj_bias", 0, 512);
+                l.q = c->lin_gemm(a + ".in_proj_weight", a + ".in_proj_bias", 0, 512, 512, qs);
                 l.kv = c->lin_gemm(a + ".in_proj_weight", a + ".in_proj_bias", 512, 1024);
             } else {
-                l.qkv = c->lin_gemm(a + ".in_proj_weight", a + ".in_proj_bias");
+                l.qkv = c->lin_gemm(a + ".in_proj_weight", a + ".in_proj_bias", 0, -1, 512, qs);
             }
             l.out = c->lin_gemm(a + ".out_proj.weight", a + ".out_proj.bias");
             l.l1 = c->lin_gemm(p + ".linear1.weight", p + ".linear1.bias");

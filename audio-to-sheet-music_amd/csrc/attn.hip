@@ -15,11 +15,11 @@ namespace athd {
 // tiles (bh-major, the ceil(Nq/128) query blocks of one (b, h) consecutive) are cut into 8 contiguous ranges, one
 // per XCD.  All query blocks of a (b, h) then run on one XCD at about the same time and its K / V come from HBM
 // once into that XCD's L2, instead of once per XCD they were spread over.
-ATHD_DEV void attn_tile(const AttnDesc& d, int& qb, int& h, int64_t& b) {
+ATHD_DEV void attn_tile(const AttnDesc& d, int& qb, int& h, int64_t& b, int qblock = 128) {
     const int n = (int)gridDim.x, i = (int)blockIdx.x;
     const int q = n / 8, r = n % 8, x = i % 8;
     const int t = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i / 8;
-    const int gq = (d.Nq + 127) / 128;
+    const int gq = (d.Nq + qblock - 1) / qblock;
     qb = t % gq;
     const int bh = t / gq;
     h = bh % d.heads;
@@ -453,9 +453,274 @@ __global__ __launch_bounds__(256, 3) void attn_bf16_kernel(const AttnDesc d) {
 #undef ATHD_FETCH
 #undef ATHD_STASH
 
+// ----------------------------------------------------------------------------------------------------------------
+// bf16 path on v_mfma_f32_32x32x16_bf16 (prescaled queries: scores are log2-unit logits).
+//
+// Per wave 32 queries, per tile 64 keys.  S^T = K Q^T as two 32x32 blocks (keys x queries): lane l holds query
+// r = l & 31 and keys (reg & 3) + 8 (reg >> 2) + 4 (l >> 5) of each block, so the online softmax is in-lane plus one
+// exchange between the two 32-lane halves.  The accumulators start at -m (the running max) instead of 0, so the MFMA
+// itself subtracts the max: p = exp2(S) is one v_exp_f32 per score.  The max moves only when a tile's scores exceed it
+// by more than ATTN_RESCALE (defer-max; the rescale runs before any of the tile's P is formed).
+//
+// O^T += V^T P^T: for PV k-step kk (16 keys of key block kk >> 1) lane (r, h) feeds its own registers
+// 8 (kk & 1) .. +7 as the B operand, i.e. keys 4h + {0..3} and 4h + 8 + {0..3} of the 16 - the k order inside the step
+// is permuted, and the A operand (V^T) is read in the same permuted order with two ds_read_b64_tr_b16 (rows
+// 4h + q and 4h + 8 + q).  No cross-lane movement of P.  MFMA issue per tile and wave: 8 (QK) + 8 (PV) 32x32x16 =
+// 512 cycles; the 32x32 shape blocks vector issue for 8 of every 32 cycles (vs 8 of 16 for 16x16x32), which leaves
+// room for the 32 exps, the max and the row sums of each lane.
+//
+// LDS: K [key][72] (row reads, conflict-free per 8 lanes), V [key][64] with the 16-B chunk XOR-swizzled by
+// ((key >> 1) & 1) << 2 so that each 32-lane half of a transposed read (4 keys x 32 d) covers all 64 banks.  2-deep
+// ring, register-staged prefetch (issue before the tile's MFMAs, LDS write after), one barrier per tile.  The output
+// tile is staged through LDS and stored as whole 128-B rows.
+typedef __attribute__((ext_vector_type(16))) float f32x16_t;
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4_t;   // (arrays of these stay in registers)
+
+constexpr int A32_KP = 72;                          // K row pitch (bf16)
+constexpr int A32_VP = 64;                          // V row pitch (bf16), swizzled chunks
+
+ATHD_DEV int a32_vchunk(int key, int chunk) { return chunk ^ (((key >> 1) & 1) << 2); }
+
+// value of lane l ^ 32 combined with the lane's own, by v_permlane32_swap (no LDS round trip)
+ATHD_DEV float half_swap_max(float x) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+ATHD_DEV float half_swap_sum(float x) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+// v_max3_f32 without the canonicalising v_max(x, x) that fmaxf puts on MFMA results (inputs are never NaN here)
+ATHD_DEV float vmax3(float a, float b, float c) {
+    float r;
+    asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
+#define ATHD_A32_QK(INIT)                                                                                      \
+    do {                                                                                                       \
+        const float init_ = (INIT);                                                                            \
+        _Pragma("unroll") for (int kb = 0; kb < NKB; ++kb)                                                    \
+            _Pragma("unroll") for (int i = 0; i < 16; ++i) sc[kb][i] = init_;                                  \
+        _Pragma("unroll") for (int ks = 0; ks < 4; ++ks)                                                      \
+            _Pragma("unroll") for (int kb = 0; kb < NKB; ++kb) {                                              \
+                const bf16v8 a_ = *reinterpret_cast<const bf16v8*>(&K_[(32 * kb + r) * A32_KP + 16 * ks + 8 * hh]); \
+                sc[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_, qf[ks], sc[kb], 0, 0, 0);                 \
+            }                                                                                                  \
+        if (kt0 + KT > d.Nk) {                                                                                 \
+            _Pragma("unroll") for (int kb = 0; kb < NKB; ++kb)                                                \
+                _Pragma("unroll") for (int i = 0; i < 16; ++i)                                                 \
+                    if (kt0 + 32 * kb + (i & 3) + 8 * (i >> 2) + 4 * hh >= d.Nk) sc[kb][i] = -INFINITY;        \
+        }                                                                                                      \
+    } while (0)
+template <int MINW, int NKB>
+__global__ __launch_bounds__(256, MINW) void attn32_kernel(const AttnDesc d) {
+    constexpr int KT = 32 * NKB;                                  // keys per tile
+    __shared__ __attribute__((aligned(16))) bf16_t Ks[2][KT * A32_KP];
+    __shared__ __attribute__((aligned(16))) bf16_t Vs[2][KT * A32_VP];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int r = lane & 31, hh = lane >> 5;
+    int qblk, h;
+    int64_t b;
+    attn_tile(d, qblk, h, b);
+    const int qw0 = qblk * 128 + wave * 32;
+    const bool active = qw0 < d.Nq;                               // wave-uniform
+    const int q = min(qw0 + r, d.Nq - 1);                          // rows past Nq compute on a copy, never stored
+
+    // Q^T fragments (B operand): lane (r, h) holds Q[q][16 ks + 8h .. +7]
+    bf16v8 qf[4];
+    {
+        const bf16_t* Qp = (const bf16_t*)d.Q + b * d.q_bs + (int64_t)q * d.q_ld + d.q_off + h * 64 + 8 * hh;
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) qf[ks] = *reinterpret_cast<const bf16v8*>(Qp + 16 * ks);
+    }
+
+    // staging: thread -> keys tid/8 + 32 j, 16-B chunk tid % 8 of the 128-B head row
+    const bf16_t* Kb = (const bf16_t*)d.K + b * d.k_bs + d.k_off + h * 64;
+    const bf16_t* Vb = (const bf16_t*)d.V + b * d.v_bs + d.v_off + h * 64;
+    const int skey = tid >> 3, sch = tid & 7;
+    // staging of tile kt0 into registers kr / vr (fetch) and from them into ring slot st (stash)
+#define ATHD_A32_FETCH(KT0)                                                                                    \
+    _Pragma("unroll") for (int j = 0; j < NKB; ++j) {                                                         \
+        const int ka = min((KT0) + skey + 32 * j, d.Nk - 1);                                                   \
+        kr[j] = *reinterpret_cast<const u32x4_t*>(Kb + (int64_t)ka * d.k_ld + 8 * sch);                         \
+        vr[j] = *reinterpret_cast<const u32x4_t*>(Vb + (int64_t)ka * d.v_ld + 8 * sch);                         \
+    }
+#define ATHD_A32_STASH(ST)                                                                                     \
+    _Pragma("unroll") for (int j = 0; j < NKB; ++j) {                                                         \
+        const int key = skey + 32 * j;                                                                         \
+        *reinterpret_cast<u32x4_t*>(&Ks[ST][key * A32_KP + 8 * sch]) = kr[j];                                    \
+        *reinterpret_cast<u32x4_t*>(&Vs[ST][key * A32_VP + 8 * a32_vchunk(key, sch)]) = vr[j];                   \
+    }
+
+    // transposed-read addresses (elements): lane 4q'+p of 16-lane group g' -> key row 4h + q' (+8, +16 s2, +32 kb),
+    // d columns 32 db + 16 (g' & 1) + 4p
+    const int g16 = lane >> 4, i16 = lane & 15, qr = i16 >> 2, pc = i16 & 3;
+    const int vrow = 4 * hh + qr;                                  // + 16 s2 + 32 kb (+ 8): same (row >> 1) & 1
+    int voff[2];
+#pragma unroll
+    for (int db = 0; db < 2; ++db) {
+        const int col = 32 * db + 16 * (g16 & 1) + 4 * pc;
+        voff[db] = vrow * A32_VP + 8 * a32_vchunk(vrow, col >> 3) + (col & 7);
+    }
+
+    f32x16_t o0, o1;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) { o0[i] = 0.f; o1[i] = 0.f; }
+    float mrun = 0.f, lrun = 0.f;
+
+    const int ntiles = (d.Nk + KT - 1) / KT;
+    {
+        u32x4_t kr[NKB], vr[NKB];
+        ATHD_A32_FETCH(0)
+        ATHD_A32_STASH(0)
+    }
+    __syncthreads();
+    int cur = 0;
+    for (int t = 0; t < ntiles; ++t) {
+        const int kt0 = t * KT;
+        const bool more = t + 1 < ntiles;
+        u32x4_t kr[NKB], vr[NKB];
+        if (more) {
+            ATHD_A32_FETCH(kt0 + KT)
+        }
+        if (active) {
+            const bf16_t* K_ = Ks[cur];
+            const bf16_t* V_ = Vs[cur];
+            // ---- S^T = K Q^T - m ----
+            f32x16_t sc[NKB];
+            // (ATHD_A32_QK: key tail -> scores of keys >= Nk are -inf)
+            ATHD_A32_QK(-mrun);
+            // ---- online softmax (log2 units) ----
+            float mxk[NKB];
+#pragma unroll
+            for (int kb = 0; kb < NKB; ++kb) {                     // independent chains, one per key block
+                float m = vmax3(sc[kb][0], sc[kb][1], sc[kb][2]);
+#pragma unroll
+                for (int i = 3; i < 15; i += 2) m = vmax3(m, sc[kb][i], sc[kb][i + 1]);
+                mxk[kb] = vmax3(m, sc[kb][15], sc[kb][15]);
+            }
+            float mx = mxk[0];
+#pragma unroll
+            for (int kb = 1; kb < NKB; ++kb) mx = vmax3(mx, mxk[kb], mxk[kb]);
+            mx = half_swap_max(mx);
+            // first tile: the max is set; later tiles: it moves only past ATTN_RESCALE.  A move rescales O and l
+            // and recomputes the tile's scores against the new max (S is never modified in place, which keeps the
+            // accumulators in place across the branch)
+            const bool jump = t == 0 || mx > ATTN_RESCALE;
+            if (__any(jump)) {
+                const float dm = jump ? mx : 0.f;
+                const float alpha = t == 0 ? 0.f : __builtin_amdgcn_exp2f(-dm);
+                mrun += dm;
+                lrun *= alpha;
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    o0[i] *= alpha;
+                    o1[i] *= alpha;
+                }
+                ATHD_A32_QK(-mrun);
+            }
+            float ls[NKB];
+#pragma unroll
+            for (int kb = 0; kb < NKB; ++kb) {
+                ls[kb] = 0.f;
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    sc[kb][i] = __builtin_amdgcn_exp2f(sc[kb][i]);
+                    ls[kb] += sc[kb][i];
+                }
+            }
+#pragma unroll
+            for (int kb = 0; kb < NKB; ++kb) lrun += ls[kb];
+            // ---- O^T += V^T P^T ----
+#pragma unroll
+            for (int kk = 0; kk < 2 * NKB; ++kk) {
+                const f32x16_t& sp = sc[kk >> 1];
+                const int j0 = 8 * (kk & 1);
+                const uint32_t w[4] = {pack2bf(sp[j0 + 0], sp[j0 + 1]), pack2bf(sp[j0 + 2], sp[j0 + 3]),
+                                       pack2bf(sp[j0 + 4], sp[j0 + 5]), pack2bf(sp[j0 + 6], sp[j0 + 7])};
+                const bf16v8 pb = __builtin_bit_cast(bf16v8, w);
+                const int rb = (32 * (kk >> 1) + 16 * (kk & 1)) * A32_VP;
+#pragma unroll
+                for (int db = 0; db < 2; ++db) {
+                    const bf16_t* base = &V_[rb + voff[db]];
+                    const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)base);
+                    const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(base + 8 * A32_VP));
+                    const bf16v8 a = __builtin_shufflevector(__builtin_bit_cast(bf16v4, lo),
+                                                             __builtin_bit_cast(bf16v4, hi), 0, 1, 2, 3, 4, 5, 6, 7);
+                    if (db == 0) o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, pb, o0, 0, 0, 0);
+                    else o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, pb, o1, 0, 0, 0);
+                }
+            }
+        }
+        if (more) {
+            ATHD_A32_STASH(cur ^ 1)
+        }
+        __syncthreads();
+        cur ^= 1;
+    }
+    // ---- normalise; stage the wave's 32 x 64 output tile in LDS; store whole 128-B rows ----
+    const float l = half_swap_sum(lrun);
+    const float inv = 1.f / l;
+    bf16_t* stage = &Ks[0][0] + wave * 32 * A32_KP;                // 4 waves x 32 rows x 72 <= 2 x 64 x 72
+    if (active) {
+#pragma unroll
+        for (int db = 0; db < 2; ++db) {
+            const f32x16_t& oo = db ? o1 : o0;
+#pragma unroll
+            for (int g4 = 0; g4 < 4; ++g4) {
+                const int dcol = 32 * db + 8 * g4 + 4 * hh;
+                *reinterpret_cast<uint2*>(&stage[r * A32_KP + dcol]) =
+                    make_uint2(pack2bf(oo[4 * g4] * inv, oo[4 * g4 + 1] * inv),
+                               pack2bf(oo[4 * g4 + 2] * inv, oo[4 * g4 + 3] * inv));
+            }
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);                         // lgkmcnt(0): the wave's own LDS writes landed
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int it = 0; it < 4; ++it) {
+            const int id = it * 64 + lane, row = id >> 3, ch = id & 7;
+            const int qq = qw0 + row;
+            if (qq < d.Nq) {
+                const uint4 v = *reinterpret_cast<const uint4*>(&stage[row * A32_KP + 8 * ch]);
+                *reinterpret_cast<uint4*>((bf16_t*)d.O + b * d.o_bs + (int64_t)qq * d.o_ld + h * 64 + 8 * ch) = v;
+            }
+        }
+    }
+}
+
+#undef ATHD_A32_FETCH
+#undef ATHD_A32_STASH
+#undef ATHD_A32_QK
+
+// kernel choice for the bf16 path: 0 = attn32_kernel<3, 2> (default: 3 waves per SIMD, 64-key tiles), 1 =
+// attn_bf16_kernel (16x16x32, ATHD_ATTN_V1=1), 2 = attn32_kernel<2, 2>, 3 = attn32_kernel<2, 4> (128-key tiles); set
+// by tools/kbench.hip for A/B timing.  Tried and dropped (kbench, B=64, N=2072): a software-pipelined form (QK^T of
+// tile t+1 issued before the softmax of tile t, 3-deep K/V ring: 761 vs 804 TFLOP/s) and 64 queries per wave
+// (256 VGPRs with spills: 757).
+int g_attn_variant = -1;
+static int attn_variant() {
+    if (g_attn_variant < 0) {
+        const char* e = std::getenv("ATHD_ATTN_V1");
+        g_attn_variant = e && *e && *e != '0' ? 1 : 0;
+    }
+    return g_attn_variant;
+}
+
+static bool attn32_ok(const AttnDesc& d, int mode) {
+    return attn_variant() != 1 && mode == 1 && d.q_bf16 && d.k_bf16 && d.v_bf16 && d.o_bf16 &&
+           fabsf(d.scale * 1.4426950408889634f - 1.f) < 1e-6f && d.q_ld % 8 == 0 && d.k_ld % 8 == 0 &&
+           d.v_ld % 8 == 0 && d.o_ld % 8 == 0 && d.q_off % 8 == 0 && d.k_off % 8 == 0 && d.v_off % 8 == 0 &&
+           d.Nq > 0 && d.Nk > 0;
+}
+
 int attn_launch(const AttnDesc& d, int mode, hipStream_t s) {
     if (d.heads * 64 > d.o_ld && d.o_ld != 0) return -2;
-    dim3 grid((unsigned)((d.Nq + 127) / 128) * (unsigned)d.heads * (unsigned)d.nb);   // attn_tile decodes it
+    const bool a32 = attn32_ok(d, mode);
+    const int qblock = 128;
+    dim3 grid((unsigned)((d.Nq + qblock - 1) / qblock) * (unsigned)d.heads * (unsigned)d.nb);   // attn_tile decodes it
     KScope ks(s);
     if (ks.on()) {
         const bool v2 = mode == 1 && d.q_bf16 && d.k_bf16 && d.v_bf16;
@@ -463,9 +728,13 @@ int attn_launch(const AttnDesc& d, int mode, hipStream_t s) {
         const double fl = 4.0 * nh * d.Nq * d.Nk * 64;
         const double by = nh * 64 * (d.Nq * (d.q_bf16 ? 2 : 4) + d.Nk * ((d.k_bf16 ? 2 : 4) + (d.v_bf16 ? 2 : 4)) +
                                      d.Nq * (d.o_bf16 ? 2 : 4));
-        ks.begin(v2 ? std::string("attn_bf16_kernel") : klabel("attn_kernel<%d>", mode), fl, by);
+        ks.begin(a32 ? std::string("attn32_kernel") : v2 ? std::string("attn_bf16_kernel") : klabel("attn_kernel<%d>", mode),
+                 fl, by);
     }
-    if (mode == 1 && d.q_bf16 && d.k_bf16 && d.v_bf16) hipLaunchKernelGGL(attn_bf16_kernel, grid, dim3(256), 0, s, d);
+    if (a32 && attn_variant() == 2) hipLaunchKernelGGL((attn32_kernel<2, 2>), grid, dim3(256), 0, s, d);
+    else if (a32 && attn_variant() == 3) hipLaunchKernelGGL((attn32_kernel<2, 4>), grid, dim3(256), 0, s, d);
+    else if (a32) hipLaunchKernelGGL((attn32_kernel<3, 2>), grid, dim3(256), 0, s, d);
+    else if (mode == 1 && d.q_bf16 && d.k_bf16 && d.v_bf16) hipLaunchKernelGGL(attn_bf16_kernel, grid, dim3(256), 0, s, d);
     else if (mode == 1) hipLaunchKernelGGL(attn_kernel<1>, grid, dim3(256), 0, s, d);
     else hipLaunchKernelGGL(attn_kernel<0>, grid, dim3(256), 0, s, d);
     return (int)hipGetLastError();

@@ -194,13 +194,20 @@ struct athd_ctx {
         for (size_t i = 0; i < v.size(); ++i) o[i] = v[glu_src((int)i, (int)v.size())];
         return o;
     }
-    GemmW lin_gemm(const std::string& wk, const std::string& bk, int row0 = 0, int rows = -1) {
+    // rows [row0, row0 + rows) of a [N][K] linear layer; the first `scaled_rows` of them (weights and bias) times
+    // `scale` (the attention query prescale, see ATTN_Q_PRESCALE)
+    GemmW lin_gemm(const std::string& wk, const std::string& bk, int row0 = 0, int rows = -1, int scaled_rows = 0,
+                   float scale = 1.f) {
         const HostT& w = W(wk);
         int N = (int)w.shape[0], K = (int)w.shape[1];
         if (rows < 0) rows = N - row0;
         std::vector<float> p(w.v.begin() + (size_t)row0 * K, w.v.begin() + (size_t)(row0 + rows) * K);
         const auto& bb = W(bk).v;
         std::vector<float> b(bb.begin() + row0, bb.begin() + row0 + rows);
+        for (int n = 0; n < scaled_rows && n < rows; ++n) {
+            for (int k = 0; k < K; ++k) p[(size_t)n * K + k] *= scale;
+            b[n] *= scale;
+        }
         return up_gemm(p, rows, K, b);
     }
 };

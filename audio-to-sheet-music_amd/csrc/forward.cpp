@@ -427,7 +427,8 @@ void encode(Run& r, const Dims& d, const Bufs& b, const float* wav) {
         void* const sO = tb ? b.Ot : b.O;
         void* const sF1 = tb ? b.F1t : b.F1;
         AttnDesc a;
-        a.nb = (int)B; a.Nq = (int)N; a.Nk = (int)Nk; a.heads = 8; a.scale = 0.125f;
+        a.nb = (int)B; a.Nq = (int)N; a.Nk = (int)Nk; a.heads = 8;
+        a.scale = r.actbf ? ATTN_SCALE_PRESCALED : 0.125f;     // bf16: queries prescaled at pack time (attn.h)
         if (!L.cross) {
             GemmDesc g = r.lin(L.qkv, Hq, ab, (int)B, N, 512);
             g.C = sQKV; g.c_bf16 = ab;

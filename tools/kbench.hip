@@ -7,6 +7,7 @@
 
 using namespace athd;
 namespace athd {
+extern int g_attn_variant;
 int gemm2_launch(const GemmDesc& d, hipStream_t s);
 int gemm3_launch(const GemmDesc& d, hipStream_t s, int variant);
 int gemm4_launch(const GemmDesc& d, hipStream_t s);
@@ -58,9 +59,11 @@ int kb_convt_quad(int variant, int kskip, const void* A, const void* W, const fl
     if (kskip == 3) d.stats = nullptr;      // probe: no statistics
     return gemm3_launch(d, (hipStream_t)stream, variant);
 }
-int kb_attn(const void* qkv, int nb, int N, void* out, void* stream) {
+// variant: 0 = attn32<2>, 1 = attn_bf16 (16x16x32), 2 = attn32<3>; prescaled = Q already x ATTN_Q_PRESCALE
+int kb_attn(int variant, int prescaled, const void* qkv, int nb, int N, void* out, void* stream) {
+    g_attn_variant = variant;
     AttnDesc a;
-    a.nb = nb; a.Nq = N; a.Nk = N; a.heads = 8; a.scale = 0.125f;
+    a.nb = nb; a.Nq = N; a.Nk = N; a.heads = 8; a.scale = prescaled ? ATTN_SCALE_PRESCALED : 0.125f;
     a.Q = qkv; a.q_bf16 = 1; a.q_bs = (int64_t)N * 1536; a.q_ld = 1536; a.q_off = 0;
     a.K = qkv; a.k_bf16 = 1; a.k_bs = (int64_t)N * 1536; a.k_ld = 1536; a.k_off = 512;
     a.V = qkv; a.v_bf16 = 1; a.v_bs = (int64_t)N * 1536; a.v_ld = 1536; a.v_off = 1024;

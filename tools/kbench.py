@@ -110,17 +110,29 @@ def quad_case(nb, H, Wd, Cin, Cout, variants):
     print(f"QUAD nb={nb} H={H} W={Wd} Cin={Cin} Cout={Cout}: " + "  ".join(out), flush=True)
 
 
-def attn_case(B, N):
+def attn_case(B, N, variants=(1, 0, 2, 3)):
     qkv = (torch.randn(B, N, 1536, device="cuda")).to(torch.bfloat16)
+    qkvp = qkv.clone()
+    qkvp[..., :512] = (qkv[..., :512].float() * (0.125 * 1.4426950408889634)).to(torch.bfloat16)
     out = torch.empty(B, N, 512, device="cuda", dtype=torch.bfloat16)
     st = torch.cuda.current_stream().cuda_stream
-    us = timeit(lambda: lib.kb_attn(vp(qkv.data_ptr()), B, N, vp(out.data_ptr()), vp(st)))
     flops = 4.0 * B * 8 * N * N * 64
     q, k, v = qkv.view(B, N, 3, 8, 64).permute(2, 0, 3, 1, 4)
     ref = torch.nn.functional.scaled_dot_product_attention(q, k, v)
-    err = (out.view(B, N, 8, 64).permute(0, 2, 1, 3).float() - ref.float()).abs().max().item()
+    res = []
+    for var in variants:
+        for pre, src in ((0, qkv), (1, qkvp)):
+            if var != 1 and not pre:
+                continue
+            if var == 1 and pre:
+                continue
+            f = lambda: lib.kb_attn(var, pre, vp(src.data_ptr()), B, N, vp(out.data_ptr()), vp(st))
+            out.zero_()
+            us = timeit(f)
+            err = (out.view(B, N, 8, 64).permute(0, 2, 1, 3).float() - ref.float()).abs().max().item()
+            res.append(f"v{var}: {us:8.1f}us {flops / us / 1e6:7.1f}TF err={err:.1e}")
     ust = timeit(lambda: torch.nn.functional.scaled_dot_product_attention(q, k, v))
-    print(f"ATTN B={B} N={N}: athd {us:8.1f}us {flops / us / 1e6:7.1f}TF err={err:.1e} | torch sdpa {ust:8.1f}us {flops / ust / 1e6:7.1f}TF", flush=True)
+    print(f"ATTN B={B} N={N}: " + " | ".join(res) + f" | torch sdpa {ust:8.1f}us {flops / ust / 1e6:7.1f}TF", flush=True)
 
 
 def tr_probe():
@@ -206,9 +218,15 @@ if __name__ == "__main__":
         convt_case(64, 259, 259, 96, 48, (2, 34, 35, 36))
         convt_case(64, 1034, 1, 384, 192, (2, 33, 34, 35))
         sys.exit(0)
+    if "attn1" in sys.argv[1:]:          # one shape, for PMC passes
+        vs = tuple(int(v) for v in os.environ.get("ATTN_VARIANTS", "1,0,2").split(","))
+        attn_case(64, 2072, vs)
+        sys.exit(0)
     if "attn" in sys.argv[1:]:
         attn_case(4, 200)
+        attn_case(2, 67)
         attn_case(64, 2072)
+        attn_case(64, 1034)
         sys.exit(0)
     M = 64 * 2072
     if "persist" in sys.argv[1:]:
