@@ -325,28 +325,40 @@ template <> struct Slice12<false> {
     }
 };
 
-// freq: one wave = (item, d-chunk of FL_DC rows, 16 consecutive w).  Lane l: position w = 16 wt + (l & 15), channel
+// freq: one wave = (item, d-chunk of FT_DC rows, 16 consecutive w).  Lane l: position w = 16 wt + (l & 15), channel
 // group cg = l >> 4.  Per row u the lane forms x[u] at its 12 channels (0.5 act(y[4u+1]) + 0.5 act(y[4u+2]) + skip,
 // dec_merge_kernel's fp32 expression order) and the 6 projections [Am; A0; Ap] x[u] come out of 12 exact-f32
 // v_mfma_f32_16x16x4_f32 (A = the folded weights, rows 0..5, K permuted to channel 12 cg + step; B = x): the row
 // reduction over channels happens in the matrix core and the weights are 12 per-lane constants.
+// Block order (1-D grid, XCD-aware): the P prompts of one segment read the same level-2 skip rows, so the blocks of
+// one region (chunk, 64 w) for the P items of a segment are consecutive in one XCD's dispatch order (block i runs on
+// XCD i % 8) and share those rows through its L2.  The chunk's FO values (16 w x FT_DC rows x 2) are staged in LDS
+// and stored as FT_DC * 8 contiguous bytes per w ([item][w][row][2], the iSTFT's frame-major order) instead of one
+// 8-B store per lane and row.
+constexpr int FT_DC = 32;
+
 template <bool BF>
-__global__ __launch_bounds__(256) void fdec_tail_kernel(const DecLastDesc d) {
-    const int64_t item = blockIdx.y;
-    const int64_t seg = item / d.P;
+__global__ __launch_bounds__(256) void fdec_tail_kernel(const DecLastDesc d, int nreg) {
+    __shared__ __attribute__((aligned(16))) float2 ost[4][16][FT_DC + 1];
+    // 1-D block index -> (segment region g, prompt): XCD x runs regions g = x, x + 8, ... with the P prompts of each
+    // back to back
+    const int L = blockIdx.x, x8 = L & 7, j = L >> 3;
+    const int g = 8 * (j / d.P) + x8, pr = j % d.P;
+    if (g >= nreg * (d.NI / d.P)) return;                    // block-uniform
+    const int64_t seg = g / nreg;
+    const int64_t item = seg * d.P + pr;
     const int H = d.H, W = d.W;
-    const int lane = threadIdx.x & 63;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int nwt = (W + 15) / 16;
-    const int nch = (H + FL_DC - 1) / FL_DC;
-    const int wv = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (wv >= nch * nwt) return;                       // wave-uniform
+    const int nch = (H + FT_DC - 1) / FT_DC;
+    const int wv = (g % nreg) * 4 + wave;
+    if (wv >= nch * nwt) return;                       // wave-uniform (no block-level barrier below)
     const int wt = wv % nwt, c = wv / nwt;
     const int p = lane & 15, cg = lane >> 4;
     const int w = wt * 16 + p;
-    const bool wok = w < W;
-    const int wc = wok ? w : W - 1;                    // clamped: the spare lanes compute a duplicate, never stored
-    const int d0 = c * FL_DC;
-    const int d1 = min(H, d0 + FL_DC);
+    const int wc = w < W ? w : W - 1;                  // clamped: the spare lanes compute a duplicate, never stored
+    const int d0 = c * FT_DC;
+    const int d1 = min(H, d0 + FT_DC);
     float mean, rstd;
     gn_params(d.stats, item, d.gn_count, mean, rstd);
     const int ch0 = 12 * cg;
@@ -363,7 +375,7 @@ __global__ __launch_bounds__(256) void fdec_tail_kernel(const DecLastDesc d) {
     const int64_t g_item = item * (int64_t)(2 * H) * W * DL_C + (int64_t)wc * DL_C + ch0;
     const int64_t sk2 = seg * (int64_t)d.H_skip2 * W * d.C_skip2 + (int64_t)wc * d.C_skip2 + ch0;
     const int64_t sk = seg * d.H_skip * W * d.C_skip;
-    float* fo = d.out + (item * W + wc) * (int64_t)H * 2;
+    float2 (*const os)[FT_DC + 1] = ost[wave];
 
     auto load = [&](int u, Slice12<BF>& r) {
         const LinIdx lj = lin_index(u, d.H_skip2, H);
@@ -411,7 +423,7 @@ __global__ __launch_bounds__(256) void fdec_tail_kernel(const DecLastDesc d) {
             ld_skip4(d.skip, BF, sk + ((int64_t)lj.i1 * W + wc) * d.C_skip, sb);
 #pragma unroll
             for (int q = 0; q < 4; ++q) s4[q] = lj.l0 * sa[q] + lj.l1 * sb[q];
-            if (u > d0 && wok) *reinterpret_cast<float2*>(fo + 2 * (u - 1)) = make_float2(pe0 + ap0, pe1 + ap1);
+            if (u > d0) os[p][u - 1 - d0] = make_float2(pe0 + ap0, pe1 + ap1);
             pe0 = cst[0] + (S[0] * s4[0] + S[1] * s4[1] + S[2] * s4[2] + S[3] * s4[3]) + cr0 + a[2];
             pe1 = cst[1] + (S[4] * s4[0] + S[5] * s4[1] + S[6] * s4[2] + S[7] * s4[3]) + cr1 + a[3];
             cr0 = a[0];
@@ -425,7 +437,16 @@ __global__ __launch_bounds__(256) void fdec_tail_kernel(const DecLastDesc d) {
         q0 = __shfl(a[0], p + 16, 64);
         q1 = __shfl(a[1], p + 16, 64);
     }
-    if (cg == 0 && wok) *reinterpret_cast<float2*>(fo + 2 * (d1 - 1)) = make_float2(pe0 + q0, pe1 + q1);
+    if (cg == 0) os[p][d1 - 1 - d0] = make_float2(pe0 + q0, pe1 + q1);
+    __builtin_amdgcn_s_waitcnt(0xc07f);        // lgkmcnt(0): the wave's staged values landed
+    __builtin_amdgcn_wave_barrier();
+    // store: per w the chunk's rows d0 .. d1 - 1 are contiguous; consecutive lanes take consecutive rows
+    const int nrow = d1 - d0;
+    for (int i = lane; i < 16 * nrow; i += 64) {
+        const int wl = i / nrow, rr = i - wl * nrow;
+        const int ww = wt * 16 + wl;
+        if (ww < W) *reinterpret_cast<float2*>(d.out + ((item * W + ww) * (int64_t)H + d0 + rr) * 2) = os[wl][rr];
+    }
 }
 
 // time (4 H == T): block = (item, TL_IN output rows + 1 halo row each side), row r <-> u = TL_IN bx - 1 + r.
@@ -544,9 +565,13 @@ int fdec_tail_launch(const DecLastDesc& d, hipStream_t s) {
     if (d.g_bf16 != d.skip2_bf16 || d.g_bf16 != d.skip_bf16 || d.g_bf16 != d.fast_gelu ||d.P < 1 || d.NI % d.P != 0 || d.H < 1 || d.W < 1 || d.C_skip < 4 || d.H_skip < 1 || !d.g || !d.stats ||
         d.C_skip2 < DL_C || d.C_skip2 % 8 != 0 || d.H_skip2 < 1)
         return -1;
-    const int nch = (d.H + FL_DC - 1) / FL_DC;
+    const int nch = (d.H + FT_DC - 1) / FT_DC;
     const int waves = nch * ((d.W + 15) / 16);
-    const dim3 grid((unsigned)((waves + 3) / 4), (unsigned)d.NI);
+    const int nreg = (waves + 3) / 4;                  // blocks per item
+    const int64_t nseg = d.NI / d.P;
+    // 8 XCD lanes x ceil(regions / 8) x P prompts (fdec_tail_kernel's block order); spare blocks return at once
+    const int64_t per_x = (nreg * nseg + 7) / 8;
+    const dim3 grid((unsigned)(8 * per_x * d.P));
     KScope ks(s);
     if (ks.on()) {
         // the two kept ConvT rows per output row once, level-2 skip rows (48 channels, 2 per output row) and level-3
@@ -557,8 +582,8 @@ int fdec_tail_launch(const DecLastDesc& d, hipStream_t s) {
                           segs * 2 * d.H * d.W * 4 * es + (double)d.NI * d.H * d.W * 2 * 4;
         ks.begin("fdec_tail_kernel", 0.0, by);
     }
-    if (d.g_bf16) hipLaunchKernelGGL(fdec_tail_kernel<true>, grid, dim3(256), 0, s, d);
-    else hipLaunchKernelGGL(fdec_tail_kernel<false>, grid, dim3(256), 0, s, d);
+    if (d.g_bf16) hipLaunchKernelGGL(fdec_tail_kernel<true>, grid, dim3(256), 0, s, d, nreg);
+    else hipLaunchKernelGGL(fdec_tail_kernel<false>, grid, dim3(256), 0, s, d, nreg);
     return (int)hipGetLastError();
 }
 

@@ -78,7 +78,8 @@ struct Bufs {
     float *U, *Yb, *x_cond, *xt_cond;
     uint16_t* Ub;       // bf16 copy of U (throughput mode: A operand of text.mlp0)
     void* Hm;
-    float *G, *D, *FO, *frames;
+    float *G, *D, *FO;
+    float* ola_part;    // boundary partial sums of the fused iSTFT (spectral.hip)
     void *S, *Z, *Zs;   // freq level 1 re-associated (fdec_lr.hip): per-tap products of the 32 / 8 source rows
     mutable float* xt2 = nullptr;   // time_out(time decoder) of the last decode chunk: D (fused tail) or G (ragged T)
 };
@@ -160,7 +161,7 @@ size_t plan(Arena& ar, const Dims& d, Bufs& b, bool actbf) {
     b.Z = act(NI * 32 * Ts * 8 * DEC_CH[2]);
     b.Zs = act(d.Bc * 8 * Ts * 8 * DEC_CH[2]);
     b.FO = ar.take<float>(NI * Ts * Ts * 2);
-    b.frames = ar.take<float>(NI * Ts * 2 * 4096);
+    b.ola_part = ar.take<float>(istft_ola_part_floats(NI, (int)Ts));
     return ar.off;
 }
 
@@ -589,7 +590,7 @@ void decode_chunk(Run& r, const Dims& d, const Bufs& b, int64_t s0, int64_t Bc, 
     text_attn(b.x_enc + s0 * d.Nf * 384, d.Nf, b.x_cond);
     text_attn(b.xt_enc + s0 * d.Nt * 384, d.Nt, b.xt_cond);
     // fork: the time decoder (below, own Gt / Dt buffers) runs on the second stream beside the frequency decoder and
-    // the iSTFT frames; the branches join before combine_kernel, which reads both
+    // the iSTFT; the branches join before istft_ola_kernel, which reads both
     if (!second_stream(r)) return;
     hipStream_t const s_main = r.s, s_t = serial_branches(r) ? r.s : c->s_time;   // (see encode)
     (void)hipEventRecord(c->ev_f, s_main);
@@ -649,8 +650,6 @@ void decode_chunk(Run& r, const Dims& d, const Bufs& b, int64_t s0, int64_t Bc, 
             r.check(fdec_tail_launch(dl, r.s), "fdec_tail");
         }
     }
-    // ---- mask + iSTFT frames (ATHTDemucs_v2.py:297-310) ----
-    istft_frames_launch(b.FO, NI, (int)Ts, P, b.specT + s0 * 2048 * Ts * 4, c->tw, r.actbf ? nullptr : c->tw64, c->win, b.frames, r.s);
 
     // ---- time decoder (ATHTDemucs_v2.py:125-139, 313-321) ----
     float* xt2 = nullptr;                            // time_out(time decoder) [NI][T][2]
@@ -707,9 +706,13 @@ void decode_chunk(Run& r, const Dims& d, const Bufs& b, int64_t s0, int64_t Bc, 
     (void)hipEventRecord(c->ev_t, s_t);              // join
     (void)hipStreamWaitEvent(s_main, c->ev_t, 0);
     r.s = s_main;
-    // ---- iSTFT overlap-add + denorm + branch sum (ATHTDemucs_v2.py:310-324) ----
+    // ---- mask + iSTFT + overlap-add + denorm + branch sum (ATHTDemucs_v2.py:297-324), one fused pass ----
     b.xt2 = xt2;
-    combine_launch(b.frames, NI, (int)Ts, d.T, c->win2, xt2, b.tnorm_std + 2 * s0, P, out + s0 * P * 2 * d.T, r.s);
+    {
+        KStage kst("istft");
+        istft_ola_launch(b.FO, NI, (int)Ts, P, d.T, b.specT + s0 * 2048 * Ts * 4, c->tw, r.actbf ? nullptr : c->tw64,
+                         c->win, c->win2, xt2, b.tnorm_std + 2 * s0, out + s0 * P * 2 * d.T, b.ola_part, r.s);
+    }
 }
 
 // Debug aid: ATHD_DUMP=<dir> makes the forward synchronise at the end and write the main intermediates of the
@@ -722,7 +725,6 @@ void dump_all(const Dims& d, const Bufs& b, hipStream_t s) {
     struct E { std::string name; const void* p; int64_t n; std::string shape; };
     std::vector<E> es = {
         {"specT", b.specT, B * Ts * 2048 * 4, "B,Ts,2048,4"},
-        {"frames", b.frames, NI * Ts * 2 * 4096, "NI,Ts,2,4096"},
         {"snorm", b.snorm, 2 * B, "B,2"},
         {"tnorm_std", b.tnorm_std, 2 * B, "B,2"},
         {"x_enc", b.x_enc, B * d.Nf * 384, "B,Nf,384"},

@@ -82,8 +82,7 @@ ATHD_DEV constexpr int vq(int q) { return 4 * (q & 3) + (q >> 2); }
 // One LDS exchange: DFT output q of this thread goes to slot dst(q), then v[r] = slot j + 256 r.  `lds` holds
 // FPAD 8-byte words: complex floats, or the real and then the imaginary parts of complex doubles.  Ends synced.
 template <typename R, typename Dst>
-ATHD_DEV void exchange(cx<R> (&v)[16], void* lds, Dst dst) {
-    const int j = threadIdx.x;
+ATHD_DEV void exchange(cx<R> (&v)[16], void* lds, Dst dst, int j) {
     if constexpr (sizeof(R) == 4) {
         cpx* b = reinterpret_cast<cpx*>(lds);
 #pragma unroll
@@ -111,11 +110,11 @@ ATHD_DEV void exchange(cx<R> (&v)[16], void* lds, Dst dst) {
 }
 
 // v[r] = x[threadIdx.x + 256 r] on entry; X[threadIdx.x + 256 q] = v[vq(q)] on exit.  tw[m] = e^{-2 pi i m/4096}.
+// j = threadIdx.x (a parameter so that a caller looping over frames can make it opaque per iteration)
 template <typename R, typename TW>
-ATHD_DEV void fft4096(cx<R> (&v)[16], void* lds, const TW* __restrict__ tw) {
-    const int j = threadIdx.x;
+ATHD_DEV void fft4096(cx<R> (&v)[16], void* lds, const TW* __restrict__ tw, int j) {
     dft16(v);                                                       // Ns = 1: no twiddles
-    exchange(v, lds, [j](int q) { return 16 * j + q; });
+    exchange(v, lds, [j](int q) { return 16 * j + q; }, j);
     {                                                               // Ns = 16
         const int k = j & 15;
 #pragma unroll
@@ -125,7 +124,7 @@ ATHD_DEV void fft4096(cx<R> (&v)[16], void* lds, const TW* __restrict__ tw) {
         }
         dft16(v);
         const int base = (j >> 4) * 256 + k;
-        exchange(v, lds, [base](int q) { return base + 16 * q; });
+        exchange(v, lds, [base](int q) { return base + 16 * q; }, j);
     }
 #pragma unroll
     for (int r = 1; r < 16; ++r) {                                  // Ns = 256
@@ -160,7 +159,7 @@ __global__ __launch_bounds__(256) void stft_kernel(const float* __restrict__ wav
         const float w = win[n];
         v[r] = {(R)(pad_sample(xl, p0 + n, pp) * w), (R)(pad_sample(xr, p0 + n, pp) * w)};
     }
-    fft4096(v, buf, tw);
+    fft4096(v, buf, tw, (int)threadIdx.x);
 #pragma unroll
     for (int q = 0; q < 16; ++q) buf[pidx(threadIdx.x + 256 * q)] = {(float)v[vq(q)].x, (float)v[vq(q)].y};
     __syncthreads();
@@ -248,7 +247,7 @@ __global__ __launch_bounds__(256) void istft_frames_kernel(const float* __restri
         v[r] = {(R)z.x, (R)z.y};
     }
     __syncthreads();
-    fft4096(v, buf, tw);
+    fft4096(v, buf, tw, (int)threadIdx.x);
     float* o = frames + (item * Tspec + t) * 2LL * NFFT;
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
@@ -271,6 +270,213 @@ void istft_frames_launch(const float* fo, int NI, int Tspec, int P, const float*
     else
         hipLaunchKernelGGL((istft_frames_kernel<float, float2>), dim3(Tspec, NI), dim3(256), 0, s, fo, Tspec, P, spec, tw,
                            win, frames);
+}
+
+// ---------------------------------------------------------------------------------------------------------
+// Fused iSTFT: mask + inverse FFT + overlap-add + envelope + time branch, no frame tensor in HBM.
+//
+// OLA coordinates: q = n + 3584 (1536 of _ispec's slice + 2048 of istft's centre); stft frame f covers
+// q in [1024 f, 1024 f + 4096); kept frame t = f - 2 (frames outside [0, Tspec) are the zero padding).  Hop block
+// B = q >> 10 receives frames B-3 .. B.  After fft4096 thread j holds the frame's samples j + 256 q' (q' = 0..15),
+// i.e. offsets o = j + 256 (q' & 3) of the frame's hop h = q' >> 2: every thread owns the same 4 offsets of every hop
+// block, so the overlap-add runs in registers: acc[h] = block f + h, frame f adds its hop h to acc[h] (ascending f,
+// from 0.0f), then block f has all of this workgroup's frames and the ring shifts by one block.
+// Workgroup k of an item runs the IO_G real frames t = IO_G k .. (one inverse FFT per frame, as istft_frames did).
+// Its blocks whose frames all lie in its range are final: divided by the window envelope, the denormalised time
+// branch added, stored (4 coalesced samples x 2 channels per thread).  The 3 blocks at each end of its range also
+// take frames of the neighbouring workgroup: their partial sums go to `part` (head: first 3 blocks, tail: the 3
+// after the last frame) and istft_fix_kernel adds tail(k-1) + head(k) and finishes them.  Workgroup 0's head and
+// the last workgroup's tail only border zero frames and are final in place.
+// Traffic per item: FO + the segment's spectrum (shared by its prompts through L2) + xt2 + out + 48 KB of partials
+// per workgroup, vs a 8.5 MB frame tensor written and read back per item by istft_frames + combine.
+constexpr int IO_G = 32;
+
+ATHD_DEV void ola_finish(int64_t B, int j, const float (&y)[4][2], int64_t T, int nfr, const float* __restrict__ win2,
+                         const float* __restrict__ x2, float mean, float stdv, float* __restrict__ o0,
+                         float* __restrict__ o1) {
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+        const int64_t q = B * HOP + j + 256 * o;
+        const int64_t n = q - 3584;
+        if (n >= 0 && n < T) {
+            const int f_lo = q - NFFT + 1 <= 0 ? 0 : (int)((q - NFFT + 1 + HOP - 1) / HOP);
+            int f_hi = (int)(q / HOP);
+            if (f_hi > nfr - 1) f_hi = nfr - 1;
+            float env = 0.f;
+            for (int ff = f_lo; ff <= f_hi; ++ff) env += win2[(int)(q - (int64_t)ff * HOP)];
+            const float2 x = *reinterpret_cast<const float2*>(x2 + n * 2);
+            o0[n] = y[o][0] / env + (x.x * stdv + mean);
+            o1[n] = y[o][1] / env + (x.y * stdv + mean);
+        }
+    }
+}
+
+// part[item][k][2 (head, tail)][3 blocks][4 offsets i][256 threads][2 channels]
+ATHD_DEV float* ola_part(float* part, int64_t item, int nwg, int k, int side, int blk) {
+    return part + ((((item * nwg + k) * 2 + side) * 3 + blk) * 4) * 256 * 2;
+}
+
+template <typename R, typename TW>
+__global__ __launch_bounds__(256, 3) void istft_ola_kernel(const float* __restrict__ fo, int Tspec, int P, int64_t T,
+                                                           const float* __restrict__ specT, const TW* __restrict__ tw,
+                                                           const float* __restrict__ win,
+                                                           const float* __restrict__ win2,
+                                                           const float* __restrict__ xt2,
+                                                           const float* __restrict__ tnorm, float* __restrict__ out,
+                                                           float* __restrict__ part) {
+    __shared__ cpx buf[FPAD];
+    const int64_t item = blockIdx.y;
+    const int64_t b = item / P;
+    const int k = blockIdx.x, nwg = gridDim.x;
+    const int t0 = k * IO_G, t1 = min(t0 + IO_G, Tspec);
+    const int nfr = Tspec + 4;
+    float acc[4][4][2];
+#pragma unroll
+    for (int h = 0; h < 4; ++h)
+#pragma unroll
+        for (int o = 0; o < 4; ++o) acc[h][o][0] = acc[h][o][1] = 0.f;
+    const float mean = tnorm[2 * b], stdv = tnorm[2 * b + 1];
+    float* o0 = out + (item * 2 + 0) * T;
+    float* o1 = out + (item * 2 + 1) * T;
+    const float* x2 = xt2 + item * T * 2;
+    // the spectrum of the next frame is loaded into registers before the current frame's FFT, so its HBM latency
+    // hides under the FFT (8 x 16 B per thread: bins k = j + 256 i)
+    float4 zs[8];
+    auto load_spec = [&](int t) {
+        const float* S = specT + (b * Tspec + t) * 2048LL * 4;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) zs[i] = *reinterpret_cast<const float4*>(S + (int64_t)(threadIdx.x + 256 * i) * 4);
+    };
+    auto put = [&](int side, int blk, int j) {             // acc[0] -> a partial slot (coalesced 8-B stores)
+        float* pp = ola_part(part, item, nwg, k, side, blk);
+#pragma unroll
+        for (int o = 0; o < 4; ++o) *reinterpret_cast<float2*>(pp + (o * 256 + j) * 2) = make_float2(acc[0][o][0], acc[0][o][1]);
+    };
+    auto shift = [&]() {
+#pragma unroll
+        for (int h = 0; h < 3; ++h)
+#pragma unroll
+            for (int o = 0; o < 4; ++o) {
+                acc[h][o][0] = acc[h + 1][o][0];
+                acc[h][o][1] = acc[h + 1][o][1];
+            }
+#pragma unroll
+        for (int o = 0; o < 4; ++o) acc[3][o][0] = acc[3][o][1] = 0.f;
+    };
+    load_spec(t0);
+#pragma unroll 1
+    for (int t = t0; t < t1; ++t) {
+        // the thread index made opaque per frame: the FFT's frame-invariant address arithmetic (twiddle pointers, LDS
+        // slots) is recomputed each frame instead of being hoisted out of the loop and spilled
+        int j;
+        asm volatile("v_mov_b32 %0, %1" : "=v"(j) : "v"((int)threadIdx.x));
+        // ---- masked, Hermitian-packed spectrum of frame t into LDS (istft_frames_kernel's arithmetic) ----
+        const float* F0 = fo + (item * (int64_t)Tspec + t) * Tspec * 2;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int kb = j + 256 * i;
+            const LinIdx li = lin_index(kb, Tspec, 2048);
+            const float* r0 = F0 + (int64_t)li.i0 * 2;
+            const float* r1 = F0 + (int64_t)li.i1 * 2;
+            const float xd0 = li.l0 * r0[0] + li.l1 * r1[0];
+            const float xd1 = li.l0 * r0[1] + li.l1 * r1[1];
+            const float m0 = sigmoidf_(xd0), m1 = sigmoidf_(xd1);
+            const float4 z = zs[i];
+            const float ms0 = z.x * m0, ms1 = z.y * m1;
+            const float d0 = z.x + 1e-8f, d1 = z.y + 1e-8f;
+            cpx X0 = {ms0 * (z.x / d0), ms0 * (z.y / d0)};
+            cpx X1 = {ms1 * (z.z / d1), ms1 * (z.w / d1)};
+            if (kb == 0) { X0.y = 0.f; X1.y = 0.f; }
+            cpx Zk = {X0.x - X1.y, X0.y + X1.x};
+            buf[pidx(kb)] = {Zk.x, -Zk.y};
+            if (kb > 0) {
+                cpx Zm = {X0.x + X1.y, -X0.y + X1.x};
+                buf[pidx(NFFT - kb)] = {Zm.x, -Zm.y};
+            }
+        }
+        if (j == 0) buf[pidx(2048)] = {0.f, 0.f};
+        if (t + 1 < t1) load_spec(t + 1);                  // next frame's spectrum, in flight during the FFT
+        __syncthreads();
+        cx<R> v[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const cpx z = buf[pidx(j + 256 * r)];
+            v[r] = {(R)z.x, (R)z.y};
+        }
+        __syncthreads();
+        fft4096(v, buf, tw, j);                            // ends synced: buf is free for the next frame
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const float wq = win[j + 256 * q] * (1.f / 64.f);   // (L1-resident 16 KB table)
+            const float x0 = (float)v[vq(q)].x * wq;
+            const float x1 = -(float)v[vq(q)].y * wq;
+            acc[q >> 2][q & 3][0] = acc[q >> 2][q & 3][0] + x0;
+            acc[q >> 2][q & 3][1] = acc[q >> 2][q & 3][1] + x1;
+        }
+        // block f = t + 2 has all of this workgroup's frames
+        const int f = t + 2;
+        if (t - t0 < 3 && k > 0) put(0, t - t0, j);        // head block: also takes workgroup k-1's last frames
+        else ola_finish(f, j, acc[0], T, nfr, win2, x2, mean, stdv, o0, o1);
+        shift();
+    }
+    // tail blocks f_last + 1 .. + 3: final if no real frame follows, else partial
+    const int j = threadIdx.x;
+#pragma unroll
+    for (int h = 0; h < 3; ++h) {
+        if (t1 >= Tspec) ola_finish(t1 + 2 + h, j, acc[0], T, nfr, win2, x2, mean, stdv, o0, o1);
+        else put(1, h, j);
+        shift();
+    }
+}
+
+// boundary blocks: block 2 + IO_G k + h (k = 1 .. nwg-1, h = 0..2) = tail partial of workgroup k-1 + head of k
+__global__ __launch_bounds__(256) void istft_fix_kernel(int Tspec, int P, int64_t T, int nwg,
+                                                        const float* __restrict__ win2, const float* __restrict__ xt2,
+                                                        const float* __restrict__ tnorm, float* __restrict__ out,
+                                                        const float* __restrict__ part) {
+    const int64_t item = blockIdx.y;
+    const int64_t b = item / P;
+    const int k = 1 + blockIdx.x / 3, h = blockIdx.x % 3, j = threadIdx.x;
+    const float* tl = ola_part(const_cast<float*>(part), item, nwg, k - 1, 1, h);
+    const float* hd = ola_part(const_cast<float*>(part), item, nwg, k, 0, h);
+    float y[4][2];
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+        const float2 a = *reinterpret_cast<const float2*>(tl + (o * 256 + j) * 2);
+        const float2 c = *reinterpret_cast<const float2*>(hd + (o * 256 + j) * 2);
+        y[o][0] = a.x + c.x;
+        y[o][1] = a.y + c.y;
+    }
+    ola_finish(2 + (int64_t)IO_G * k + h, j, y, T, Tspec + 4, win2, xt2 + item * T * 2, tnorm[2 * b], tnorm[2 * b + 1],
+               out + (item * 2 + 0) * T, out + (item * 2 + 1) * T);
+}
+
+int istft_ola_nwg(int Tspec) { return (Tspec + IO_G - 1) / IO_G; }
+
+void istft_ola_launch(const float* fo, int NI, int Tspec, int P, int64_t T, const float* spec, const float2* tw,
+                      const double2* tw64, const float* win, const float* win2, const float* xt2, const float* tnorm,
+                      float* out, float* part, hipStream_t s) {
+    const int nwg = istft_ola_nwg(Tspec);
+    {
+        const dim3 grid((unsigned)nwg, (unsigned)NI);
+        KScope ks(s);
+        if (ks.on())
+            ks.begin("istft_ola_kernel", 0.0,
+                     (double)NI * Tspec * Tspec * 2 * 4 + (double)(NI / P) * 2048 * Tspec * 4 * 4 + (double)NI * T * 2 * 4 +
+                         (double)NI * 2 * T * 4);
+        if (tw64)
+            hipLaunchKernelGGL((istft_ola_kernel<double, double2>), grid, dim3(256), 0, s, fo, Tspec, P, T, spec, tw64,
+                               win, win2, xt2, tnorm, out, part);
+        else
+            hipLaunchKernelGGL((istft_ola_kernel<float, float2>), grid, dim3(256), 0, s, fo, Tspec, P, T, spec, tw, win,
+                               win2, xt2, tnorm, out, part);
+    }
+    if (nwg > 1) {
+        const dim3 grid((unsigned)(3 * (nwg - 1)), (unsigned)NI);
+        KScope ks(s);
+        if (ks.on()) ks.begin("istft_fix_kernel", 0.0, (double)NI * (nwg - 1) * 3 * 1024 * 2 * 4 * 4);
+        hipLaunchKernelGGL(istft_fix_kernel, grid, dim3(256), 0, s, Tspec, P, T, nwg, win2, xt2, tnorm, out, part);
+    }
 }
 
 // out[item][c][n] = OLA(frames)/env + xt2[item][n][c] * stdt[b] + meant[b]   (ATHTDemucs_v2.py:310-324; xt2 is

@@ -223,21 +223,6 @@ def test_intermediates_f32(models, oracle_model, text_table, T):
     z = cap["z"]
     spec = torch.view_as_real(z).permute(0, 2, 3, 1, 4).reshape(B, 2048, Ts, 4).numpy()
     cmp("specT", spec.transpose(0, 2, 1, 3), dump["specT"])
-    # iSTFT frames: masked spectrum (ATHTDemucs_v2.py:300-309), Nyquist bin zero (HTDemucs._ispec), inverse real
-    # FFT, periodic Hann window, normalized=True (x sqrt(4096) / 4096 per frame)
-    mag = cap["mag"] if "mag" in cap else None
-    zz = z[:, :2].numpy().astype(np.complex128)
-    mask = cap["mask"].numpy().astype(np.float64)
-    m = np.stack([zz[:, 0].real, zz[:, 0].imag], 1) if mag is None else mag[:, :2].numpy()
-    mz = (m * mask) * (zz / (m + 1e-8))                                   # (NI=B here, 2, 2048, Ts)
-    mz = np.concatenate([mz, np.zeros_like(mz[:, :, :1])], 2)            # Nyquist
-    win = 0.5 - 0.5 * np.cos(2 * np.pi * np.arange(4096) / 4096)
-    fr = np.fft.irfft(mz, n=4096, axis=2) * 64.0 * win[None, None, :, None]   # (B, 2, 4096, Ts)
-    cmp("frames", fr.transpose(0, 3, 1, 2), dump["frames"])
-    if os.environ.get("ATHD_TEST_SAVE"):
-        np.savez(os.path.join(REPO, "gpurun_out", f"frames_T{T}.npz"), ref=fr.transpose(0, 3, 1, 2).astype(np.float32),
-                 got=dump["frames"].reshape(fr.shape[0], fr.shape[3], 2, 4096), mask=mask.astype(np.float32),
-                 fo=dump["FO"], specT=dump["specT"])
     for i in range(4):
         cmp(f"saved{i}", cap["saved"][i].permute(0, 2, 3, 1).numpy(), dump[f"saved{i}"])
         cmp(f"saved_t{i}", cap["saved_t"][i].permute(0, 2, 1).numpy(), dump[f"saved_t{i}"])
