@@ -14,6 +14,8 @@
 // windowed into a frame buffer.  The combine kernel then gathers the <=4 overlapping frames per output sample,
 // divides by the window envelope of ALL le+4 frames (torch.istft), and adds the denormalised time branch after
 // its 1x1 output conv (ATHTDemucs_v2.py:314-324).
+#include <cstdlib>
+
 #include "common.h"
 #include "prof.h"
 #include "kernels.h"
@@ -291,23 +293,39 @@ void istft_frames_launch(const float* fo, int NI, int Tspec, int P, const float*
 // per workgroup, vs a 8.5 MB frame tensor written and read back per item by istft_frames + combine.
 constexpr int IO_G = 32;
 
-ATHD_DEV void ola_finish(int64_t B, int j, const float (&y)[4][2], int64_t T, int nfr, const float* __restrict__ win2,
+// Finish hop block B: out = y / env + denormalised time branch, for the samples of [0, T).  Every block holding an
+// output sample is interior (q = n + 3584 >= 3 HOP, and B <= (T + 3583) / HOP <= Tspec + 3 = nfr - 1 because
+// Tspec = ceil(T / HOP)), i.e. receives all four frames B-3 .. B, so its window envelope (torch.istft: the sum of
+// win^2 over ALL le + 4 frames) is the thread's precomputed `env_in` of its 4 offsets (FAST: the reciprocal).
+template <bool FAST>
+ATHD_DEV void ola_finish(int B, int j, const float (&y)[4][2], int T, const float (&env_in)[4],
                          const float* __restrict__ x2, float mean, float stdv, float* __restrict__ o0,
                          float* __restrict__ o1) {
 #pragma unroll
     for (int o = 0; o < 4; ++o) {
-        const int64_t q = B * HOP + j + 256 * o;
-        const int64_t n = q - 3584;
+        const int n = B * HOP + j + 256 * o - 3584;
         if (n >= 0 && n < T) {
-            const int f_lo = q - NFFT + 1 <= 0 ? 0 : (int)((q - NFFT + 1 + HOP - 1) / HOP);
-            int f_hi = (int)(q / HOP);
-            if (f_hi > nfr - 1) f_hi = nfr - 1;
-            float env = 0.f;
-            for (int ff = f_lo; ff <= f_hi; ++ff) env += win2[(int)(q - (int64_t)ff * HOP)];
-            const float2 x = *reinterpret_cast<const float2*>(x2 + n * 2);
-            o0[n] = y[o][0] / env + (x.x * stdv + mean);
-            o1[n] = y[o][1] / env + (x.y * stdv + mean);
+            const float2 x = *reinterpret_cast<const float2*>(x2 + (int64_t)n * 2);
+            float r0, r1;
+            if constexpr (FAST) {
+                r0 = y[o][0] * env_in[o];
+                r1 = y[o][1] * env_in[o];
+            } else {
+                r0 = y[o][0] / env_in[o];
+                r1 = y[o][1] / env_in[o];
+            }
+            o0[n] = r0 + (x.x * stdv + mean);
+            o1[n] = r1 + (x.y * stdv + mean);
         }
+    }
+}
+
+// interior envelope at offsets j + 256 o of a hop block: frames B-3 .. B in ascending order
+ATHD_DEV void ola_env_in(int j, const float* __restrict__ win2, float (&e)[4]) {
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+        const int q = 3 * HOP + j + 256 * o;
+        e[o] = ((win2[q] + win2[q - HOP]) + win2[q - 2 * HOP]) + win2[q - 3 * HOP];
     }
 }
 
@@ -316,20 +334,38 @@ ATHD_DEV float* ola_part(float* part, int64_t item, int nwg, int k, int side, in
     return part + ((((item * nwg + k) * 2 + side) * 3 + blk) * 4) * 256 * 2;
 }
 
-template <typename R, typename TW>
-__global__ __launch_bounds__(256, 3) void istft_ola_kernel(const float* __restrict__ fo, int Tspec, int P, int64_t T,
+// FAST (R = float, the bf16 throughput mode): the mask's sigmoid and phase division and the envelope division use
+// v_exp / v_rcp (~1 ulp) instead of the IEEE sequences; the f32 parity mode (R = double) keeps them exact.
+template <typename R, typename TW, int MINW>
+__global__ __launch_bounds__(256, MINW) void istft_ola_kernel(const float* __restrict__ fo, int Tspec, int P, int T,
                                                            const float* __restrict__ specT, const TW* __restrict__ tw,
                                                            const float* __restrict__ win,
                                                            const float* __restrict__ win2,
                                                            const float* __restrict__ xt2,
                                                            const float* __restrict__ tnorm, float* __restrict__ out,
-                                                           float* __restrict__ part) {
+                                                           float* __restrict__ part, int nwg, int units) {
+    constexpr bool FAST = sizeof(R) == 4;
     __shared__ cpx buf[FPAD];
-    const int64_t item = blockIdx.y;
-    const int64_t b = item / P;
-    const int k = blockIdx.x, nwg = gridDim.x;
+    __shared__ uint2 ltab[2048];       // resize of the Tspec decoder rows to 2048 bins: {i0 | i1 << 16, l1}
+    // XCD-aware order: workgroup L runs on XCD L % 8; the P prompts of one (segment, frame range) unit are
+    // consecutive on one XCD, so they run together and share the segment's spectrum through that XCD's L2
+    const int L = blockIdx.x, xcd = L & 7, jx = L >> 3;
+    const int u = 8 * (jx / P) + xcd;
+    if (u >= units) return;
+    const int64_t b = u / nwg;
+    const int k = u % nwg;
+    const int64_t item = b * P + jx % P;
     const int t0 = k * IO_G, t1 = min(t0 + IO_G, Tspec);
-    const int nfr = Tspec + 4;
+    for (int kb = threadIdx.x; kb < 2048; kb += 256) {
+        const LinIdx li = lin_index(kb, Tspec, 2048);
+        ltab[kb] = make_uint2((uint32_t)li.i0 | ((uint32_t)li.i1 << 16), __float_as_uint(li.l1));
+    }
+    float env_in[4];                   // interior envelope of this thread's offsets j + 256 o (FAST: reciprocal)
+    ola_env_in(threadIdx.x, win2, env_in);
+    if constexpr (FAST) {
+#pragma unroll
+        for (int o = 0; o < 4; ++o) env_in[o] = __builtin_amdgcn_rcpf(env_in[o]);
+    }
     float acc[4][4][2];
 #pragma unroll
     for (int h = 0; h < 4; ++h)
@@ -364,6 +400,7 @@ __global__ __launch_bounds__(256, 3) void istft_ola_kernel(const float* __restri
         for (int o = 0; o < 4; ++o) acc[3][o][0] = acc[3][o][1] = 0.f;
     };
     load_spec(t0);
+    __syncthreads();                                       // ltab
 #pragma unroll 1
     for (int t = t0; t < t1; ++t) {
         // the thread index made opaque per frame: the FFT's frame-invariant address arithmetic (twiddle pointers, LDS
@@ -375,17 +412,25 @@ __global__ __launch_bounds__(256, 3) void istft_ola_kernel(const float* __restri
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             const int kb = j + 256 * i;
-            const LinIdx li = lin_index(kb, Tspec, 2048);
-            const float* r0 = F0 + (int64_t)li.i0 * 2;
-            const float* r1 = F0 + (int64_t)li.i1 * 2;
-            const float xd0 = li.l0 * r0[0] + li.l1 * r1[0];
-            const float xd1 = li.l0 * r0[1] + li.l1 * r1[1];
-            const float m0 = sigmoidf_(xd0), m1 = sigmoidf_(xd1);
+            const uint2 e = ltab[kb];
+            const float l1 = __uint_as_float(e.y), l0 = 1.f - l1;
+            const float2 ra = *reinterpret_cast<const float2*>(F0 + 2 * (int)(e.x & 0xFFFFu));
+            const float2 rb = *reinterpret_cast<const float2*>(F0 + 2 * (int)(e.x >> 16));
+            const float xd0 = l0 * ra.x + l1 * rb.x;
+            const float xd1 = l0 * ra.y + l1 * rb.y;
+            const float m0 = sigmoid<FAST>(xd0), m1 = sigmoid<FAST>(xd1);
             const float4 z = zs[i];
             const float ms0 = z.x * m0, ms1 = z.y * m1;
             const float d0 = z.x + 1e-8f, d1 = z.y + 1e-8f;
-            cpx X0 = {ms0 * (z.x / d0), ms0 * (z.y / d0)};
-            cpx X1 = {ms1 * (z.z / d1), ms1 * (z.w / d1)};
+            cpx X0, X1;
+            if constexpr (FAST) {
+                const float q0 = __builtin_amdgcn_rcpf(d0), q1 = __builtin_amdgcn_rcpf(d1);
+                X0 = {ms0 * (z.x * q0), ms0 * (z.y * q0)};
+                X1 = {ms1 * (z.z * q1), ms1 * (z.w * q1)};
+            } else {
+                X0 = {ms0 * (z.x / d0), ms0 * (z.y / d0)};
+                X1 = {ms1 * (z.z / d1), ms1 * (z.w / d1)};
+            }
             if (kb == 0) { X0.y = 0.f; X1.y = 0.f; }
             cpx Zk = {X0.x - X1.y, X0.y + X1.x};
             buf[pidx(kb)] = {Zk.x, -Zk.y};
@@ -416,21 +461,22 @@ __global__ __launch_bounds__(256, 3) void istft_ola_kernel(const float* __restri
         // block f = t + 2 has all of this workgroup's frames
         const int f = t + 2;
         if (t - t0 < 3 && k > 0) put(0, t - t0, j);        // head block: also takes workgroup k-1's last frames
-        else ola_finish(f, j, acc[0], T, nfr, win2, x2, mean, stdv, o0, o1);
+        else ola_finish<FAST>(f, j, acc[0], T, env_in, x2, mean, stdv, o0, o1);
         shift();
     }
     // tail blocks f_last + 1 .. + 3: final if no real frame follows, else partial
     const int j = threadIdx.x;
 #pragma unroll
     for (int h = 0; h < 3; ++h) {
-        if (t1 >= Tspec) ola_finish(t1 + 2 + h, j, acc[0], T, nfr, win2, x2, mean, stdv, o0, o1);
+        if (t1 >= Tspec) ola_finish<FAST>(t1 + 2 + h, j, acc[0], T, env_in, x2, mean, stdv, o0, o1);
         else put(1, h, j);
         shift();
     }
 }
 
 // boundary blocks: block 2 + IO_G k + h (k = 1 .. nwg-1, h = 0..2) = tail partial of workgroup k-1 + head of k
-__global__ __launch_bounds__(256) void istft_fix_kernel(int Tspec, int P, int64_t T, int nwg,
+// (exact division by the envelope: the blocks are few, so the f32 parity arithmetic serves both modes)
+__global__ __launch_bounds__(256) void istft_fix_kernel(int Tspec, int P, int T, int nwg,
                                                         const float* __restrict__ win2, const float* __restrict__ xt2,
                                                         const float* __restrict__ tnorm, float* __restrict__ out,
                                                         const float* __restrict__ part) {
@@ -439,7 +485,7 @@ __global__ __launch_bounds__(256) void istft_fix_kernel(int Tspec, int P, int64_
     const int k = 1 + blockIdx.x / 3, h = blockIdx.x % 3, j = threadIdx.x;
     const float* tl = ola_part(const_cast<float*>(part), item, nwg, k - 1, 1, h);
     const float* hd = ola_part(const_cast<float*>(part), item, nwg, k, 0, h);
-    float y[4][2];
+    float y[4][2], env_in[4];
 #pragma unroll
     for (int o = 0; o < 4; ++o) {
         const float2 a = *reinterpret_cast<const float2*>(tl + (o * 256 + j) * 2);
@@ -447,8 +493,9 @@ __global__ __launch_bounds__(256) void istft_fix_kernel(int Tspec, int P, int64_
         y[o][0] = a.x + c.x;
         y[o][1] = a.y + c.y;
     }
-    ola_finish(2 + (int64_t)IO_G * k + h, j, y, T, Tspec + 4, win2, xt2 + item * T * 2, tnorm[2 * b], tnorm[2 * b + 1],
-               out + (item * 2 + 0) * T, out + (item * 2 + 1) * T);
+    ola_env_in(j, win2, env_in);
+    ola_finish<false>(2 + IO_G * k + h, j, y, T, env_in, xt2 + item * (int64_t)T * 2, tnorm[2 * b],
+                      tnorm[2 * b + 1], out + (item * 2 + 0) * T, out + (item * 2 + 1) * T);
 }
 
 int istft_ola_nwg(int Tspec) { return (Tspec + IO_G - 1) / IO_G; }
@@ -458,24 +505,33 @@ void istft_ola_launch(const float* fo, int NI, int Tspec, int P, int64_t T, cons
                       float* out, float* part, hipStream_t s) {
     const int nwg = istft_ola_nwg(Tspec);
     {
-        const dim3 grid((unsigned)nwg, (unsigned)NI);
+        const int units = (NI / P) * nwg;
+        const dim3 grid((unsigned)(8 * ((units + 7) / 8) * P));
         KScope ks(s);
         if (ks.on())
             ks.begin("istft_ola_kernel", 0.0,
                      (double)NI * Tspec * Tspec * 2 * 4 + (double)(NI / P) * 2048 * Tspec * 4 * 4 + (double)NI * T * 2 * 4 +
                          (double)NI * 2 * T * 4);
+        static int minw = -1;
+        if (minw < 0) {
+            const char* e = std::getenv("ATHD_ISTFT_MINW");
+            minw = e && *e == '3' ? 3 : 2;      // 2 waves/SIMD (181 VGPRs, no spill): 1766 vs 1996 us at 3 (60 B spill)
+        }
         if (tw64)
-            hipLaunchKernelGGL((istft_ola_kernel<double, double2>), grid, dim3(256), 0, s, fo, Tspec, P, T, spec, tw64,
-                               win, win2, xt2, tnorm, out, part);
+            hipLaunchKernelGGL((istft_ola_kernel<double, double2, 3>), grid, dim3(256), 0, s, fo, Tspec, P, (int)T, spec,
+                               tw64, win, win2, xt2, tnorm, out, part, nwg, units);
+        else if (minw == 2)
+            hipLaunchKernelGGL((istft_ola_kernel<float, float2, 2>), grid, dim3(256), 0, s, fo, Tspec, P, (int)T, spec, tw,
+                               win, win2, xt2, tnorm, out, part, nwg, units);
         else
-            hipLaunchKernelGGL((istft_ola_kernel<float, float2>), grid, dim3(256), 0, s, fo, Tspec, P, T, spec, tw, win,
-                               win2, xt2, tnorm, out, part);
+            hipLaunchKernelGGL((istft_ola_kernel<float, float2, 3>), grid, dim3(256), 0, s, fo, Tspec, P, (int)T, spec, tw,
+                               win, win2, xt2, tnorm, out, part, nwg, units);
     }
     if (nwg > 1) {
         const dim3 grid((unsigned)(3 * (nwg - 1)), (unsigned)NI);
         KScope ks(s);
         if (ks.on()) ks.begin("istft_fix_kernel", 0.0, (double)NI * (nwg - 1) * 3 * 1024 * 2 * 4 * 4);
-        hipLaunchKernelGGL(istft_fix_kernel, grid, dim3(256), 0, s, Tspec, P, T, nwg, win2, xt2, tnorm, out, part);
+        hipLaunchKernelGGL(istft_fix_kernel, grid, dim3(256), 0, s, Tspec, P, (int)T, nwg, win2, xt2, tnorm, out, part);
     }
 }
 

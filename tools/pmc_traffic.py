@@ -1,6 +1,9 @@
 """HBM traffic per kernel launch from two rocprofv3 PMC passes (FETCH_SIZE and WRITE_SIZE cannot share a pass on
-gfx950: MI355X_MICROARCH.md §rocprofv3 PMC slots).  Per MI355X_MICROARCH.md §HBM, FETCH_SIZE (KiB) reports half
-the bytes of a wide coalesced read on gfx950, so  hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024.
+gfx950: MI355X_MICROARCH.md §rocprofv3 PMC slots).  Per MI355X_MICROARCH.md §HBM, FETCH_SIZE (KiB) reports exactly
+half the bytes of a wide coalesced streaming read (16 B per lane) on gfx950 and is uncalibrated for other widths.
+So the x2 correction is applied only to the kernels whose HBM reads are 16-B-per-lane streams (WIDE_READS: the GEMM
+and attention tile loads, the fused iSTFT's spectrum loads); for the others hbm_bytes_per_launch is the raw
+(FETCH_SIZE + WRITE_SIZE) * 1024 and `fetch_correction` says 1 (uncalibrated width).  Both figures are recorded.
 
     python tools/pmc_traffic.py <fetch_dir> <write_dir> --batch B --dtype bf16 [-o profiles/pmc_traffic.json]
 
@@ -16,6 +19,9 @@ import sys
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from knames import short_name  # noqa: E402
+
+
+WIDE_READS = ("gemm", "attn", "istft_ola")
 
 
 def per_kernel(d, counter):
@@ -51,15 +57,17 @@ def main():
     fe = per_kernel(a.fetch_dir, "FETCH_SIZE")
     wr = per_kernel(a.write_dir, "WRITE_SIZE")
     out = {"batch": a.batch, "dtype": a.dtype,
-           "correction": "hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 per launch (gfx950 FETCH_SIZE halving)",
+           "correction": "hbm_bytes = (c * FETCH_SIZE + WRITE_SIZE) * 1024 per launch; c = 2 for 16-B/lane read "
+                         "streams (gfx950 FETCH_SIZE halving, kernels " + ", ".join(WIDE_READS) + "), else 1",
            "kernels": {}}
     for k in sorted(set(fe) | set(wr)):
         nf, f = fe.get(k, [0, 0.0])
         nw, w = wr.get(k, [0, 0.0])
         fk = f / nf if nf else 0.0
         wk = w / nw if nw else 0.0
-        out["kernels"][k] = {"launches": max(nf, nw), "fetch_kib": fk, "write_kib": wk,
-                             "hbm_bytes_per_launch": (2 * fk + wk) * 1024}
+        c = 2 if k.startswith(WIDE_READS) else 1
+        out["kernels"][k] = {"launches": max(nf, nw), "fetch_kib": fk, "write_kib": wk, "fetch_correction": c,
+                             "hbm_bytes_raw": (fk + wk) * 1024, "hbm_bytes_per_launch": (c * fk + wk) * 1024}
     os.makedirs(os.path.dirname(a.o), exist_ok=True)
     json.dump(out, open(a.o, "w"), indent=1)
     for k, v in sorted(out["kernels"].items(), key=lambda kv: -kv[1]["hbm_bytes_per_launch"] * kv[1]["launches"])[:15]:
