@@ -20,6 +20,8 @@
 //           then the GroupNorm -> GLU -> LayerScale -> residual pass) instead of being kept
 //   rewrite K = C, N = 2C GLU-interleaved, output staged in LDS and stored as one contiguous T x C bf16 row.
 // Throughput (bf16) mode only; T <= 16 * FR_MT_MAX (the forward falls back to the unfused path otherwise).
+#include <cstdlib>
+
 #include "common.h"
 #include "kernels.h"
 #include "prof.h"
@@ -347,6 +349,326 @@ __global__ __launch_bounds__(FR_NT, CIN == 4 ? 3 : 1) void fenc_row_kernel(const
     }
 }
 
+// ---------------------------------------------------------------------------------------------------------
+// Level 0 (Cin = 4 CaC channels, C = 48) as a branch-free kernel.  Same contractions and arithmetic as
+// fenc_row_kernel<4, 48>, restructured for latency:
+//   - a fixed 18-tile (288-position) row: wave w owns channel tile w % 3 and m-tiles w / 3 + 2 i (i < 9), conv3
+//     m-tiles w + 6 i (i < 3); positions >= T are computed and masked with selects instead of per-tile branches
+//     (the data-dependent `mt < MT` / `m < T` branches of the generic kernel cost exec-mask save/restore and
+//     accumulator copies on every tile);
+//   - the input gather is 3 fixed chunks per thread, all six 16-B loads in flight at once;
+//   - weight fragments and per-channel parameters of the next phase are loaded before the barrier that ends the
+//     current one, so their L2 latency overlaps it;
+//   - workgroup sums by DPP row rotations + 4 readlanes (no LDS round trips inside the wave reduction);
+//   - <= 128 VGPRs, so two 6-wave workgroups are always co-resident on a CU whatever their SIMD placement.
+namespace {
+
+constexpr int F0_NT = 18;                 // m-tiles per row
+constexpr int F0_TP = 16 * F0_NT;         // positions per row (T <= 288)
+constexpr int F0_C = 48, F0_H = 6;
+constexpr int F0_XIN_P = 40, F0_XS_P = 56, F0_HS_P = 40;
+
+ATHD_DEV float dpp_row_sum(float v) {     // every lane: the sum over its row of 16 lanes
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));   // quad_perm 1032
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false));   // quad_perm 2301
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x124, 0xF, 0xF, false));  // row_ror 4
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x128, 0xF, 0xF, false));  // row_ror 8
+    return v;
+}
+ATHD_DEV float wave_sum_dpp(float v) {
+    v = dpp_row_sum(v);
+    return (__int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0)) +
+            __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16))) +
+           (__int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32)) +
+            __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48)));
+}
+// workgroup sum of (s1, s2); `red` is a fresh [2][FR_NW] slot per call.  Ends synced.
+ATHD_DEV void block_sum2_dpp(float& s1, float& s2, float* red) {
+    s1 = wave_sum_dpp(s1);
+    s2 = wave_sum_dpp(s2);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        red[w] = s1;
+        red[FR_NW + w] = s2;
+    }
+    __syncthreads();
+    s1 = ((red[0] + red[1]) + (red[2] + red[3])) + (red[4] + red[5]);
+    s2 = ((red[FR_NW + 0] + red[FR_NW + 1]) + (red[FR_NW + 2] + red[FR_NW + 3])) + (red[FR_NW + 4] + red[FR_NW + 5]);
+}
+
+ATHD_DEV float4 ld4f(const float* p) { return *reinterpret_cast<const float4*>(p); }
+// keeps the next m-tile's LDS fragment loads (and the MFMAs fed by them) below this point: without it the scheduler
+// hoists all nine tiles' loads and MFMAs of a pass for ILP and the pass needs ~200 VGPRs
+#define FR_PIN() asm volatile("" ::: "memory")
+#define FR_SCHED() __builtin_amdgcn_sched_barrier(0)      // (no instruction is scheduled across it)
+// the lane index made opaque per phase: per-tile LDS addresses and position masks are recomputed in each phase
+// instead of being computed once and held in registers across the whole kernel (~40 VGPRs)
+// a pointer the compiler cannot see through: loads from it stay in the phase that issues them (weights are
+// otherwise treated as invariant and hoisted into earlier phases, where they occupy registers)
+template <typename T>
+ATHD_DEV const T* launder(const T* p) {
+    uint64_t v = (uint64_t)p;
+    asm volatile("" : "+s"(v));
+    return (const T*)v;
+}
+ATHD_DEV int opaque_lane() {
+    int l;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(l) : "v"((int)(threadIdx.x & 63)));
+    return l;
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(FR_NT, 4) void fenc_row0_kernel(const FencRowDesc d) {
+    constexpr int C = F0_C, H = F0_H, NCT = 3, MTW = 9;
+    __shared__ __attribute__((aligned(16))) bf16_t xin[F0_TP * F0_XIN_P];    // conv input, then the hidden tile
+    __shared__ __attribute__((aligned(16))) bf16_t xs[(F0_TP + 2 * FR_HALO) * F0_XS_P];
+    bf16_t* const hs = xin;
+    __shared__ float red[4][2 * FR_NW];
+
+    const int R = d.B * d.Fout;
+    const int per = (R + 7) / 8;
+    const int r = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
+    if (r >= R) return;
+    const int b = r / d.Fout, f = r % d.Fout;
+    const int T = d.T;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int l15 = lane & 15, l4 = lane >> 4;
+    const int ct = wave % NCT, mg = wave / NCT;
+    const int cb = ct * 16 + 4 * l4;             // first of this lane's 4 x channels
+    const int pa = 32 * ct + 4 * l4;             // packed GLU column of this lane's 'a' values (gate: pa + 16)
+
+    // ---- input gather: chunk c = tid + 384 i -> position c / 4, taps 2 (c % 4), +1 (8 floats = 2 x 16 B)
+    float4 u[3][2];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const int c = tid + FR_NT * i, m = c >> 2, q = c & 3;
+        const int fi = 4 * f - 2 + 2 * q;
+        if (m < T && fi >= 0 && fi + 1 < d.Fin) {
+            const float* p = (const float*)d.in + (((int64_t)b * T + m) * d.Fin + fi) * 4;
+            u[i][0] = ld4f(p);
+            u[i][1] = ld4f(p + 4);
+        } else {
+            u[i][0] = u[i][1] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    }
+    const bf16x8_t wf = ldfrag(d.wc + (int64_t)(ct * 16 + l15) * d.wc_ld + 8 * l4);
+    const float4 bc = ld4f(d.bc + cb);
+    const float sub = d.a_norm[2 * b], rdv = 1.0f / d.a_norm[2 * b + 1];
+    // halo rows of xs (conv3 zero padding); positions >= T are written as zeros by the conv epilogue
+    if (tid < 2 * FR_HALO * F0_XS_P / 8) {
+        const int hr = tid / (F0_XS_P / 8), hc = tid % (F0_XS_P / 8);
+        const int row = hr < FR_HALO ? hr : F0_TP + hr;
+        *reinterpret_cast<uint4*>(&xs[row * F0_XS_P + hc * 8]) = make_uint4(0u, 0u, 0u, 0u);
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const int c = tid + FR_NT * i, m = c >> 2, q = c & 3;
+        const bool ok = m < T && 4 * f - 2 + 2 * q >= 0 && 4 * f - 2 + 2 * q + 1 < d.Fin;
+        const float4 a = u[i][0], e = u[i][1];
+        uint4 v = make_uint4(pack2bf((a.x - sub) * rdv, (a.y - sub) * rdv), pack2bf((a.z - sub) * rdv, (a.w - sub) * rdv),
+                             pack2bf((e.x - sub) * rdv, (e.y - sub) * rdv), pack2bf((e.z - sub) * rdv, (e.w - sub) * rdv));
+        if (!ok) v = make_uint4(0u, 0u, 0u, 0u);
+        *reinterpret_cast<uint4*>(&xin[m * F0_XIN_P + q * 8]) = v;
+    }
+    __syncthreads();
+
+    // ---- conv (8,1)/(4,1)/(2,0): one K-step of 32 + bias + GELU; residual stream xr in registers
+    f32x4_t xr[MTW];
+#pragma unroll
+    for (int i = 0; i < MTW; ++i) {
+        const int mt = mg + 2 * i;
+        if (i % 3 == 0) FR_SCHED();
+        xr[i] = mfma(wf, ldfrag(&xin[(mt * 16 + l15) * F0_XIN_P + 8 * l4]), f32x4_t{0.f, 0.f, 0.f, 0.f});
+    }
+    {
+        const float bcv[4] = {bc.x, bc.y, bc.z, bc.w};
+        const int l15 = opaque_lane() & 15;
+#pragma unroll
+        for (int i = 0; i < MTW; ++i) {
+            const int m = (mg + 2 * i) * 16 + l15;
+            const bool ok = m < T;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) xr[i][q] = ok ? gelu_fast(xr[i][q] + bcv[q]) : 0.f;
+            st4bf(&xs[(FR_HALO + m) * F0_XS_P + cb], xr[i][0], xr[i][1], xr[i][2], xr[i][3]);
+        }
+    }
+    __syncthreads();
+    // the conv input is dead: zero the hidden tile's K padding columns 16..31
+    for (int i = tid; i < F0_TP * 2; i += FR_NT)
+        *reinterpret_cast<uint4*>(&hs[(i >> 1) * F0_HS_P + 16 + 8 * (i & 1)]) = make_uint4(0u, 0u, 0u, 0u);
+
+    // ---- DConv: x += LayerScale(GLU(GN(1x1(GELU(GN(conv3(x)))))))
+#pragma unroll 1
+    for (int dd = 0; dd < 2; ++dd) {
+        const int dil = 1 << dd;
+        const int l15 = opaque_lane() & 15;
+        f32x4_t ha[3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) ha[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < 5; ++ks) {
+            const int k0 = ks * 32 + 8 * l4;
+            const int tap = k0 / C, c0 = k0 - tap * C;
+            const bool kok = k0 < 3 * C;
+            FR_SCHED();
+            // (rows >= H and k >= 3C are zero in the packed matrix)
+            const bf16x8_t w3f = ldfrag(d.w3[dd] + (int64_t)l15 * d.w3_ld + k0);
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+                const int mt = wave + FR_NW * i;
+                bf16x8_t xf = ldfrag(&xs[(FR_HALO + mt * 16 + l15 + (kok ? (tap - 1) * dil : 0)) * F0_XS_P + (kok ? c0 : 0)]);
+                if (!kok) xf = bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+                ha[i] = mfma(w3f, xf, ha[i]);
+            }
+        }
+        float hb[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) hb[q] = d.b3[dd][min(4 * l4 + q, H - 1)];
+        const bf16x8_t wa = ldfrag(d.w1[dd] + (int64_t)(32 * ct + l15) * d.w1_ld + 8 * l4);
+        const bf16x8_t wg = ldfrag(d.w1[dd] + (int64_t)(32 * ct + 16 + l15) * d.w1_ld + 8 * l4);
+        const float4 ba = ld4f(d.b1[dd] + pa), bg = ld4f(d.b1[dd] + pa + 16);
+        float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            const bool ok = (wave + FR_NW * i) * 16 + l15 < T;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float v = ha[i][q] + hb[q];
+                const bool use = ok && 4 * l4 + q < H;
+                s1 += use ? v : 0.f;
+                s2 += use ? v * v : 0.f;
+            }
+        }
+        float g1w[4], g1b[4];             // (issued before the reduction's barrier)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            g1w[q] = d.g1w[dd][min(4 * l4 + q, H - 1)];
+            g1b[q] = d.g1b[dd][min(4 * l4 + q, H - 1)];
+        }
+        block_sum2_dpp(s1, s2, red[2 * dd]);
+        float hm, hr;
+        gn_from_sums(s1, s2, (float)(H * T), hm, hr);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            const int mt = wave + FR_NW * i;
+            float g[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float v = gelu_fast((ha[i][q] + hb[q] - hm) * hr * g1w[q] + g1b[q]);
+                g[q] = 4 * l4 + q < H ? v : 0.f;
+            }
+            st4bf(&hs[(mt * 16 + l15) * F0_HS_P + 4 * l4], g[0], g[1], g[2], g[3]);
+        }
+        __syncthreads();
+
+        // 1x1 (H -> 2C), GLU-interleaved rows; pass 1: GroupNorm statistics
+        const float bav[4] = {ba.x, ba.y, ba.z, ba.w}, bgv[4] = {bg.x, bg.y, bg.z, bg.w};
+        const int l15b = opaque_lane() & 15;
+        s1 = 0.f;
+        s2 = 0.f;
+#pragma unroll
+        for (int i = 0; i < MTW; ++i) {
+            const int mt = mg + 2 * i;
+            FR_SCHED();
+            const bf16x8_t hf = ldfrag(&hs[(mt * 16 + l15b) * F0_HS_P + 8 * l4]);
+            const f32x4_t z = f32x4_t{0.f, 0.f, 0.f, 0.f};
+            const f32x4_t ya = mfma(wa, hf, z), yg = mfma(wg, hf, z);
+            const bool ok = mt * 16 + l15b < T;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float a = ya[q] + bav[q], g = yg[q] + bgv[q];
+                s1 += ok ? a + g : 0.f;
+                s2 += ok ? a * a + g * g : 0.f;
+            }
+        }
+        const float4 gwa = ld4f(d.g2w[dd] + pa), gba = ld4f(d.g2b[dd] + pa);
+        const float4 gwg = ld4f(d.g2w[dd] + pa + 16), gbg = ld4f(d.g2b[dd] + pa + 16);
+        const float4 sc4 = ld4f(d.scale[dd] + cb);
+        block_sum2_dpp(s1, s2, red[2 * dd + 1]);
+        float ym, yr;
+        gn_from_sums(s1, s2, (float)(2 * C * T), ym, yr);
+        // (y + b - mean) * rstd * w + beta  as  y * wa + ca  (wa = rstd w, ca = (b - mean) wa + beta)
+        const float gwav[4] = {gwa.x * yr, gwa.y * yr, gwa.z * yr, gwa.w * yr};
+        const float gwgv[4] = {gwg.x * yr, gwg.y * yr, gwg.z * yr, gwg.w * yr};
+        const float cav[4] = {(bav[0] - ym) * gwav[0] + gba.x, (bav[1] - ym) * gwav[1] + gba.y,
+                              (bav[2] - ym) * gwav[2] + gba.z, (bav[3] - ym) * gwav[3] + gba.w};
+        const float cgv[4] = {(bgv[0] - ym) * gwgv[0] + gbg.x, (bgv[1] - ym) * gwgv[1] + gbg.y,
+                              (bgv[2] - ym) * gwgv[2] + gbg.z, (bgv[3] - ym) * gwgv[3] + gbg.w};
+        const float scv[4] = {sc4.x, sc4.y, sc4.z, sc4.w};
+        // pass 2: GroupNorm -> GLU -> LayerScale -> residual
+        const int l15c = opaque_lane() & 15;
+#pragma unroll
+        for (int i = 0; i < MTW; ++i) {
+            const int mt = mg + 2 * i;
+            const int m = mt * 16 + l15c;
+            FR_SCHED();
+            const bf16x8_t hf = ldfrag(&hs[m * F0_HS_P + 8 * l4]);
+            const f32x4_t z = f32x4_t{0.f, 0.f, 0.f, 0.f};
+            const f32x4_t ya = mfma(wa, hf, z), yg = mfma(wg, hf, z);
+            const bool ok = m < T;                // positions >= T stay 0 in xr and xs
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float a = ya[q] * gwav[q] + cav[q];
+                const float g = yg[q] * gwgv[q] + cgv[q];
+                const float nx = xr[i][q] + scv[q] * (a * sigmoid_fast(g));
+                xr[i][q] = ok ? nx : 0.f;
+            }
+            st4bf(&xs[(FR_HALO + m) * F0_XS_P + cb], xr[i][0], xr[i][1], xr[i][2], xr[i][3]);
+        }
+        __syncthreads();
+    }
+
+    // ---- rewrite 1x1 (C -> 2C) + GLU + freq embedding
+    {
+        const float* br = launder(d.br);
+        const uint16_t* wr = launder(d.wr);
+        const float4 ba = ld4f(br + pa), bg = ld4f(br + pa + 16);
+        float4 ra = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (d.row_add) ra = ld4f(launder(d.row_add) + (int64_t)f * C + cb);
+        bf16x8_t wa[2], wg[2];
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            wa[ks] = ldfrag(wr + (int64_t)(32 * ct + l15) * d.wr_ld + ks * 32 + 8 * l4);
+            wg[ks] = ldfrag(wr + (int64_t)(32 * ct + 16 + l15) * d.wr_ld + ks * 32 + 8 * l4);
+        }
+        const float bav[4] = {ba.x, ba.y, ba.z, ba.w}, bgv[4] = {bg.x, bg.y, bg.z, bg.w};
+        const float rav[4] = {ra.x, ra.y, ra.z, ra.w};
+        uint2 ov[MTW];
+        const int l15 = opaque_lane() & 15;
+#pragma unroll
+        for (int i = 0; i < MTW; ++i) {
+            const int m = (mg + 2 * i) * 16 + l15;
+            FR_PIN();
+            f32x4_t za = f32x4_t{0.f, 0.f, 0.f, 0.f}, zg = za;
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) {
+                const int k0 = ks * 32 + 8 * l4;
+                bf16x8_t xf = ldfrag(&xs[(FR_HALO + m) * F0_XS_P + (k0 < C ? k0 : 0)]);
+                if (k0 >= C) xf = bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+                za = mfma(wa[ks], xf, za);
+                zg = mfma(wg[ks], xf, zg);
+            }
+            float o[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) o[q] = (za[q] + bav[q]) * sigmoid_fast(zg[q] + bgv[q]) + rav[q];
+            ov[i] = make_uint2(pack2bf(o[0], o[1]), pack2bf(o[2], o[3]));
+        }
+        __syncthreads();         // every wave has read xs: stage the output row [T][C] there
+        bf16_t* ob = xs;
+#pragma unroll
+        for (int i = 0; i < MTW; ++i) {
+            const int m = (mg + 2 * i) * 16 + l15;
+            if (m < T) *reinterpret_cast<uint2*>(&ob[m * C + cb]) = ov[i];
+        }
+        __syncthreads();
+        bf16_t* dst = d.out + ((int64_t)b * d.Fout + f) * (int64_t)T * C;
+        for (int i = tid; i < T * C / 8; i += FR_NT)
+            reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(ob)[i];
+    }
+}
+
 bool fenc_row_supported(int cin, int c, int T) {
     return ((cin == 4 && c == 48) || (cin == 48 && c == 96)) && T >= 1 && T <= 16 * FR_MT_MAX;
 }
@@ -362,9 +684,15 @@ int fenc_row_launch(const FencRowDesc& d, int cin, int c, hipStream_t s) {
         const double H = c / 8.0;
         const double macs = rows * T * (c * 8.0 * cin + 2 * (H * 3 * c + 2.0 * c * H) + 2.0 * c * c);
         const double in_b = cin == 4 ? (double)d.B * d.Fin * T * 4 * 4 : (double)d.B * d.Fin * T * cin * 2;
-        ks.begin(klabel("fenc_row_kernel<%d,%d>", cin, c), 2.0 * macs, in_b + rows * T * c * 2);
+        ks.begin(cin == 4 ? "fenc_row0_kernel" : klabel("fenc_row_kernel<%d,%d>", cin, c), 2.0 * macs, in_b + rows * T * c * 2);
     }
-    if (cin == 4) hipLaunchKernelGGL((fenc_row_kernel<4, 48>), grid, dim3(FR_NT), 0, s, d);
+    static int v1 = -1;
+    if (v1 < 0) {
+        const char* e = std::getenv("ATHD_FENC_V1");
+        v1 = e && *e && *e != '0' ? 1 : 0;
+    }
+    if (cin == 4 && !v1 && d.T <= F0_TP) hipLaunchKernelGGL(fenc_row0_kernel, grid, dim3(FR_NT), 0, s, d);
+    else if (cin == 4) hipLaunchKernelGGL((fenc_row_kernel<4, 48>), grid, dim3(FR_NT), 0, s, d);
     else hipLaunchKernelGGL((fenc_row_kernel<48, 96>), grid, dim3(FR_NT), 0, s, d);
     return (int)hipGetLastError();
 }
