@@ -15,6 +15,7 @@
 //   fdec_lr_merge_kernel: rows 4d+1, 4d+2 (the only rows the exact /4 bilinear resize reads) -> GN -> GELU ->
 //                         lerp -> + 0.1 * resize_H(skip2) -> D1 [item][d][w][Co].
 #include <algorithm>
+#include <cstdlib>
 
 #include "common.h"
 #include "kernels.h"
@@ -49,6 +50,21 @@ ATHD_DEV f2 gelu2(f2 x) {
         return (f2){gelu_fast(x.x), gelu_fast(x.y)};
     }
 }
+
+// packed tanh-form GELU: the arithmetic of common.h::gelu_fast on both lanes of the pair (the polynomial and the
+// scaling as v_pk ops, the exp2 / rcp per lane)
+ATHD_DEV f2 gelu2_pk(f2 x) {
+    const f2 u = x * pfma(splat(0.044715f * 1.5957691216057308f), x * x, splat(1.5957691216057308f));
+    const f2 t = u * splat(-1.4426950408889634f);
+    const f2 den = (f2){__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)} + splat(1.0f);
+    return x * (f2){__builtin_amdgcn_rcpf(den.x), __builtin_amdgcn_rcpf(den.y)};
+}
+
+// rows i0, i1 of a [H][W][8 Co] tap matrix at the thread's (w, channel pair): r0 = scale row[i0], dr = scale (row[i1] -
+// row[i0]) for the NT tap slots (tap_of); i0 / i1 are wave-uniform (scalar offsets)
+template <typename ZT, int NT>
+ATHD_DEV void load_rows(const ZT* base, int64_t rowpitch, int Co, int i0, int i1, float scale, f2 (&r0)[NT],
+                        f2 (&dr)[NT]);
 
 // Per-step resize indices of lin_index(v, in, Hd), tabulated once per block in LDS for v < LR_TAB.
 constexpr int LR_TAB = 1024;
@@ -87,6 +103,21 @@ ATHD_DEV Lerp lr_get(const LrTab* t, int v, int in, int out) {
 // tap index of slot t: all 8 taps (stats pass) or {0, 3, 4, 7} (merge pass: rows 4d+1, 4d+2)
 template <int NT>
 ATHD_DEV constexpr int tap_of(int t) { return NT == 8 ? t : (t == 0 ? 0 : t == 1 ? 3 : t == 2 ? 4 : 7); }
+
+template <typename ZT, int NT>
+ATHD_DEV void load_rows(const ZT* base, int64_t rowpitch, int Co, int i0, int i1, float scale, f2 (&r0)[NT],
+                        f2 (&dr)[NT]) {
+    f2 a[NT], b[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) a[t] = ld2(base + (int64_t)i0 * rowpitch + tap_of<NT>(t) * Co);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) b[t] = ld2(base + (int64_t)i1 * rowpitch + tap_of<NT>(t) * Co);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        r0[t] = a[t] * splat(scale);
+        dr[t] = (b[t] - a[t]) * splat(scale);
+    }
+}
 
 // The two rows (i0, i1) one lerp reads: r0 = scale * row[i0], dr = scale * (row[i1] - row[i0]) per tap slot, so the
 // lerp is fma(l1, dr, r0) (same value as l0 * a + l1 * b up to rounding; l0 = 1 - l1).
@@ -284,6 +315,230 @@ __global__ __launch_bounds__(256) void fdec_lr_merge_kernel(const LowRankDesc d)
     }
 }
 
+
+// ---------------------------------------------------------------------------------------------------------
+// v2 passes: the same arithmetic as fdec_lr_stats_kernel / fdec_lr_merge_kernel, with the per-step resize lerps and
+// row-change flags read from a step table in global memory (fdec_lr_steps_kernel, once per forward): the step index
+// is wave-uniform, so the entry arrives through scalar loads and the lerp weights feed the packed FMAs as SGPR
+// operands.  This removes the per-step LDS lookups, readfirstlanes and row-index compares (about half the VALU
+// instructions of a step in v1, where both passes are VALU-bound), and the GELU pair runs packed.
+// step entry v through the constant address space: the index is wave-uniform, so this is a scalar load (through a
+// generic pointer the compiler may use a vector load, which the step then waits on)
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(4))) const u32x4_t c_u32x4;
+ATHD_DEV LrStep lr_step(const LrStep* steps, int v) {
+    static_assert(sizeof(LrStep) == 32, "LrStep layout");
+    const c_u32x4* p = (const c_u32x4*)steps + 2 * __builtin_amdgcn_readfirstlane(v);
+    const u32x4_t a = p[0], b = p[1];
+    LrStep e;
+    e.lz = __uint_as_float(a.x);
+    e.lk = __uint_as_float(a.y);
+    e.lj = __uint_as_float(a.z);
+    e.zk = a.w;
+    e.jj = b.x;
+    e.flags = b.y;
+    return e;
+}
+
+__global__ __launch_bounds__(256) void fdec_lr_steps_kernel(LrStep* steps, int Hd, int Hs, int Hk, int H_skip) {
+    for (int v = threadIdx.x; v <= Hd; v += blockDim.x) {
+        LrStep e = {};
+        int z0 = -1, z1 = -1, k0 = -1, k1 = -1, j0 = -1, j1 = -1, pz0 = -2, pz1 = -2, pk0 = -2, pk1 = -2, pj0 = -2,
+            pj1 = -2;
+        if (v < Hd) {
+            const LinIdx a = lin_index(v, Hs, Hd), k = lin_index(v, Hk, Hd);
+            z0 = a.i0; z1 = a.i1; k0 = k.i0; k1 = k.i1;
+            e.lz = a.l1;
+            e.lk = k.l1;
+        }
+        if (v >= 1) {
+            const LinIdx j = lin_index(v - 1, H_skip, Hd);
+            j0 = j.i0; j1 = j.i1;
+            e.lj = j.l1;
+            if (v - 1 < Hd) {
+                const LinIdx pa = lin_index(v - 1, Hs, Hd), pk = lin_index(v - 1, Hk, Hd);
+                pz0 = pa.i0; pz1 = pa.i1; pk0 = pk.i0; pk1 = pk.i1;
+            }
+            if (v >= 2) {
+                const LinIdx pj = lin_index(v - 2, H_skip, Hd);
+                pj0 = pj.i0; pj1 = pj.i1;
+            }
+        }
+        e.zk = (uint32_t)(z0 & 0xFF) | (uint32_t)(z1 & 0xFF) << 8 | (uint32_t)(k0 & 0xFF) << 16 | (uint32_t)(k1 & 0xFF) << 24;
+        e.jj = (uint32_t)(j0 & 0xFFFF) | (uint32_t)(j1 & 0xFFFF) << 16;
+        e.flags = (v < Hd && (z0 != pz0 || z1 != pz1) ? 1u : 0u) | (v < Hd && (k0 != pk0 || k1 != pk1) ? 2u : 0u) |
+                  (v >= 1 && (j0 != pj0 || j1 != pj1) ? 4u : 0u);
+        steps[v] = e;
+    }
+}
+
+template <typename ZT>
+__global__ __launch_bounds__(256) void fdec_lr_stats2_kernel(const LowRankDesc d) {
+    const LrThread th = lr_thread(d);
+    const int N8 = 8 * d.Co;
+    const int64_t rp = (int64_t)d.W * N8;
+    const ZT* zb = (const ZT*)d.Z + (int64_t)th.item * d.Hs * rp + (int64_t)th.w * N8 + th.c;
+    const ZT* sb = (const ZT*)d.Zs + (int64_t)th.seg * d.Hk * rp + (int64_t)th.w * N8 + th.c;
+    const f2 bias = ld2(d.bias + th.c);
+    f2 zr0[8], zdr[8], sr0[8], sdr[8];
+    f2 base[8];                // r0(Z) + r0(Zs) (+ bias on taps 2..5: every output row has exactly one of those)
+    f2 prev[4] = {};           // T_{v-1}[4..7]
+    double s1 = 0.0, s2 = 0.0;
+    LrStep nx = lr_step(d.steps, 0);
+    if (th.active) {
+        for (int v0 = 0; v0 <= d.Hd; v0 += 16) {
+            f2 a1 = {}, a2 = {};
+            const int v1 = min(v0 + 16, d.Hd + 1);
+            for (int v = v0; v < v1; ++v) {
+                f2 T[8];
+                const LrStep st = nx;             // the next step's entry is in flight during this step
+                if (v < d.Hd) nx = lr_step(d.steps, v + 1);
+                if (v < d.Hd) {
+                    if (st.flags & 3u) {
+                        if (st.flags & 1u)
+                            load_rows<ZT, 8>(zb, rp, d.Co, st.zk & 0xFF, (st.zk >> 8) & 0xFF, 1.0f, zr0, zdr);
+                        if (st.flags & 2u)
+                            load_rows<ZT, 8>(sb, rp, d.Co, (st.zk >> 16) & 0xFF, st.zk >> 24, 0.1f, sr0, sdr);
+#pragma unroll
+                        for (int t = 0; t < 8; ++t) base[t] = zr0[t] + sr0[t] + ((t >= 2 && t <= 5) ? bias : f2{});
+                    }
+#pragma unroll
+                    for (int t = 0; t < 8; ++t) T[t] = pfma(splat(st.lz), zdr[t], pfma(splat(st.lk), sdr[t], base[t]));
+                } else {
+#pragma unroll
+                    for (int t = 0; t < 8; ++t) T[t] = f2{};
+                }
+                if (v >= 1) {          // rows 4(v-1)+2, 4(v-1)+3
+                    const f2 y2 = prev[0] + T[0];
+                    const f2 y3 = prev[1] + T[1];
+                    a1 += y2 + y3;
+                    a2 = pfma(y2, y2, pfma(y3, y3, a2));
+                }
+                if (v < d.Hd) {        // rows 4v, 4v+1
+                    const f2 y0 = T[2] + prev[2];
+                    const f2 y1 = T[3] + prev[3];
+                    a1 += y0 + y1;
+                    a2 = pfma(y0, y0, pfma(y1, y1, a2));
+                }
+#pragma unroll
+                for (int t = 0; t < 4; ++t) prev[t] = T[4 + t];
+            }
+            s1 += (double)a1.x + (double)a1.y;
+            s2 += (double)a2.x + (double)a2.y;
+        }
+    }
+    s1 = wave_sum_d(s1);
+    s2 = wave_sum_d(s2);
+    __shared__ double sh[2][4];
+    const int wv = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) { sh[0][wv] = s1; sh[1][wv] = s2; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        atomicAdd(&d.stats[2 * th.item], sh[0][0] + sh[0][1] + sh[0][2] + sh[0][3]);
+        atomicAdd(&d.stats[2 * th.item + 1], sh[1][0] + sh[1][1] + sh[1][2] + sh[1][3]);
+    }
+}
+
+template <typename ZT, bool FAST>
+__global__ __launch_bounds__(256) void fdec_lr_merge2_kernel(const LowRankDesc d) {
+    const LrThread th = lr_thread(d);
+    if (!th.active) return;
+    const int N8 = 8 * d.Co;
+    const int64_t rp = (int64_t)d.W * N8;
+    const ZT* zb = (const ZT*)d.Z + (int64_t)th.item * d.Hs * rp + (int64_t)th.w * N8 + th.c;
+    const ZT* sb = (const ZT*)d.Zs + (int64_t)th.seg * d.Hk * rp + (int64_t)th.w * N8 + th.c;
+    float mean, rstd;
+    gn_params(d.stats, th.item, 4LL * d.Hd * d.W * d.Co, mean, rstd);
+    const f2 bias = ld2(d.bias + th.c);
+    const f2 gsc = ld2(d.gn_w + th.c) * splat(rstd);     // (y - mean) * rstd * w + b  as  (y - mean) * gsc + b
+    const f2 gb = ld2(d.gn_b + th.c);
+    const int64_t kp = (int64_t)d.W * d.C_skip;
+    const int64_t kb = (int64_t)th.seg * d.H_skip * kp + (int64_t)th.w * d.C_skip + th.c;
+    f2 ka = {}, kd = {};
+    const int64_t ob = (int64_t)th.item * d.Hd * d.W * d.Co + (int64_t)th.w * d.Co + th.c;
+    const int64_t op = (int64_t)d.W * d.Co;
+
+    f2 zr0[4], zdr[4], sr0[4], sdr[4];   // slots: taps 0, 3, 4, 7
+    f2 base[4];
+    f2 cur3 = {}, cur4 = {}, cur7 = {}, prev7 = {};
+    LrStep nx = lr_step(d.steps, 0);
+    for (int v = 0; v <= d.Hd; ++v) {
+        const LrStep st = nx;                     // the next step's entry is in flight during this step
+        if (v < d.Hd) nx = lr_step(d.steps, v + 1);
+        f2 T[4];
+        if (v < d.Hd) {
+            if (st.flags & 3u) {
+                if (st.flags & 1u) load_rows<ZT, 4>(zb, rp, d.Co, st.zk & 0xFF, (st.zk >> 8) & 0xFF, 1.0f, zr0, zdr);
+                if (st.flags & 2u) load_rows<ZT, 4>(sb, rp, d.Co, (st.zk >> 16) & 0xFF, st.zk >> 24, 0.1f, sr0, sdr);
+#pragma unroll
+                for (int t = 0; t < 4; ++t) base[t] = zr0[t] + sr0[t] + ((t == 1 || t == 2) ? bias : f2{});
+            }
+#pragma unroll
+            for (int t = 0; t < 4; ++t) T[t] = pfma(splat(st.lz), zdr[t], pfma(splat(st.lk), sdr[t], base[t]));
+        } else {
+#pragma unroll
+            for (int t = 0; t < 4; ++t) T[t] = f2{};
+        }
+        if (v >= 1) {
+            // output row dd = v - 1: the exact /4 bilinear resize of the 4*Hd ConvT rows reads rows 4dd+1 and 4dd+2
+            // with weights 0.5 / 0.5 (src = 4dd + 1.5, exact in fp32)
+            const int dd = v - 1;
+            if (st.flags & 4u) {
+                const int j0 = (int)(st.jj & 0xFFFF), j1 = (int)(st.jj >> 16);
+                f2 a, b;
+                if (d.skip_bf16) {
+                    a = ld2((const bf16_t*)d.skip + kb + (int64_t)j0 * kp);
+                    b = ld2((const bf16_t*)d.skip + kb + (int64_t)j1 * kp);
+                } else {
+                    a = ld2((const float*)d.skip + kb + (int64_t)j0 * kp);
+                    b = ld2((const float*)d.skip + kb + (int64_t)j1 * kp);
+                }
+                ka = a * splat(0.1f);
+                kd = (b - a) * splat(0.1f);
+            }
+            const f2 y1 = cur3 + prev7;
+            const f2 y2 = cur4 + T[0];
+            f2 g1, g2;
+            if constexpr (FAST) {
+                g1 = gelu2_pk(pfma(y1 - splat(mean), gsc, gb));
+                g2 = gelu2_pk(pfma(y2 - splat(mean), gsc, gb));
+            } else {
+                g1 = gelu2<false>(pfma(y1 - splat(mean), gsc, gb));
+                g2 = gelu2<false>(pfma(y2 - splat(mean), gsc, gb));
+            }
+            const f2 o = pfma(g1 + g2, splat(0.5f), pfma(splat(st.lj), kd, ka));
+            const int64_t oi = ob + (int64_t)dd * op;
+            if (d.out_bf16) {
+                const bf2_t h = __builtin_convertvector(o, bf2_t);
+                *reinterpret_cast<bf2_t*>((bf16_t*)d.out + oi) = h;
+            } else {
+                *reinterpret_cast<f2*>((float*)d.out + oi) = o;
+            }
+        }
+        prev7 = cur7;
+        cur3 = T[1];
+        cur4 = T[2];
+        cur7 = T[3];
+    }
+}
+
+static bool lr_v1() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = std::getenv("ATHD_LR_V1");
+        v = e && *e && *e != '0' ? 1 : 0;
+    }
+    return v == 1;
+}
+
+int fdec_lr_steps_launch(LrStep* steps, int Hd, int Hs, int Hk, int H_skip, hipStream_t s) {
+    if (!steps || Hd <= 0 || Hs <= 0 || Hs > 256 || Hk <= 0 || Hk > 256 || H_skip <= 0 || H_skip > 65536) return -1;
+    KScope ks(s);
+    if (ks.on()) ks.begin("fdec_lr_steps_kernel", 0.0, (double)(Hd + 1) * sizeof(LrStep));
+    hipLaunchKernelGGL(fdec_lr_steps_kernel, dim3(1), dim3(256), 0, s, steps, Hd, Hs, Hk, H_skip);
+    return (int)hipGetLastError();
+}
+
 static bool lr_ok(const LowRankDesc& d) {
     return d.Z && d.Zs && d.bias && d.stats && d.Co % 2 == 0 && d.Hd > 0 && d.Hd < 65536 && d.W > 0 && d.P > 0 &&
            d.NI % d.P == 0 && d.Hs > 0 && d.Hk > 0;
@@ -299,7 +554,10 @@ int fdec_lr_stats_launch(const LowRankDesc& d, hipStream_t s) {
         const double by = ze * 8.0 * d.Co * d.W * ((double)d.NI * d.Hs + (double)(d.NI / d.P) * d.Hk);
         ks.begin(d.z_bf16 ? "fdec_lr_stats_kernel<unsignedshort>" : "fdec_lr_stats_kernel<float>", 0.0, by);
     }
-    if (d.z_bf16) hipLaunchKernelGGL(fdec_lr_stats_kernel<bf16_t>, grid, dim3(256), 0, s, d);
+    if (d.steps && !lr_v1()) {
+        if (d.z_bf16) hipLaunchKernelGGL(fdec_lr_stats2_kernel<bf16_t>, grid, dim3(256), 0, s, d);
+        else hipLaunchKernelGGL(fdec_lr_stats2_kernel<float>, grid, dim3(256), 0, s, d);
+    } else if (d.z_bf16) hipLaunchKernelGGL(fdec_lr_stats_kernel<bf16_t>, grid, dim3(256), 0, s, d);
     else hipLaunchKernelGGL(fdec_lr_stats_kernel<float>, grid, dim3(256), 0, s, d);
     return (int)hipGetLastError();
 }
@@ -320,7 +578,15 @@ int fdec_lr_merge_launch(const LowRankDesc& d, hipStream_t s) {
         ks.begin(klabel("fdec_lr_merge_kernel<%s,%s>", d.z_bf16 ? "unsignedshort" : "float",
                         d.fast_gelu ? "true" : "false"), 0.0, by);
     }
-    if (d.z_bf16) {
+    if (d.steps && !lr_v1()) {
+        if (d.z_bf16) {
+            if (d.fast_gelu) hipLaunchKernelGGL((fdec_lr_merge2_kernel<bf16_t, true>), grid, dim3(256), 0, s, d);
+            else hipLaunchKernelGGL((fdec_lr_merge2_kernel<bf16_t, false>), grid, dim3(256), 0, s, d);
+        } else {
+            if (d.fast_gelu) hipLaunchKernelGGL((fdec_lr_merge2_kernel<float, true>), grid, dim3(256), 0, s, d);
+            else hipLaunchKernelGGL((fdec_lr_merge2_kernel<float, false>), grid, dim3(256), 0, s, d);
+        }
+    } else if (d.z_bf16) {
         if (d.fast_gelu) hipLaunchKernelGGL((fdec_lr_merge_kernel<bf16_t, true>), grid, dim3(256), 0, s, d);
         else hipLaunchKernelGGL((fdec_lr_merge_kernel<bf16_t, false>), grid, dim3(256), 0, s, d);
     } else {

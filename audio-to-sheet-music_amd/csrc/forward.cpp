@@ -80,6 +80,7 @@ struct Bufs {
     void* Hm;
     float *G, *D, *FO;
     float* ola_part;    // boundary partial sums of the fused iSTFT (spectral.hip)
+    LrStep* lrsteps;    // level-1 low-rank decoder step table (fdec_lr.hip)
     void *S, *Z, *Zs;   // freq level 1 re-associated (fdec_lr.hip): per-tap products of the 32 / 8 source rows
     mutable float* xt2 = nullptr;   // time_out(time decoder) of the last decode chunk: D (fused tail) or G (ragged T)
 };
@@ -162,6 +163,7 @@ size_t plan(Arena& ar, const Dims& d, Bufs& b, bool actbf) {
     b.Zs = act(d.Bc * 8 * Ts * 8 * DEC_CH[2]);
     b.FO = ar.take<float>(NI * Ts * Ts * 2);
     b.ola_part = ar.take<float>(istft_ola_part_floats(NI, (int)Ts));
+    b.lrsteps = ar.take<LrStep>(Ts + 1);
     return ar.off;
 }
 
@@ -623,6 +625,8 @@ void decode_chunk(Run& r, const Dims& d, const Bufs& b, int64_t s0, int64_t Bc, 
         gs.C = b.Zs;
         r.gemm(gs, "fdec1.zs");
         LowRankDesc lr;
+        r.check(fdec_lr_steps_launch(b.lrsteps, (int)Ts, 32, 8, 32, r.s), "fdec_lr_steps");
+        lr.steps = b.lrsteps;
         lr.Z = b.Z; lr.Zs = b.Zs; lr.z_bf16 = ab; lr.Hs = 32; lr.Hk = 8; lr.Hd = (int)Ts; lr.W = (int)Ts;
         lr.Co = w1.cout; lr.P = P; lr.NI = NI; lr.bias = w1.bias; lr.stats = r.stats(NI);
         lr.gn_w = w1.gnw; lr.gn_b = w1.gnb; lr.fast_gelu = ab;

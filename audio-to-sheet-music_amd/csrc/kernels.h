@@ -81,7 +81,18 @@ struct MergeDesc {
 int dec_merge_launch(const MergeDesc& d, hipStream_t s);   // -1: P > 256 or NI % P != 0
 // fdec_lr.hip: FreqDecoder level 1 from the 32-row level-0 output (re-associated ConvT; see fdec_lr.hip).
 // Z [NI][Hs][W][8*Co] = W_k S[j] per tap k; Zs [NI/P][Hk][W][8*Co] = W_k skip3[m]; skip [NI/P][H_skip][W][C_skip].
+// per output-row step v of the level-1 low-rank decoder (fdec_lr.hip): the resize lerps of the Z rows (Hs -> Hd), the
+// skip-projection rows (Hk -> Hd) and, for row dd = v - 1, the skip rows (H_skip -> Hd); flags: bit 0 / 1 / 2 = the
+// z / k / j rows differ from step v - 1 (always set at v = 0)
+struct LrStep {
+    float lz, lk, lj;
+    uint32_t zk;        // i0z | i1z << 8 | i0k << 16 | i1k << 24
+    uint32_t jj;        // i0j | i1j << 16
+    uint32_t flags;
+    uint32_t pad[2];
+};
 struct LowRankDesc {
+    const LrStep* steps = nullptr;                // Hd + 1 entries (fdec_lr_steps_launch)
     const void* Z = nullptr; const void* Zs = nullptr; int z_bf16 = 0;
     int Hs = 32, Hk = 8, Hd = 0, W = 0, Co = 0, P = 1, NI = 0;
     const float* bias = nullptr;                  // ConvT bias [Co]
@@ -90,6 +101,7 @@ struct LowRankDesc {
     const void* skip = nullptr; int skip_bf16 = 0; int H_skip = 0; int C_skip = 0;
     void* out = nullptr; int out_bf16 = 0;        // [NI][Hd][W][Co]
 };
+int fdec_lr_steps_launch(LrStep* steps, int Hd, int Hs, int Hk, int H_skip, hipStream_t s);
 int fdec_lr_stats_launch(const LowRankDesc& d, hipStream_t s);
 int fdec_lr_merge_launch(const LowRankDesc& d, hipStream_t s);
 // fenc_row.hip: a whole narrow frequency-encoder level (conv + GELU + DConv + rewrite GLU) per (b, f) row, bf16 mode
