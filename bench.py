@@ -248,7 +248,11 @@ def main():
     if kp is None or kp["launches"] == 0:
         raise RuntimeError(f"roofline kernel {dominant!r} was not launched in the timed region")
     per_launch_ms = kp["ms"] / kp["launches"]
-    if dominant.startswith(MFMA_KERNELS):
+    # the kernel's bound is the larger of its two floors: algorithmic flops at the MFMA peak, algorithmic bytes at
+    # the HBM peak (e.g. the decoder's K = 288 ConvT GEMM moves 6.2 GB for 1.2 TFLOP: HBM-bound)
+    t_mfma = kp["flops"] / (peak_mfma * 1e12) if dominant.startswith(MFMA_KERNELS) else 0.0
+    t_hbm = kp["bytes"] / (HBM_PEAK_GBS * 1e9)
+    if t_mfma >= t_hbm:
         peak = peak_mfma
         ach = kp["flops"] / (kp["ms"] * 1e-3) / 1e12
         bound, unit = "mfma", "TFLOP/s"
@@ -262,6 +266,8 @@ def main():
                 "share_of_step": round(kp["ms"] / ROOF_STEPS / ms, 4),
                 "algorithmic_per_launch": {"flops": kp["flops"] / kp["launches"],
                                            "bytes": kp["bytes"] / kp["launches"]},
+                "floors_ms_per_launch": {"mfma": round(t_mfma * 1e3 / kp["launches"], 4),
+                                         "hbm": round(t_hbm * 1e3 / kp["launches"], 4)},
                 "timing": f"HIP events on the launch stream around every launch of the kernel, {ROOF_STEPS} forwards "
                           "after the timed region (branches serialised on one stream)",
                 "step": {"achieved_tflops": round(step_tf, 2), "peak": peak_mfma, "frac": round(step_tf / peak_mfma, 4),
