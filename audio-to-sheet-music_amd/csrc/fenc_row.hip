@@ -44,22 +44,23 @@ ATHD_DEV void st4bf(bf16_t* p, float a, float b, float c, float d) {
     *reinterpret_cast<uint2*>(p) = make_uint2(pack2bf(a, b), pack2bf(c, d));
 }
 
-// sum of (s1, s2) over the workgroup; `red` is a fresh [2][FR_NW] slot per call
+// sum of (s1, s2) over the workgroup of NW waves; `red` is a fresh [2][NW] slot per call
+template <int NW>
 ATHD_DEV void block_sum2(float& s1, float& s2, float* red) {
     s1 = wave_sum(s1);
     s2 = wave_sum(s2);
     const int w = threadIdx.x >> 6;
     if ((threadIdx.x & 63) == 0) {
         red[w] = s1;
-        red[FR_NW + w] = s2;
+        red[NW + w] = s2;
     }
     __syncthreads();
     s1 = 0.f;
     s2 = 0.f;
 #pragma unroll
-    for (int i = 0; i < FR_NW; ++i) {
+    for (int i = 0; i < NW; ++i) {
         s1 += red[i];
-        s2 += red[FR_NW + i];
+        s2 += red[NW + i];
     }
 }
 
@@ -72,10 +73,12 @@ ATHD_DEV void gn_from_sums(float s1, float s2, float cnt, float& mean, float& rs
 
 }  // namespace
 
-template <int CIN, int C>
-__global__ __launch_bounds__(FR_NT, CIN == 4 ? 3 : 1) void fenc_row_kernel(const FencRowDesc d) {
+// NW waves per workgroup (6 for C = 48, 12 for C = 96: one workgroup per CU either way at C = 96 (114 KB LDS), so
+// twice the waves per row halve each wave's m-tiles (and the residual stream's registers: 36 instead of 68))
+template <int CIN, int C, int NW>
+__global__ __launch_bounds__(NW * 64, CIN == 4 ? 3 : 1) void fenc_row_kernel(const FencRowDesc d) {
     constexpr int NCT = C / 16;                  // x channel tiles
-    constexpr int MG = FR_NW / NCT;              // m-tile groups per channel tile
+    constexpr int MG = NW / NCT;              // m-tile groups per channel tile
     constexpr int MTW = (FR_MT_MAX + MG - 1) / MG;
     constexpr int TPM = FR_MT_MAX * 16;
     constexpr int H = C / 8;
@@ -87,17 +90,18 @@ __global__ __launch_bounds__(FR_NT, CIN == 4 ? 3 : 1) void fenc_row_kernel(const
     constexpr int HS_P = 40;
     constexpr int K3 = 3 * C, K3S = (K3 + 31) / 32;
     constexpr int KRS = (C + 31) / 32;
+    constexpr int C3I = (FR_MT_MAX + NW - 1) / NW;  // conv3 m-tiles per wave
     // LDS: the conv input stage and the DConv hidden tile share one buffer (the conv is done before the first
     // hidden tile is written); the output row is staged in xs once the rewrite has read it.  C = 48: 52.7 KB and
     // <= 168 VGPRs (launch bound: 3 waves per SIMD), so two 6-wave workgroups share a CU.
     constexpr int XIN_E = (TPM * XIN_P > TPM * HS_P) ? TPM * XIN_P : TPM * HS_P;
-    static_assert(C % 16 == 0 && FR_NW % NCT == 0 && KC % KS == 0 && KS % 32 == 0 && (CIN == 4 || CIN % 8 == 0),
+    static_assert(C % 16 == 0 && NW % NCT == 0 && KC % KS == 0 && KS % 32 == 0 && (CIN == 4 || CIN % 8 == 0),
                   "fenc_row shape");
     static_assert(TPM * C <= (TPM + 2 * FR_HALO) * XS_P, "output staging fits xs");
     __shared__ __attribute__((aligned(16))) bf16_t xin[XIN_E];
     __shared__ __attribute__((aligned(16))) bf16_t xs[(TPM + 2 * FR_HALO) * XS_P];
     bf16_t* const hs = xin;
-    __shared__ float red[4][2 * FR_NW];
+    __shared__ float red[4][2 * NW];
 
     // row r -> block: the 8 XCDs each take a contiguous run of rows, so neighbouring output rows (which share 4 of
     // their 8 input rows) run on one XCD and re-read those rows from its L2
@@ -115,7 +119,7 @@ __global__ __launch_bounds__(FR_NT, CIN == 4 ? 3 : 1) void fenc_row_kernel(const
     const int cb = ct * 16 + 4 * l4;             // first of this lane's 4 x channels
 
     // zero xs (conv3 zero padding: halo rows and positions >= T)
-    for (int i = tid; i < (TPM + 2 * FR_HALO) * XS_P / 8; i += FR_NT)
+    for (int i = tid; i < (TPM + 2 * FR_HALO) * XS_P / 8; i += (NW * 64))
         reinterpret_cast<uint4*>(xs)[i] = make_uint4(0u, 0u, 0u, 0u);
 
     // ---------------------------------------------------------------- conv (8,1)/(4,1)/(2,0) + GELU
@@ -124,7 +128,7 @@ __global__ __launch_bounds__(FR_NT, CIN == 4 ? 3 : 1) void fenc_row_kernel(const
     for (int i = 0; i < MTW; ++i) xr[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
     for (int s = 0; s < NSTAGE; ++s) {
         if (s > 0) __syncthreads();
-        for (int c = tid; c < TP * (KS / 8); c += FR_NT) {
+        for (int c = tid; c < TP * (KS / 8); c += (NW * 64)) {
             const int m = c / (KS / 8), q = c - m * (KS / 8);
             uint4 v = make_uint4(0u, 0u, 0u, 0u);
             if constexpr (CIN == 4) {
@@ -175,7 +179,7 @@ __global__ __launch_bounds__(FR_NT, CIN == 4 ? 3 : 1) void fenc_row_kernel(const
     __syncthreads();
     // the conv input stage is dead: zero the hidden tile's K padding columns 16..31 (columns 0..15 are written by
     // every conv3 pass, zeros past H included)
-    for (int i = tid; i < TPM * 2; i += FR_NT)
+    for (int i = tid; i < TPM * 2; i += (NW * 64))
         *reinterpret_cast<uint4*>(&hs[(i >> 1) * HS_P + 16 + 8 * (i & 1)]) = make_uint4(0u, 0u, 0u, 0u);
 
     // ---------------------------------------------------------------- DConv: x += LayerScale(GLU(GN(1x1(GELU(GN(conv3(x)))))))
@@ -183,17 +187,17 @@ __global__ __launch_bounds__(FR_NT, CIN == 4 ? 3 : 1) void fenc_row_kernel(const
     for (int dd = 0; dd < 2; ++dd) {
         const int dil = 1 << dd;
         // conv3 (C -> H, 3 taps, dilation dil, zero padding) on m-tiles wave, wave + 6, wave + 12
-        f32x4_t ha[3];
+        f32x4_t ha[C3I];
 #pragma unroll
-        for (int i = 0; i < 3; ++i) ha[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+        for (int i = 0; i < C3I; ++i) ha[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int ks = 0; ks < K3S; ++ks) {
             const int k0 = ks * 32 + 8 * l4;
             const bf16x8_t wf = ldfrag(d.w3[dd] + (int64_t)l15 * d.w3_ld + k0);   // rows >= H and k >= 3C are zero
             const int tap = k0 / C, c0 = k0 - tap * C;
 #pragma unroll
-            for (int i = 0; i < 3; ++i) {
-                const int mt = wave + FR_NW * i;
+            for (int i = 0; i < C3I; ++i) {
+                const int mt = wave + NW * i;
                 if (mt >= MT) continue;
                 bf16x8_t xf = bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
                 if (k0 < K3) xf = ldfrag(&xs[(FR_HALO + mt * 16 + l15 + (tap - 1) * dil) * XS_P + c0]);
@@ -205,8 +209,8 @@ __global__ __launch_bounds__(FR_NT, CIN == 4 ? 3 : 1) void fenc_row_kernel(const
         for (int q = 0; q < 4; ++q) hb[q] = (4 * l4 + q < H) ? d.b3[dd][4 * l4 + q] : 0.f;
         float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            const int mt = wave + FR_NW * i;
+        for (int i = 0; i < C3I; ++i) {
+            const int mt = wave + NW * i;
             const int m = mt * 16 + l15;
             if (mt >= MT || m >= T) continue;
 #pragma unroll
@@ -218,12 +222,12 @@ __global__ __launch_bounds__(FR_NT, CIN == 4 ? 3 : 1) void fenc_row_kernel(const
                 }
             }
         }
-        block_sum2(s1, s2, red[2 * dd]);
+        block_sum2<NW>(s1, s2, red[2 * dd]);
         float hm, hr;
         gn_from_sums(s1, s2, (float)(H * T), hm, hr);
 #pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            const int mt = wave + FR_NW * i;
+        for (int i = 0; i < C3I; ++i) {
+            const int mt = wave + NW * i;
             if (mt >= MT) continue;
             float g[4];
 #pragma unroll
@@ -263,7 +267,7 @@ __global__ __launch_bounds__(FR_NT, CIN == 4 ? 3 : 1) void fenc_row_kernel(const
                 s2 += a * a + g * g;
             }
         }
-        block_sum2(s1, s2, red[2 * dd + 1]);
+        block_sum2<NW>(s1, s2, red[2 * dd + 1]);
         float ym, yr;
         gn_from_sums(s1, s2, (float)(2 * C * T), ym, yr);
         float gwa[4], gba[4], gwg[4], gbg[4], sc[4];
@@ -344,7 +348,7 @@ __global__ __launch_bounds__(FR_NT, CIN == 4 ? 3 : 1) void fenc_row_kernel(const
         }
         __syncthreads();
         bf16_t* dst = d.out + ((int64_t)b * d.Fout + f) * (int64_t)T * C;
-        for (int i = tid; i < T * C / 8; i += FR_NT)
+        for (int i = tid; i < T * C / 8; i += (NW * 64))
             reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(ob)[i];
     }
 }
@@ -692,8 +696,9 @@ int fenc_row_launch(const FencRowDesc& d, int cin, int c, hipStream_t s) {
         v1 = e && *e && *e != '0' ? 1 : 0;
     }
     if (cin == 4 && !v1 && d.T <= F0_TP) hipLaunchKernelGGL(fenc_row0_kernel, grid, dim3(FR_NT), 0, s, d);
-    else if (cin == 4) hipLaunchKernelGGL((fenc_row_kernel<4, 48>), grid, dim3(FR_NT), 0, s, d);
-    else hipLaunchKernelGGL((fenc_row_kernel<48, 96>), grid, dim3(FR_NT), 0, s, d);
+    else if (cin == 4) hipLaunchKernelGGL((fenc_row_kernel<4, 48, 6>), grid, dim3(6 * 64), 0, s, d);
+    else if (v1) hipLaunchKernelGGL((fenc_row_kernel<48, 96, 6>), grid, dim3(6 * 64), 0, s, d);
+    else hipLaunchKernelGGL((fenc_row_kernel<48, 96, 12>), grid, dim3(12 * 64), 0, s, d);
     return (int)hipGetLastError();
 }
 
