@@ -13,6 +13,27 @@ namespace athd {
 
 enum Act { ACT_NONE = 0, ACT_GELU = 1, ACT_GLU = 2 };
 
+// n / d for 0 <= n < 2^31 as a multiply-high and a shift (Granlund-Montgomery with a 31+l bit reciprocal:
+// mul = ceil(2^(31+l) / d), l = ceil(log2 d), exact for every n < 2^31).  Filled by gemm_launch; the kernels' row
+// index decompositions (m -> w, h, b) and GroupNorm group indices use it instead of the ~30-instruction integer
+// division sequence.
+struct FastDivU {
+    uint32_t mul = 0, shift = 0, d = 1;
+};
+inline FastDivU make_fastdiv(uint32_t d) {
+    FastDivU f;
+    f.d = d;
+    if (d <= 1) return f;
+    uint32_t l = 0;
+    while ((1ull << l) < d) ++l;
+    f.mul = (uint32_t)((((uint64_t)1 << (31 + l)) + d - 1) / d);
+    f.shift = l - 1;
+    return f;
+}
+#if defined(__HIPCC__)
+__device__ inline uint32_t fdiv(uint32_t n, const FastDivU& f) { return f.d == 1 ? n : __umulhi(n, f.mul) >> f.shift; }
+#endif
+
 struct GemmDesc {
     // A operand (activations), channels-last
     const void* A = nullptr;
@@ -53,6 +74,7 @@ struct GemmDesc {
     const float* row_add = nullptr;   // out += row_add[ho][n]   (freq embedding after encoder level 0)
     double* stats = nullptr;          // per-batch {sum, sumsq} of the final output value
     const double* gn_stats = nullptr; // GroupNorm(1) applied to v (after bias, before act) with per-batch
+    FastDivU fd_w, fd_h, fd_hw;       // W, H_out, H_out * W (filled by the launchers: with_fastdiv)
     int64_t gn_count = 0;             //   statistics {sum, sumsq} over gn_count elements and per-column
     const float* gn_w = nullptr;      //   affine (packed in the same column order as the weights)
     const float* gn_b = nullptr;
@@ -71,5 +93,13 @@ inline void gemm_work(const GemmDesc& d, int mode, double& flops, double& bytes)
 
 // mode: 0 = exact fp32 (v_mfma_f32_16x16x4_f32), 1 = bf16 (v_mfma_f32_16x16x32_bf16, fp32 accumulate)
 int gemm_launch(const GemmDesc& d, int mode, hipStream_t s);
+// d with its fast-division constants filled (every kernel launcher passes this copy to the kernel)
+inline GemmDesc with_fastdiv(const GemmDesc& d) {
+    GemmDesc e = d;
+    e.fd_w = make_fastdiv((uint32_t)d.W);
+    e.fd_h = make_fastdiv((uint32_t)d.H_out);
+    e.fd_hw = make_fastdiv((uint32_t)d.H_out * (uint32_t)d.W);
+    return e;
+}
 
 }  // namespace athd

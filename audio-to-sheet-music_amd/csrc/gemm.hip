@@ -8,6 +8,8 @@
 //         permutation of the 32 k that A and B share, so the result is the exact f32 fmaf chain per k-order.
 // Global->LDS is register staged and double buffered: tile t+1 is loaded into registers before the MFMAs of
 // tile t and written to the other LDS buffer after them; one barrier per k-step.
+#include <cstdlib>
+
 #include "common.h"
 #include "prof.h"
 #include "gemm.h"
@@ -263,8 +265,8 @@ static void launch_cfg(const GemmDesc& d, hipStream_t s) {
         gemm_work(d, MODE, fl, by);
         ks.begin(klabel("gemm_kernel<%d,%d,%d,%d,%d,%s>", MODE, BM, BN, WM, WN, vec8 ? "true" : "false"), fl, by);
     }
-    if (vec8) hipLaunchKernelGGL((gemm_kernel<MODE, BM, BN, WM, WN, true>), grid, dim3(256), 0, s, d);
-    else hipLaunchKernelGGL((gemm_kernel<MODE, BM, BN, WM, WN, false>), grid, dim3(256), 0, s, d);
+    if (vec8) hipLaunchKernelGGL((gemm_kernel<MODE, BM, BN, WM, WN, true>), grid, dim3(256), 0, s, with_fastdiv(d));
+    else hipLaunchKernelGGL((gemm_kernel<MODE, BM, BN, WM, WN, false>), grid, dim3(256), 0, s, with_fastdiv(d));
 }
 
 template <int MODE>
@@ -282,8 +284,9 @@ int gemm3_launch(const GemmDesc& d, hipStream_t s, int variant);
 bool gemm4_supported(const GemmDesc& d);
 int gemm4_launch(const GemmDesc& d, hipStream_t s);
 
-int gemm_launch(const GemmDesc& d, int mode, hipStream_t s) {
-    if (d.Kp % BK != 0 || d.Kp < d.K || d.C_in <= 0 || d.N <= 0) return -2;
+int gemm_launch(const GemmDesc& d0, int mode, hipStream_t s) {
+    if (d0.Kp % BK != 0 || d0.Kp < d0.K || d0.C_in <= 0 || d0.N <= 0) return -2;
+    const GemmDesc d = with_fastdiv(d0);
     if (d.act == ACT_GLU && (d.N % 32 != 0)) return -2;
     // bf16 activations, N a multiple of 256: 256x256 tile, half-tile staged pipeline (gemm4.hip).  (Measured on
     // N = 192 / 384: slower than gemm3's 256x192 tiles, which waste no columns.)
@@ -291,7 +294,16 @@ int gemm_launch(const GemmDesc& d, int mode, hipStream_t s) {
     // other N >= 192: 256x192 or 192x192 tile, 8 waves (gemm3.hip)
     // (K >= 384: 192x192 tiles with a 3-stage ring, two K-tiles in flight across each barrier; measured per call
     // site 2-20 % faster there.  Shorter K, e.g. the K=288 four-residue ConvT, keeps 256x192 x 2 stages.)
-    if (mode == 1 && gemm3_supported(d) && d.N >= 192) return gemm3_launch(d, s, 100 + (d.K >= 384 ? 7 : 3));   // persistent grid
+    if (mode == 1 && gemm3_supported(d) && d.N >= 192) {
+        int v = d.K >= 384 ? 7 : 3;
+        static int quad_v = -2;
+        if (quad_v == -2) {
+            const char* e = std::getenv("ATHD_G3_QUAD");
+            quad_v = e && *e ? std::atoi(e) : -1;
+        }
+        if (d.k_blk > 0 && quad_v >= 0) v = quad_v;       // (measurement override for the four-residue ConvT)
+        return gemm3_launch(d, s, 100 + v);               // persistent grid
+    }
     if (mode == 1 && gemm2_supported(d)) return gemm2_launch(d, s);
     if (mode == 1) launch_mode<1>(d, s);
     else launch_mode<0>(d, s);

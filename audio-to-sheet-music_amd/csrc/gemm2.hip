@@ -216,8 +216,8 @@ static void launch2f(const GemmDesc& d, hipStream_t s) {
         gemm_work(d, 1, fl, by);
         ks.begin(klabel("gemm2_kernel<%d,%d,%s,%u>", BM, BN, d.a_bf16 ? "true" : "false", F), fl, by);
     }
-    if (d.a_bf16) hipLaunchKernelGGL((gemm2_kernel<BM, BN, true, F>), grid, dim3(256), 0, s, d);
-    else hipLaunchKernelGGL((gemm2_kernel<BM, BN, false, F>), grid, dim3(256), 0, s, d);
+    if (d.a_bf16) hipLaunchKernelGGL((gemm2_kernel<BM, BN, true, F>), grid, dim3(256), 0, s, with_fastdiv(d));
+    else hipLaunchKernelGGL((gemm2_kernel<BM, BN, false, F>), grid, dim3(256), 0, s, with_fastdiv(d));
 }
 
 template <int BM, int BN>

@@ -70,10 +70,10 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm3_kernel(const GemmDesc d) {
             const uint32_t m = (uint32_t)(m0 + 8 * (wave + NW * q) + lrow);
             a_ok[q] = m < (uint32_t)M;
             const uint32_t mm = a_ok[q] ? m : 0u;
-            const uint32_t w = mm % (uint32_t)d.W;
-            const uint32_t tt = mm / (uint32_t)d.W;
-            const uint32_t ho = tt % (uint32_t)d.H_out;
-            const uint32_t bb = tt / (uint32_t)d.H_out;
+            const uint32_t tt = fdiv(mm, d.fd_w);
+            const uint32_t w = mm - tt * (uint32_t)d.W;
+            const uint32_t bb = fdiv(tt, d.fd_h);
+            const uint32_t ho = tt - bb * (uint32_t)d.H_out;
             a_base[q] = (int64_t)bb * a_bs + (int64_t)w * d.a_ld;
             a_h0[q] = (int)ho * d.in_stride + d.in_off;
         }
@@ -224,7 +224,7 @@ static void launch3f(const GemmDesc& d, hipStream_t s, bool persist) {
         gemm_work(d, 1, fl, by);
         ks.begin(klabel("gemm3_kernel<%d,%d,%d,%d,%d,%u>", BM, BN, WM, WN, ST, F), fl, by);
     }
-    hipLaunchKernelGGL((gemm3_kernel<BM, BN, WM, WN, ST, F>), grid, dim3(WM * WN * 64), 0, s, d);
+    hipLaunchKernelGGL((gemm3_kernel<BM, BN, WM, WN, ST, F>), grid, dim3(WM * WN * 64), 0, s, with_fastdiv(d));
 }
 
 template <int BM, int BN, int WM, int WN, int ST>
@@ -240,7 +240,8 @@ static void launch3(const GemmDesc& d, hipStream_t s, bool persist) {
 
 // variant: 0 = auto, 1 = 256x128 (8 waves, 3 stages), 2 = 128x128 (4 waves, 3 stages), 3 = 256x192 (8 waves, 2 st),
 // 4 = 128x192 (4 waves, 2 stages: 80 KB LDS, 2 blocks/CU), 5 = 128x192 (4 waves, 3 stages), 6 = 128x96 (4 waves, 3 st),
-// 7 = 192x192 (8 waves, 3 stages: 144 KB LDS); + 100: persistent grid (resident blocks walk the M tiles)
+// 7 = 192x192 (8 waves, 3 stages: 144 KB LDS), 8 = 128x192 (8 waves, 2 stages: 80 KB, 2 blocks/CU); + 100: persistent
+// grid (resident blocks walk the M tiles)
 int gemm3_launch(const GemmDesc& d, hipStream_t s, int variant) {
     const bool persist = variant >= 100;
     if (persist) variant -= 100;
@@ -251,6 +252,7 @@ int gemm3_launch(const GemmDesc& d, hipStream_t s, int variant) {
     else if (variant == 5) launch3<128, 192, 2, 2, 3>(d, s, persist);
     else if (variant == 6) launch3<128, 96, 2, 2, 3>(d, s, persist);
     else if (variant == 7) launch3<192, 192, 4, 2, 3>(d, s, persist);
+    else if (variant == 8) launch3<128, 192, 4, 2, 2>(d, s, persist);     // 8 waves, 80 KB: 2 blocks per CU
     else launch3<256, 192, 4, 2, 2>(d, s, persist);
     return (int)hipGetLastError();
 }

@@ -114,10 +114,10 @@ __global__ __launch_bounds__(512) void gemm4_kernel(const GemmDesc d) {
             const uint32_t m = (uint32_t)(m0 + r);
             const bool ok = m < (uint32_t)M;
             const uint32_t mm = ok ? m : 0u;
-            const uint32_t w = mm % (uint32_t)d.W;
-            const uint32_t t = mm / (uint32_t)d.W;
-            const uint32_t ho = t % (uint32_t)d.H_out;
-            const uint32_t b = t / (uint32_t)d.H_out;
+            const uint32_t t = fdiv(mm, d.fd_w);
+            const uint32_t w = mm - t * (uint32_t)d.W;
+            const uint32_t b = fdiv(t, d.fd_h);
+            const uint32_t ho = t - b * (uint32_t)d.H_out;
             a_base[h][q] = (uint32_t)(b * a_bs + (int64_t)w * d.a_ld);
             a_h0[h][q] = ok ? (int)ho * d.in_stride + d.in_off : (INT_MIN / 2);
             if (h == 0) b_off[q] = (uint32_t)(((int64_t)(n0 + (sr >> 5) * 64 + (sr & 31)) * d.Kp + 8 * chunk) * 2);
@@ -280,7 +280,7 @@ static void launch4f(const GemmDesc& d, hipStream_t s) {
         gemm_work(d, 1, fl, by);
         ks.begin(klabel("gemm4_kernel<%u>", F), fl, by);
     }
-    hipLaunchKernelGGL((gemm4_kernel<F>), dim3((unsigned)tiles), dim3(512), 0, s, d);
+    hipLaunchKernelGGL((gemm4_kernel<F>), dim3((unsigned)tiles), dim3(512), 0, s, with_fastdiv(d));
 }
 
 #ifdef ATHD_G4_STAMP

@@ -106,13 +106,12 @@ ATHD_DEV void gemm_epilogue(const GemmDesc& d, const f32x4_t (&acc)[TM][TN], int
 
     const int fr = lane & 15, fg = lane >> 4;
     const uint32_t M = (uint32_t)d.nb * d.H_out * d.W;       // < 2^31 on every use
-    const uint32_t HW = (uint32_t)d.H_out * d.W;
     const int64_t c_bs = d.c_bs >= 0 ? d.c_bs : (int64_t)d.H_out_total * d.W * d.ldo;
     const int Nout = f_glu ? d.N / 2 : d.N;
-    const uint32_t g0 = (uint32_t)(m0 / HW);                  // first GroupNorm group touched by this block
+    const uint32_t g0 = fdiv((uint32_t)m0, d.fd_hw);                  // first GroupNorm group touched by this block
     uint32_t mlast = (uint32_t)m0 + (uint32_t)BM - 1;
     if (mlast >= M) mlast = M - 1;
-    const bool one_group = (mlast / HW) == g0;                // fast path: the whole tile in one group
+    const bool one_group = fdiv(mlast, d.fd_hw) == g0;                // fast path: the whole tile in one group
     const int64_t hi_off = f_split ? (int64_t)d.hi_row_off * d.W * d.ldo - d.col_split : 0;
     // one batch of W = 1 rows (the transformer / linear layers): row m is (b, ho, w) = (0, m, 0), no divisions
     const bool linear = d.W == 1 && d.nb == 1;
@@ -144,10 +143,10 @@ ATHD_DEV void gemm_epilogue(const GemmDesc& d, const f32x4_t (&acc)[TM][TN], int
         if (m < M) {
             uint32_t w = 0, ho = m, b = 0;
             if (!linear) {
-                w = m % (uint32_t)d.W;
-                const uint32_t t = m / (uint32_t)d.W;
-                ho = t % (uint32_t)d.H_out;
-                b = t / (uint32_t)d.H_out;
+                const uint32_t t = fdiv(m, d.fd_w);
+                w = m - t * (uint32_t)d.W;
+                b = fdiv(t, d.fd_h);
+                ho = t - b * (uint32_t)d.H_out;
             }
             // signed row arithmetic: o_off may be negative (its row is then masked out by store_mask / hi_row_off)
             const int64_t orow = (int64_t)(int)ho * d.o_stride + d.o_off;
@@ -264,7 +263,7 @@ ATHD_DEV void gemm_epilogue(const GemmDesc& d, const f32x4_t (&acc)[TM][TN], int
             p1 += __shfl_xor(p1, 32, 64);
             p2 += __shfl_xor(p2, 32, 64);
             if (fg == 0 && m < M) {
-                const uint32_t gi = m / HW - g0;
+                const uint32_t gi = fdiv(m, d.fd_hw) - g0;
                 if (gi < (uint32_t)EPI_MAXG) {
                     atomicAdd(&st_lds[2 * gi], (double)p1);
                     atomicAdd(&st_lds[2 * gi + 1], (double)p2);
@@ -315,11 +314,10 @@ ATHD_DEV void gemm_epilogue_res(const GemmDesc& d, const f32x4_t (&acc)[TM][TN],
     constexpr bool f_stats = (F & F_STATS) != 0;
     const int fr = lane & 15, fg = lane >> 4;
     const uint32_t M = (uint32_t)d.nb * d.H_out * d.W;
-    const uint32_t HW = (uint32_t)d.H_out * d.W;
-    const uint32_t g0 = (uint32_t)(m0 / HW);
+    const uint32_t g0 = fdiv((uint32_t)m0, d.fd_hw);
     uint32_t mlast = (uint32_t)m0 + (uint32_t)BM - 1;
     if (mlast >= M) mlast = M - 1;
-    const bool one_group = (mlast / HW) == g0;
+    const bool one_group = fdiv(mlast, d.fd_hw) == g0;
     int ncol[TN];
     float4 sc[TN];
 #pragma unroll
@@ -395,7 +393,7 @@ ATHD_DEV void gemm_epilogue_res(const GemmDesc& d, const f32x4_t (&acc)[TM][TN],
                 b += __shfl_xor(b, 32, 64);
                 const uint32_t m = (uint32_t)m0 + wm0 + 16 * i + fr;
                 if (fg == 0 && ok[i]) {
-                    const uint32_t gi = m / HW - g0;
+                    const uint32_t gi = fdiv(m, d.fd_hw) - g0;
                     if (gi < (uint32_t)EPI_MAXG) {
                         atomicAdd(&st_lds[2 * gi], (double)a);
                         atomicAdd(&st_lds[2 * gi + 1], (double)b);

@@ -223,10 +223,11 @@ if __name__ == "__main__":
         attn_case(64, 2072, vs)
         sys.exit(0)
     if "attn" in sys.argv[1:]:
-        attn_case(4, 200)
-        attn_case(2, 67)
-        attn_case(64, 2072)
-        attn_case(64, 1034)
+        av = tuple(int(x) for x in os.environ.get("ATTN_VARIANTS", "1,0,2,3").split(","))
+        attn_case(4, 200, av)
+        attn_case(2, 67, av)
+        attn_case(64, 2072, av)
+        attn_case(64, 1034, av)
         sys.exit(0)
     M = 64 * 2072
     if "persist" in sys.argv[1:]:
