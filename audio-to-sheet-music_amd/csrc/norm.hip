@@ -1,6 +1,8 @@
 // Normalisation, elementwise, resize/merge and table kernels of the hot path (gfx950).
 // GroupNorm/LayerNorm statistics are accumulated in fp64 (sum, sum of squares) so that the one-pass
 // variance matches PyTorch's fp32 two-pass/Welford results to rounding.
+#include <cstdlib>
+
 #include "common.h"
 #include "prof.h"
 #include "kernels.h"
@@ -444,6 +446,114 @@ __global__ __launch_bounds__(256) void dec_merge_kernel(const MergeDesc d) {
     }
 }
 
+// Time-branch merge (W = 1, all rows stored, V = 8 channels per thread, P prompt items per segment): each thread walks a
+// run of DM_RUN consecutive output rows.  The H resize reads source rows (i0, i1) with i0 advancing by ~1 per output
+// row, so the GroupNorm -> GELU'd rows are cached per item and each source row is loaded and activated once instead of
+// twice (dec_merge_kernel: two rows per output row); the P items' rows are processed together (their loads in flight
+// at once), the skip rows once per segment.  Same arithmetic as dec_merge_kernel, value for value.
+constexpr int DM_RUN = 16;
+
+template <int P, int PP, bool FAST>
+__global__ __launch_bounds__(256) void dec_merge_w1_kernel(const MergeDesc d) {
+    const int64_t seg = blockIdx.y;
+    const int cv = d.C / 8;
+    const int t = blockIdx.x * 256 + threadIdx.x;
+    const int run = t / cv, c = (t - run * cv) * 8;
+    const int h0 = run * DM_RUN;
+    if (h0 >= d.H_out) return;
+    const int h1 = min(h0 + DM_RUN, d.H_out);
+    const bool gn = d.stats != nullptr;
+    float gw[8], gb[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        gw[j] = gn ? d.gn_w[c + j] : 1.f;
+        gb[j] = gn ? d.gn_b[c + j] : 0.f;
+    }
+    const int64_t src_item = (int64_t)d.H_src * d.C;
+    const int64_t out_item = (int64_t)d.H_out * d.C;
+    const int64_t sk = seg * (int64_t)d.H_skip * d.C_skip + c;
+    // PP items per pass over the run (the skip rows are re-read per pass, from L2)
+#pragma unroll 1
+    for (int p0 = 0; p0 < P; p0 += PP) {
+        float mean[PP], rstd[PP];
+#pragma unroll
+        for (int p = 0; p < PP; ++p) {
+            mean[p] = 0.f;
+            rstd[p] = 1.f;
+            if (gn) gn_params(d.stats, seg * P + p0 + p, d.gn_count, mean[p], rstd[p]);
+        }
+        // activated source row `row` of item p0 + p into x
+        auto act_row = [&](int p, int row, float* x) {
+            ldv<8>(d.src, d.src_bf16, (seg * P + p0 + p) * src_item + (int64_t)row * d.C + c, x);
+            if (gn) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const float u = (x[j] - mean[p]) * rstd[p] * gw[j] + gb[j];
+                    x[j] = FAST ? gelu_fast(u) : gelu_erf(u);
+                }
+            }
+        };
+        float r0[PP][8], r1[PP][8], ka[8], kb[8];
+        int c0 = -1, c1 = -1, s0 = -1, s1 = -1;
+        for (int ho = h0; ho < h1; ++ho) {
+            const LinIdx li = lin_index(ho, d.H_src, d.H_out);
+            const LinIdx lj = lin_index(ho, d.H_skip, d.H_out);
+            if (li.i0 != c0) {
+                if (li.i0 == c1) {
+#pragma unroll
+                    for (int p = 0; p < PP; ++p)
+#pragma unroll
+                        for (int j = 0; j < 8; ++j) r0[p][j] = r1[p][j];
+                } else {
+#pragma unroll
+                    for (int p = 0; p < PP; ++p) act_row(p, li.i0, r0[p]);
+                }
+            }
+            if (li.i1 != c1) {
+                if (li.i1 == li.i0) {
+#pragma unroll
+                    for (int p = 0; p < PP; ++p)
+#pragma unroll
+                        for (int j = 0; j < 8; ++j) r1[p][j] = r0[p][j];
+                } else {
+#pragma unroll
+                    for (int p = 0; p < PP; ++p) act_row(p, li.i1, r1[p]);
+                }
+            }
+            c0 = li.i0;
+            c1 = li.i1;
+            if (lj.i0 != s0 || lj.i1 != s1) {
+                ldv<8>(d.skip, d.skip_bf16, sk + (int64_t)lj.i0 * d.C_skip, ka);
+                ldv<8>(d.skip, d.skip_bf16, sk + (int64_t)lj.i1 * d.C_skip, kb);
+                s0 = lj.i0;
+                s1 = lj.i1;
+            }
+            float sv[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) sv[j] = d.H_skip == d.H_out ? ka[j] * 0.1f : (lj.l0 * ka[j] + lj.l1 * kb[j]) * 0.1f;
+#pragma unroll
+            for (int p = 0; p < PP; ++p) {
+                float v[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const float m = d.H_src == d.H_out ? r0[p][j] : li.l0 * r0[p][j] + li.l1 * r1[p][j];
+                    v[j] = m + sv[j];
+                }
+                const int64_t o = (seg * P + p0 + p) * out_item + (int64_t)ho * d.C + c;
+                if (d.out_bf16) {
+                    bf16_t h[8];
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) h[j] = f2bf(v[j]);
+                    *reinterpret_cast<uint4*>((bf16_t*)d.out + o) = *reinterpret_cast<uint4*>(h);
+                } else {
+                    *reinterpret_cast<float4*>((float*)d.out + o) = make_float4(v[0], v[1], v[2], v[3]);
+                    *reinterpret_cast<float4*>((float*)d.out + o + 4) = make_float4(v[4], v[5], v[6], v[7]);
+                }
+            }
+        }
+    }
+}
+
 // last freq level: C = 4 merged channels -> freq_out 1x1 (4 -> 2), FO^T [item][w][ho][2] (frame-major for the iSTFT)
 __global__ __launch_bounds__(256) void dec_merge_proj_kernel(const MergeDesc d) {
     const int64_t seg = blockIdx.y;
@@ -487,6 +597,28 @@ int dec_merge_launch(const MergeDesc& d, hipStream_t s) {
         ks.begin(d.proj_w ? "dec_merge_proj_kernel" : (V == 8 ? "dec_merge_kernel<8>" : "dec_merge_kernel<4>"), 0.0, by);
     }
     const dim3 grid(blocks, d.NI / d.P);
+    static int v1 = -1;
+    if (v1 < 0) {
+        const char* e = std::getenv("ATHD_MERGE_V1");
+        v1 = e && *e && *e != '0' ? 1 : 0;
+    }
+    if (!v1 && !d.proj_w && V == 8 && d.W == 1 && !d.kept && d.P == 4 && d.C_skip >= d.C) {
+        const int64_t threads = (int64_t)((d.H_out + DM_RUN - 1) / DM_RUN) * (d.C / 8);
+        const dim3 g1((unsigned)((threads + 255) / 256), d.NI / d.P);
+        static int pp = -1;
+        if (pp < 0) {
+            const char* e = std::getenv("ATHD_MERGE_PP");
+            pp = e && *e == '4' ? 4 : e && *e == '1' ? 1 : 2;
+        }
+        if (d.fast_gelu) {
+            if (pp == 4) hipLaunchKernelGGL((dec_merge_w1_kernel<4, 4, true>), g1, dim3(256), 0, s, d);
+            else if (pp == 1) hipLaunchKernelGGL((dec_merge_w1_kernel<4, 1, true>), g1, dim3(256), 0, s, d);
+            else hipLaunchKernelGGL((dec_merge_w1_kernel<4, 2, true>), g1, dim3(256), 0, s, d);
+        } else {
+            hipLaunchKernelGGL((dec_merge_w1_kernel<4, 2, false>), g1, dim3(256), 0, s, d);
+        }
+        return (int)hipGetLastError();
+    }
     if (d.proj_w) hipLaunchKernelGGL(dec_merge_proj_kernel, grid, dim3(256), 0, s, d);
     else if (V == 8) hipLaunchKernelGGL(dec_merge_kernel<8>, grid, dim3(256), 0, s, d);
     else hipLaunchKernelGGL(dec_merge_kernel<4>, grid, dim3(256), 0, s, d);
