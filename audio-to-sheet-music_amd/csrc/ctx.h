@@ -30,6 +30,9 @@ struct DConvW {
     // 1x1 [2C][H], its bias and GroupNorm affine
     float *w3f[2] = {nullptr, nullptr}, *w1f[2] = {nullptr, nullptr}, *b1f[2] = {nullptr, nullptr};
     float *g2wf[2] = {nullptr, nullptr}, *g2bf[2] = {nullptr, nullptr};
+    // moments of the 1x1 conv for its GroupNorm statistics (dconv.hip c1stat): G = W^T W [H][H], v = W^T b [H],
+    // ws = W^T 1 [H], sum b, sum b^2 (so sum_n y_n and sum_n y_n^2 of y = W h + b come from h alone)
+    float* gram1[2] = {nullptr, nullptr};
 };
 
 struct EncW {

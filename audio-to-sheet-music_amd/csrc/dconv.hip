@@ -157,14 +157,15 @@ ATHD_DEV void gn_lookup(const double* st, double cnt, int64_t g, int64_t g_first
     }
 }
 
-// ---- c1stat: one thread per position; y (2C channels) only feeds the GroupNorm statistics
+// ---- c1stat: one thread per position.  y = W h + b (2C channels) only feeds the GroupNorm statistics, and
+// sum_n y_n = sum b + ws.h, sum_n y_n^2 = sum b^2 + 2 v.h + h^T G h with the 1x1 conv's moments (G = W^T W, v = W^T b,
+// ws = W^T 1: ctx.h DConvW::gram1, computed in fp64 at pack time): H^2 + 3H FMAs per position instead of 2 x 2C x H
 template <int C, bool FAST>
 __global__ __launch_bounds__(256) void dconv_c1_stats_kernel(const float* __restrict__ h, int64_t nb, int64_t L,
                                                              const double* __restrict__ st_h,
                                                              const float* __restrict__ g1w, const float* __restrict__ g1b,
-                                                             const float* __restrict__ W, const float* __restrict__ bias,
-                                                             double* __restrict__ st_y) {
-    constexpr int H = C / 8, N = 2 * C;
+                                                             const float* __restrict__ gram, double* __restrict__ st_y) {
+    constexpr int H = C / 8;
     __shared__ float tm[GN_TAB], tr[GN_TAB];
     __shared__ double sh[16];
     const int64_t P = nb * L;
@@ -180,14 +181,21 @@ __global__ __launch_bounds__(256) void dconv_c1_stats_kernel(const float* __rest
         gn_lookup(st_h, (double)L * H, p / L, gf, ng, tm, tr, mean, rstd);
         float hv[H];
         load_hg<H, FAST>(h, p, mean, rstd, g1w, g1b, hv);
-#pragma unroll 4
-        for (int n = 0; n < N; ++n) {
-            float y = bias[n];
+        const float* G = gram;
+        const float* v = gram + H * H;
+        const float* ws = v + H;
+        float q = 0.f, lv = 0.f, lw = 0.f;
 #pragma unroll
-            for (int j = 0; j < H; ++j) y += W[n * H + j] * hv[j];
-            s1 += y;
-            s2 += y * y;
+        for (int j = 0; j < H; ++j) {
+            float t = 0.f;
+#pragma unroll
+            for (int k = 0; k < H; ++k) t += G[j * H + k] * hv[k];
+            q += hv[j] * t;
+            lv += v[j] * hv[j];
+            lw += ws[j] * hv[j];
         }
+        s1 = ws[H] + lw;
+        s2 = ws[H + 1] + (2.f * lv + q);
     }
     group_stats_add(st_y, p0, p, valid, L, s1, s2, sh);
 }
@@ -249,8 +257,9 @@ __global__ __launch_bounds__(256) void dconv_c1_apply_kernel(TS* __restrict__ x,
 
 template <int C, typename TS, bool FAST>
 static void dconv_small_t(void* x, float* h, int64_t nb, int64_t L, int dil, const float* w3, const float* b3,
-                          const float* g1w, const float* g1b, const float* w1, const float* b1, const float* g2w,
-                          const float* g2b, const float* scale, double* st_h, double* st_y, hipStream_t s) {
+                          const float* g1w, const float* g1b, const float* w1, const float* b1, const float* gram1,
+                          const float* g2w, const float* g2b, const float* scale, double* st_h, double* st_y,
+                          hipStream_t s) {
     constexpr int H = C / 8, TILE = sizeof(TS) == 2 ? 256 : 128;
     const int64_t P = nb * L;
     const double px = (double)P;
@@ -264,9 +273,9 @@ static void dconv_small_t(void* x, float* h, int64_t nb, int64_t L, int dil, con
     }
     {
         KScope ks(s);
-        if (ks.on()) ks.begin(klabel("dconv_c1_stats_kernel<%d>", C), 2.0 * px * 2 * C * H, px * H * 4);
+        if (ks.on()) ks.begin(klabel("dconv_c1_stats_kernel<%d>", C), 2.0 * px * (H * H + 3 * H), px * H * 4);
         hipLaunchKernelGGL((dconv_c1_stats_kernel<C, FAST>), dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, h, nb,
-                           L, st_h, g1w, g1b, w1, b1, st_y);
+                           L, st_h, g1w, g1b, gram1, st_y);
     }
     {
         KScope ks(s);
@@ -278,11 +287,11 @@ static void dconv_small_t(void* x, float* h, int64_t nb, int64_t L, int dil, con
 
 int dconv_small_launch(void* x, int x_bf16, float* h, int64_t nb, int64_t L, int C, int dil, const float* w3,
                        const float* b3, const float* g1w, const float* g1b, const float* w1, const float* b1,
-                       const float* g2w, const float* g2b, const float* scale, double* st_h, double* st_y, hipStream_t s,
-                       bool fast) {
-    if (dil < 1 || dil > 2) return -2;
+                       const float* gram1, const float* g2w, const float* g2b, const float* scale, double* st_h,
+                       double* st_y, hipStream_t s, bool fast) {
+    if (dil < 1 || dil > 2 || !gram1) return -2;
 #define ATHD_DC(CC, TS, FA) \
-    dconv_small_t<CC, TS, FA>(x, h, nb, L, dil, w3, b3, g1w, g1b, w1, b1, g2w, g2b, scale, st_h, st_y, s)
+    dconv_small_t<CC, TS, FA>(x, h, nb, L, dil, w3, b3, g1w, g1b, w1, b1, gram1, g2w, g2b, scale, st_h, st_y, s)
     if (C == 48) {
         if (x_bf16) { if (fast) ATHD_DC(48, bf16_t, true); else ATHD_DC(48, bf16_t, false); }
         else { if (fast) ATHD_DC(48, float, true); else ATHD_DC(48, float, false); }

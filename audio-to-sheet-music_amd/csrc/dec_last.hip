@@ -465,10 +465,47 @@ ATHD_HD int tt_span(int bx, int Lin, int Hg, int& r0) {
     return lin_index(ub, Hg, Lin).i1 - r0 + 1;
 }
 
+// bf16 mode keeps the activated rows as bf16 in LDS (29.6 KB instead of 52.8: 5 blocks per CU instead of 3); the
+// f32 parity mode keeps fp32
+constexpr int TT_LDB = 56;       // bf16 row pitch (elements)
+template <bool BF> struct TtRow;
+template <> struct TtRow<false> {
+    static constexpr int BYTES = TT_ROWS * TT_LD * 4;
+    ATHD_DEV static void put8(char* g, int row, int c0, const float* v) {
+        float2* dst = reinterpret_cast<float2*>((float*)g + row * TT_LD + c0);
+#pragma unroll
+        for (int j = 0; j < 8; j += 2) dst[j / 2] = make_float2(v[j], v[j + 1]);
+    }
+    ATHD_DEV static void get12(const char* g, int row, int c0, float* v) {
+        const float* src = (const float*)g + row * TT_LD + c0;
+#pragma unroll
+        for (int s = 0; s < 12; ++s) v[s] = src[s];
+    }
+};
+template <> struct TtRow<true> {
+    static constexpr int BYTES = TT_ROWS * TT_LDB * 2;
+    ATHD_DEV static void put8(char* g, int row, int c0, const float* v) {
+        *reinterpret_cast<uint4*>((bf16_t*)g + row * TT_LDB + c0) =
+            make_uint4(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]), pack2bf(v[4], v[5]), pack2bf(v[6], v[7]));
+    }
+    ATHD_DEV static void get12(const char* g, int row, int c0, float* v) {
+        const uint2* src = reinterpret_cast<const uint2*>((const bf16_t*)g + row * TT_LDB + c0);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            const uint2 q = src[i];
+            v[4 * i + 0] = __uint_as_float(q.x << 16);
+            v[4 * i + 1] = __uint_as_float(q.x & 0xFFFF0000u);
+            v[4 * i + 2] = __uint_as_float(q.y << 16);
+            v[4 * i + 3] = __uint_as_float(q.y & 0xFFFF0000u);
+        }
+    }
+};
+
 template <bool BF>
 __global__ __launch_bounds__(TL_NT) void tdec_tail_kernel(const DecLastDesc d) {
-    __shared__ __attribute__((aligned(16))) float gs[TT_ROWS * TT_LD];
-    float* zb = gs;                              // phase 3: z rows [TL_NT][16], over the dead phase-1 tile
+    constexpr int GS_BYTES = TtRow<BF>::BYTES > TL_NT * 16 * 4 ? TtRow<BF>::BYTES : TL_NT * 16 * 4;
+    __shared__ __attribute__((aligned(16))) char gsm[GS_BYTES];
+    float* zb = reinterpret_cast<float*>(gsm);  // phase 3: z rows [TL_NT][16], over the dead phase-1 tile
     const int64_t item = blockIdx.y;
     const int64_t seg = item / d.P;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -482,11 +519,9 @@ __global__ __launch_bounds__(TL_NT) void tdec_tail_kernel(const DecLastDesc d) {
         const int rr = i / (DL_C / 8), q = i % (DL_C / 8);
         float a[8];
         ld8(d.g, BF, gb + (int64_t)rr * DL_C + 8 * q, a);
-        float2* dst = reinterpret_cast<float2*>(gs + rr * TT_LD + 8 * q);
 #pragma unroll
-        for (int j = 0; j < 8; j += 2)
-            dst[j / 2] = make_float2(gn_act<BF>(a[j], mean, rstd, d.gn_w[8 * q + j], d.gn_b[8 * q + j]),
-                                     gn_act<BF>(a[j + 1], mean, rstd, d.gn_w[8 * q + j + 1], d.gn_b[8 * q + j + 1]));
+        for (int j = 0; j < 8; ++j) a[j] = gn_act<BF>(a[j], mean, rstd, d.gn_w[8 * q + j], d.gn_b[8 * q + j]);
+        TtRow<BF>::put8(gsm, rr, 8 * q, a);
     }
     __syncthreads();
     const int p = lane & 15, cg = lane >> 4, ch0 = 12 * cg;
@@ -507,8 +542,9 @@ __global__ __launch_bounds__(TL_NT) void tdec_tail_kernel(const DecLastDesc d) {
             Slice12<BF> sl;
             sl.load(2, d.skip2, (seg * d.H_skip2 + lj.i0) * (int64_t)d.C_skip2 + ch0);
             sl.load(3, d.skip2, (seg * d.H_skip2 + lj.i1) * (int64_t)d.C_skip2 + ch0);
-            const float* ga = gs + (li.i0 - r0) * TT_LD + ch0;
-            const float* gq = gs + (li.i1 - r0) * TT_LD + ch0;
+            float ga[12], gq[12];
+            TtRow<BF>::get12(gsm, li.i0 - r0, ch0, ga);
+            TtRow<BF>::get12(gsm, li.i1 - r0, ch0, gq);
 #pragma unroll
             for (int s = 0; s < 12; ++s) {
                 const float sv = (lj.l0 * sl.get(2, s) + lj.l1 * sl.get(3, s)) * 0.1f;

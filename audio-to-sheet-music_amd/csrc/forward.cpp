@@ -248,7 +248,7 @@ void dconv(Run& r, const EncW& e, void* x, int64_t nb, int64_t L, float* hbuf, u
         if (C <= 96) {   // narrow levels: HBM-bound VALU kernels (dconv.hip)
             KSite site(dd == 0 ? "dconv0" : "dconv1");
             r.check(dconv_small_launch(x, ab, hbuf, nb, L, C, dil, e.dc.w3f[dd], e.dc.c3[dd].bias, e.dc.g1w[dd],
-                                       e.dc.g1b[dd], e.dc.w1f[dd], e.dc.b1f[dd], e.dc.g2wf[dd], e.dc.g2bf[dd],
+                                       e.dc.g1b[dd], e.dc.w1f[dd], e.dc.b1f[dd], e.dc.gram1[dd], e.dc.g2wf[dd], e.dc.g2bf[dd],
                                        e.dc.scale[dd], st_h, st_y, r.s, r.actbf), "dconv_small");
             continue;
         }

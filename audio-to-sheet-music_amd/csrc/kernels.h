@@ -153,8 +153,8 @@ int tdec_tail_launch(const DecLastDesc& d, hipStream_t s);
 // x: [nb][L][C] f32 or bf16 (x_bf16), updated in place; h: [nb][L][C/8] f32 scratch
 int dconv_small_launch(void* x, int x_bf16, float* h, int64_t nb, int64_t L, int C, int dil, const float* w3,
                        const float* b3, const float* g1w, const float* g1b, const float* w1, const float* b1,
-                       const float* g2w, const float* g2b, const float* scale, double* st_h, double* st_y, hipStream_t s,
-                       bool fast);
+                       const float* gram1, const float* g2w, const float* g2b, const float* scale, double* st_h,
+                       double* st_y, hipStream_t s, bool fast);
 // (B, 2, T) -> (B, T, 2)
 void wav_interleave_launch(const float* wav, int nb, int64_t T, float* out, hipStream_t s);
 // positional tables of the cross-transformer (computed on device with the fp32 op order of demucs)
