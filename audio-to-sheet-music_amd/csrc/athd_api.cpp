@@ -228,23 +228,9 @@ int athd_finalize(athd_ctx* c) {
                         e.dc.c3p[d] = c->up_gemm(t16, 16, 3 * C, {});
                     }
                     e.dc.w1f[d] = c->up_key(q + ".3.weight");        // [2C][H][1] == [2C][H]
-                    {
-                        const auto& w1 = c->W(q + ".3.weight").v;
-                        const auto& b1 = c->W(q + ".3.bias").v;
-                        std::vector<double> g((size_t)H * H + 2 * H + 2, 0.0);
-                        for (int n = 0; n < 2 * C; ++n) {
-                            const double bn = b1[n];
-                            for (int j = 0; j < H; ++j) {
-                                const double wj = w1[(size_t)n * H + j];
-                                for (int k = 0; k < H; ++k) g[(size_t)j * H + k] += wj * w1[(size_t)n * H + k];
-                                g[(size_t)H * H + j] += bn * wj;
-                                g[(size_t)H * H + H + j] += wj;
-                            }
-                            g[(size_t)H * H + 2 * H] += bn;
-                            g[(size_t)H * H + 2 * H + 1] += bn * bn;
-                        }
-                        e.dc.gram1[d] = c->up_f32(std::vector<float>(g.begin(), g.end()));
-                    }
+                    e.dc.gram1[d] = c->up_f32(conv1x1_moments(c->W(q + ".3.weight").v, c->W(q + ".3.bias").v, 2 * C, H, false));
+                    if (c->mode == 1)
+                        e.dc.gram1b[d] = c->up_f32(conv1x1_moments(c->W(q + ".3.weight").v, c->W(q + ".3.bias").v, 2 * C, H, true));
                     e.dc.b1f[d] = c->up_key(q + ".3.bias");
                     e.dc.g2wf[d] = c->up_key(q + ".4.weight");
                     e.dc.g2bf[d] = c->up_key(q + ".4.bias");

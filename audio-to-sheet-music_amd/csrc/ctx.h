@@ -33,6 +33,7 @@ struct DConvW {
     // moments of the 1x1 conv for its GroupNorm statistics (dconv.hip c1stat): G = W^T W [H][H], v = W^T b [H],
     // ws = W^T 1 [H], sum b, sum b^2 (so sum_n y_n and sum_n y_n^2 of y = W h + b come from h alone)
     float* gram1[2] = {nullptr, nullptr};
+    float* gram1b[2] = {nullptr, nullptr};   // the same from the bf16-rounded weights (fenc_row.hip, bf16 mode)
 };
 
 struct EncW {
@@ -65,6 +66,34 @@ inline uint16_t host_f2bf(float f) {
     std::memcpy(&u, &f, 4);
     u += 0x7FFFu + ((u >> 16) & 1u);
     return (uint16_t)(u >> 16);
+}
+
+// Moments of a 1x1 conv W [N][H] (row-major), b [N] for GroupNorm statistics from its input alone:
+// [G = W^T W (H x H) | v = W^T b (H) | ws = W^T 1 (H) | sum b | sum b^2], accumulated in fp64; round_bf16: from the
+// bf16-rounded weights the MFMA kernels multiply with
+inline std::vector<float> conv1x1_moments(const std::vector<float>& w, const std::vector<float>& b, int N, int H,
+                                          bool round_bf16) {
+    std::vector<double> g((size_t)H * H + 2 * H + 2, 0.0);
+    auto wv = [&](int n, int j) -> double {
+        const float x = w[(size_t)n * H + j];
+        if (!round_bf16) return x;
+        const uint32_t u = (uint32_t)host_f2bf(x) << 16;
+        float r;
+        std::memcpy(&r, &u, 4);
+        return r;
+    };
+    for (int n = 0; n < N; ++n) {
+        const double bn = b[n];
+        for (int j = 0; j < H; ++j) {
+            const double wj = wv(n, j);
+            for (int k = 0; k < H; ++k) g[(size_t)j * H + k] += wj * wv(n, k);
+            g[(size_t)H * H + j] += bn * wj;
+            g[(size_t)H * H + H + j] += wj;
+        }
+        g[(size_t)H * H + 2 * H] += bn;
+        g[(size_t)H * H + 2 * H + 1] += bn * bn;
+    }
+    return std::vector<float>(g.begin(), g.end());
 }
 inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 inline int64_t rup(int64_t a, int64_t b) { return cdiv(a, b) * b; }

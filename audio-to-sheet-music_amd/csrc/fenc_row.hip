@@ -75,7 +75,9 @@ ATHD_DEV void gn_from_sums(float s1, float s2, float cnt, float& mean, float& rs
 
 // NW waves per workgroup (6 for C = 48, 12 for C = 96: one workgroup per CU either way at C = 96 (114 KB LDS), so
 // twice the waves per row halve each wave's m-tiles (and the residual stream's registers: 36 instead of 68))
-template <int CIN, int C, int NW>
+#define FR_SCHED() __builtin_amdgcn_sched_barrier(0)      // (no instruction is scheduled across it)
+// GRAM: the 1x1 output's GroupNorm statistics from the 1x1 conv's moments (d.gram) instead of a statistics pass
+template <int CIN, int C, int NW, bool GRAM>
 __global__ __launch_bounds__(NW * 64, CIN == 4 ? 3 : 1) void fenc_row_kernel(const FencRowDesc d) {
     constexpr int NCT = C / 16;                  // x channel tiles
     constexpr int MG = NW / NCT;              // m-tile groups per channel tile
@@ -102,6 +104,7 @@ __global__ __launch_bounds__(NW * 64, CIN == 4 ? 3 : 1) void fenc_row_kernel(con
     __shared__ __attribute__((aligned(16))) bf16_t xs[(TPM + 2 * FR_HALO) * XS_P];
     bf16_t* const hs = xin;
     __shared__ float red[4][2 * NW];
+    __shared__ float gsh[2][H * H + 2 * H + 2];  // the 1x1 convs' moments (when d.gram is set)
 
     // row r -> block: the 8 XCDs each take a contiguous run of rows, so neighbouring output rows (which share 4 of
     // their 8 input rows) run on one XCD and re-read those rows from its L2
@@ -118,6 +121,12 @@ __global__ __launch_bounds__(NW * 64, CIN == 4 ? 3 : 1) void fenc_row_kernel(con
     const int ct = wave % NCT, mg = wave / NCT;
     const int cb = ct * 16 + 4 * l4;             // first of this lane's 4 x channels
 
+    if constexpr (GRAM) {
+        for (int i = tid; i < 2 * (H * H + 2 * H + 2); i += NW * 64) {
+            const int l = i / (H * H + 2 * H + 2), e = i % (H * H + 2 * H + 2);
+            gsh[l][e] = d.gram[l][e];
+        }
+    }
     // zero xs (conv3 zero padding: halo rows and positions >= T)
     for (int i = tid; i < (TPM + 2 * FR_HALO) * XS_P / 8; i += (NW * 64))
         reinterpret_cast<uint4*>(xs)[i] = make_uint4(0u, 0u, 0u, 0u);
@@ -237,7 +246,46 @@ __global__ __launch_bounds__(NW * 64, CIN == 4 ? 3 : 1) void fenc_row_kernel(con
             }
             st4bf(&hs[(mt * 16 + l15) * HS_P + 4 * l4], g[0], g[1], g[2], g[3]);
         }
-        __syncthreads();
+        s1 = 0.f;
+        s2 = 0.f;
+        if constexpr (GRAM) {
+            // the 1x1 output's GroupNorm statistics from the moments of the 1x1 conv (see fenc_row0_kernel), one
+            // position per lane (l4 = 0) from the hidden rows this wave wrote (in-wave LDS order)
+            const float* G = gsh[dd];
+            if (l4 == 0) {
+#pragma unroll
+                for (int i = 0; i < C3I; ++i) {
+                    const int mt = wave + NW * i;
+                    if (mt >= MT || mt * 16 + l15 >= T) continue;
+                    FR_SCHED();
+                    float x[16];
+                    const uint4* hr_ = reinterpret_cast<const uint4*>(&hs[(mt * 16 + l15) * HS_P]);
+#pragma unroll
+                    for (int u = 0; u < (H + 7) / 8; ++u) {
+                        const uint4 hq = hr_[u];
+                        const uint32_t w4[4] = {hq.x, hq.y, hq.z, hq.w};
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) {
+                            x[8 * u + 2 * e] = __uint_as_float(w4[e] << 16);
+                            x[8 * u + 2 * e + 1] = __uint_as_float(w4[e] & 0xFFFF0000u);
+                        }
+                    }
+                    float q = 0.f, lv = 0.f, lw = 0.f;
+#pragma unroll 1
+                    for (int j = 0; j < H; ++j) {            // (rolled: G's rows are read from LDS per j)
+                        float t = 0.f;
+#pragma unroll
+                        for (int kk = 0; kk < H; ++kk) t += G[j * H + kk] * x[kk];
+                        q += x[j] * t;
+                        lv += G[H * H + j] * x[j];
+                        lw += G[H * H + H + j] * x[j];
+                    }
+                    s1 += G[H * H + 2 * H] + lw;
+                    s2 += G[H * H + 2 * H + 1] + (2.f * lv + q);
+                }
+            }
+        }
+        if constexpr (!GRAM) __syncthreads();
 
         // 1x1 (H -> 2C), GLU-interleaved rows: 'a' = 32 ct + l15, gate = 32 ct + 16 + l15; K = 32 (H zero-padded)
         const bf16x8_t wa = ldfrag(d.w1[dd] + (int64_t)(32 * ct + l15) * d.w1_ld + 8 * l4);
@@ -249,25 +297,25 @@ __global__ __launch_bounds__(NW * 64, CIN == 4 ? 3 : 1) void fenc_row_kernel(con
             ba[q] = d.b1[dd][pa + q];
             bg[q] = d.b1[dd][pa + 16 + q];
         }
-        s1 = 0.f;
-        s2 = 0.f;
+        if constexpr (!GRAM) {                      // statistics pass: the 1x1 computed once more
 #pragma unroll
-        for (int i = 0; i < MTW; ++i) {
-            const int mt = mg + MG * i;
-            const int m = mt * 16 + l15;
-            if (mt >= MT) continue;               // wave-uniform: the MFMAs run on full waves
-            const bf16x8_t hf = ldfrag(&hs[(mt * 16 + l15) * HS_P + 8 * l4]);
-            const f32x4_t z = f32x4_t{0.f, 0.f, 0.f, 0.f};
-            const f32x4_t ya = mfma(wa, hf, z), yg = mfma(wg, hf, z);
-            if (m >= T) continue;
+            for (int i = 0; i < MTW; ++i) {
+                const int mt = mg + MG * i;
+                const int m = mt * 16 + l15;
+                if (mt >= MT) continue;               // wave-uniform: the MFMAs run on full waves
+                const bf16x8_t hf = ldfrag(&hs[(mt * 16 + l15) * HS_P + 8 * l4]);
+                const f32x4_t z = f32x4_t{0.f, 0.f, 0.f, 0.f};
+                const f32x4_t ya = mfma(wa, hf, z), yg = mfma(wg, hf, z);
+                if (m >= T) continue;
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const float a = ya[q] + ba[q], g = yg[q] + bg[q];
-                s1 += a + g;
-                s2 += a * a + g * g;
+                for (int q = 0; q < 4; ++q) {
+                    const float a = ya[q] + ba[q], g = yg[q] + bg[q];
+                    s1 += a + g;
+                    s2 += a * a + g * g;
+                }
             }
         }
-        block_sum2<NW>(s1, s2, red[2 * dd + 1]);
+        block_sum2<NW>(s1, s2, red[2 * dd + 1]);      // (its barrier also publishes hs)
         float ym, yr;
         gn_from_sums(s1, s2, (float)(2 * C * T), ym, yr);
         float gwa[4], gba[4], gwg[4], gbg[4], sc[4];
@@ -404,7 +452,7 @@ ATHD_DEV float4 ld4f(const float* p) { return *reinterpret_cast<const float4*>(p
 // keeps the next m-tile's LDS fragment loads (and the MFMAs fed by them) below this point: without it the scheduler
 // hoists all nine tiles' loads and MFMAs of a pass for ILP and the pass needs ~200 VGPRs
 #define FR_PIN() asm volatile("" ::: "memory")
-#define FR_SCHED() __builtin_amdgcn_sched_barrier(0)      // (no instruction is scheduled across it)
+
 // the lane index made opaque per phase: per-tile LDS addresses and position masks are recomputed in each phase
 // instead of being computed once and held in registers across the whole kernel (~40 VGPRs)
 // a pointer the compiler cannot see through: loads from it stay in the phase that issues them (weights are
@@ -429,6 +477,7 @@ __global__ __launch_bounds__(FR_NT, 4) void fenc_row0_kernel(const FencRowDesc d
     __shared__ __attribute__((aligned(16))) bf16_t xs[(F0_TP + 2 * FR_HALO) * F0_XS_P];
     bf16_t* const hs = xin;
     __shared__ float red[4][2 * FR_NW];
+    __shared__ float gsh[2][52];                 // the 1x1 convs' moments (50 floats per layer)
 
     const int R = d.B * d.Fout;
     const int per = (R + 7) / 8;
@@ -460,6 +509,7 @@ __global__ __launch_bounds__(FR_NT, 4) void fenc_row0_kernel(const FencRowDesc d
     const bf16x8_t wf = ldfrag(d.wc + (int64_t)(ct * 16 + l15) * d.wc_ld + 8 * l4);
     const float4 bc = ld4f(d.bc + cb);
     const float sub = d.a_norm[2 * b], rdv = 1.0f / d.a_norm[2 * b + 1];
+    if (tid < 100) gsh[tid / 50][tid % 50] = d.gram[tid / 50][tid % 50];
     // halo rows of xs (conv3 zero padding); positions >= T are written as zeros by the conv epilogue
     if (tid < 2 * FR_HALO * F0_XS_P / 8) {
         const int hr = tid / (F0_XS_P / 8), hc = tid % (F0_XS_P / 8);
@@ -530,9 +580,6 @@ __global__ __launch_bounds__(FR_NT, 4) void fenc_row0_kernel(const FencRowDesc d
         float hb[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) hb[q] = d.b3[dd][min(4 * l4 + q, H - 1)];
-        const bf16x8_t wa = ldfrag(d.w1[dd] + (int64_t)(32 * ct + l15) * d.w1_ld + 8 * l4);
-        const bf16x8_t wg = ldfrag(d.w1[dd] + (int64_t)(32 * ct + 16 + l15) * d.w1_ld + 8 * l4);
-        const float4 ba = ld4f(d.b1[dd] + pa), bg = ld4f(d.b1[dd] + pa + 16);
         float s1 = 0.f, s2 = 0.f;
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
@@ -554,39 +601,54 @@ __global__ __launch_bounds__(FR_NT, 4) void fenc_row0_kernel(const FencRowDesc d
         block_sum2_dpp(s1, s2, red[2 * dd]);
         float hm, hr;
         gn_from_sums(s1, s2, (float)(H * T), hm, hr);
+        // GELU(GN(h)) -> hs (bf16); then the 1x1 output's GroupNorm statistics from the moments of the 1x1 conv
+        // (sum_n y = sum b + ws.x, sum_n y^2 = sum b^2 + 2 v.x + x^T G x over the bf16 x the MFMAs multiply), one
+        // position per lane (l4 = 0) from its hidden row: this replaces a full 1x1 MFMA pass over the row
+        const float* G = gsh[dd];
+        s1 = 0.f;
+        s2 = 0.f;
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
             const int mt = wave + FR_NW * i;
+            FR_SCHED();
             float g[4];
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const float v = gelu_fast((ha[i][q] + hb[q] - hm) * hr * g1w[q] + g1b[q]);
                 g[q] = 4 * l4 + q < H ? v : 0.f;
             }
-            st4bf(&hs[(mt * 16 + l15) * F0_HS_P + 4 * l4], g[0], g[1], g[2], g[3]);
+            *reinterpret_cast<uint2*>(&hs[(mt * 16 + l15) * F0_HS_P + 4 * l4]) =
+                make_uint2(pack2bf(g[0], g[1]), pack2bf(g[2], g[3]));
         }
-        __syncthreads();
-
-        // 1x1 (H -> 2C), GLU-interleaved rows; pass 1: GroupNorm statistics
-        const float bav[4] = {ba.x, ba.y, ba.z, ba.w}, bgv[4] = {bg.x, bg.y, bg.z, bg.w};
-        const int l15b = opaque_lane() & 15;
-        s1 = 0.f;
-        s2 = 0.f;
+        // (the hidden rows of this wave's positions were written by this wave: LDS order within a wave suffices)
+        if (l4 == 0) {
 #pragma unroll
-        for (int i = 0; i < MTW; ++i) {
-            const int mt = mg + 2 * i;
-            FR_SCHED();
-            const bf16x8_t hf = ldfrag(&hs[(mt * 16 + l15b) * F0_HS_P + 8 * l4]);
-            const f32x4_t z = f32x4_t{0.f, 0.f, 0.f, 0.f};
-            const f32x4_t ya = mfma(wa, hf, z), yg = mfma(wg, hf, z);
-            const bool ok = mt * 16 + l15b < T;
+            for (int i = 0; i < 3; ++i) {
+                const int mt = wave + FR_NW * i;
+                if (mt * 16 + l15 >= T) continue;
+                const uint4 hq = *reinterpret_cast<const uint4*>(&hs[(mt * 16 + l15) * F0_HS_P]);
+                const float x[6] = {__uint_as_float(hq.x << 16), __uint_as_float(hq.x & 0xFFFF0000u),
+                                    __uint_as_float(hq.y << 16), __uint_as_float(hq.y & 0xFFFF0000u),
+                                    __uint_as_float(hq.z << 16), __uint_as_float(hq.z & 0xFFFF0000u)};
+                float q = 0.f, lv = 0.f, lw = 0.f;
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const float a = ya[q] + bav[q], g = yg[q] + bgv[q];
-                s1 += ok ? a + g : 0.f;
-                s2 += ok ? a * a + g * g : 0.f;
+                for (int j = 0; j < 6; ++j) {
+                    float t = 0.f;
+#pragma unroll
+                    for (int kk = 0; kk < 6; ++kk) t += G[j * 6 + kk] * x[kk];
+                    q += x[j] * t;
+                    lv += G[36 + j] * x[j];
+                    lw += G[42 + j] * x[j];
+                }
+                s1 += G[48] + lw;
+                s2 += G[49] + (2.f * lv + q);
             }
         }
+        // the apply pass's 1x1 weights and GroupNorm affine (issued before the reduction's barrier)
+        const bf16x8_t wa = ldfrag(d.w1[dd] + (int64_t)(32 * ct + l15) * d.w1_ld + 8 * l4);
+        const bf16x8_t wg = ldfrag(d.w1[dd] + (int64_t)(32 * ct + 16 + l15) * d.w1_ld + 8 * l4);
+        const float4 ba = ld4f(d.b1[dd] + pa), bg = ld4f(d.b1[dd] + pa + 16);
+        const float bav[4] = {ba.x, ba.y, ba.z, ba.w}, bgv[4] = {bg.x, bg.y, bg.z, bg.w};
         const float4 gwa = ld4f(d.g2w[dd] + pa), gba = ld4f(d.g2b[dd] + pa);
         const float4 gwg = ld4f(d.g2w[dd] + pa + 16), gbg = ld4f(d.g2b[dd] + pa + 16);
         const float4 sc4 = ld4f(d.scale[dd] + cb);
@@ -695,10 +757,10 @@ int fenc_row_launch(const FencRowDesc& d, int cin, int c, hipStream_t s) {
         const char* e = std::getenv("ATHD_FENC_V1");
         v1 = e && *e && *e != '0' ? 1 : 0;
     }
-    if (cin == 4 && !v1 && d.T <= F0_TP) hipLaunchKernelGGL(fenc_row0_kernel, grid, dim3(FR_NT), 0, s, d);
-    else if (cin == 4) hipLaunchKernelGGL((fenc_row_kernel<4, 48, 6>), grid, dim3(6 * 64), 0, s, d);
-    else if (v1) hipLaunchKernelGGL((fenc_row_kernel<48, 96, 6>), grid, dim3(6 * 64), 0, s, d);
-    else hipLaunchKernelGGL((fenc_row_kernel<48, 96, 12>), grid, dim3(12 * 64), 0, s, d);
+    if (cin == 4 && !v1 && d.T <= F0_TP && d.gram[0] && d.gram[1]) hipLaunchKernelGGL(fenc_row0_kernel, grid, dim3(FR_NT), 0, s, d);
+    else if (cin == 4) hipLaunchKernelGGL((fenc_row_kernel<4, 48, 6, false>), grid, dim3(6 * 64), 0, s, d);
+    else if (v1 || !d.gram[0] || !d.gram[1]) hipLaunchKernelGGL((fenc_row_kernel<48, 96, 6, false>), grid, dim3(6 * 64), 0, s, d);
+    else hipLaunchKernelGGL((fenc_row_kernel<48, 96, 12, true>), grid, dim3(12 * 64), 0, s, d);
     return (int)hipGetLastError();
 }
 

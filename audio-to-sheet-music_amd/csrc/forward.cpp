@@ -338,6 +338,7 @@ void encode(Run& r, const Dims& d, const Bufs& b, const float* wav) {
                 fr.g1w[dd] = e.dc.g1w[dd]; fr.g1b[dd] = e.dc.g1b[dd];
                 fr.w1[dd] = (const uint16_t*)e.dc.c1[dd].w; fr.w1_ld = e.dc.c1[dd].Kp; fr.b1[dd] = e.dc.c1[dd].bias;
                 fr.g2w[dd] = e.dc.g2w[dd]; fr.g2b[dd] = e.dc.g2b[dd]; fr.scale[dd] = e.dc.scale[dd];
+                fr.gram[dd] = e.dc.gram1b[dd];
             }
             fr.wr = (const uint16_t*)e.rewrite.w; fr.wr_ld = e.rewrite.Kp; fr.br = e.rewrite.bias;
             fr.row_add = i == 0 ? c->femb : nullptr;

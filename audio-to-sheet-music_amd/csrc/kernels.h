@@ -117,6 +117,7 @@ struct FencRowDesc {
     const uint16_t* w1[2] = {nullptr, nullptr}; int w1_ld = 0;                    // 1x1 [2C][C/8] GLU-interleaved
     const float* b1[2] = {nullptr, nullptr};
     const float* g2w[2] = {nullptr, nullptr}; const float* g2b[2] = {nullptr, nullptr};   // packed order
+    const float* gram[2] = {nullptr, nullptr};    // 1x1 moments (ctx.h conv1x1_moments, bf16-rounded weights)
     const float* scale[2] = {nullptr, nullptr};
     const uint16_t* wr = nullptr; int wr_ld = 0; const float* br = nullptr;      // rewrite [2C][C] GLU-interleaved
     const float* row_add = nullptr;    // level 0: freq embedding [Fout][C]
