@@ -49,6 +49,15 @@ ATHD_DEV float gelu_fast(float x) {
 }
 template <bool FAST>
 ATHD_DEV float gelu(float x) { if constexpr (FAST) return gelu_fast(x); else return gelu_erf(x); }
+// gelu_fast on a pair: the polynomial and scaling on packed f32 ops (v_pk_mul / v_pk_fma), exp2 / rcp per lane
+ATHD_DEV athd_f2v gelu_fast_pk(athd_f2v x) {
+    const athd_f2v c1 = {0.044715f * 1.5957691216057308f, 0.044715f * 1.5957691216057308f};
+    const athd_f2v c0 = {1.5957691216057308f, 1.5957691216057308f};
+    const athd_f2v u = x * __builtin_elementwise_fma(c1, x * x, c0);
+    const athd_f2v t = u * (athd_f2v){-1.4426950408889634f, -1.4426950408889634f};
+    const athd_f2v den = (athd_f2v){__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)} + (athd_f2v){1.0f, 1.0f};
+    return x * (athd_f2v){__builtin_amdgcn_rcpf(den.x), __builtin_amdgcn_rcpf(den.y)};
+}
 ATHD_DEV float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
 // bf16-mode sigmoid: v_exp_f32 + v_rcp_f32 (~1 ulp each; 4 instructions vs ~25 for expf and an IEEE divide).  The
 // f32 parity mode keeps sigmoidf_.

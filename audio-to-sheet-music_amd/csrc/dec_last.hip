@@ -312,6 +312,11 @@ template <> struct Slice12<true> {
         const uint32_t w = (j & 2) ? q.y : q.x;
         return (j & 1) ? __uint_as_float(w & 0xFFFF0000u) : __uint_as_float(w << 16);
     }
+    ATHD_DEV athd_f2v get2(int r, int sp) const {        // channels 2 sp, 2 sp + 1
+        const uint2 q = v[r][sp >> 1];
+        const uint32_t w = (sp & 1) ? q.y : q.x;
+        return (athd_f2v){__uint_as_float(w << 16), __uint_as_float(w & 0xFFFF0000u)};
+    }
 };
 template <> struct Slice12<false> {
     float4 v[4][3];
@@ -369,6 +374,13 @@ __global__ __launch_bounds__(256) void fdec_tail_kernel(const DecLastDesc d, int
         gw[s] = d.gn_w[ch0 + s];
         gb[s] = d.gn_b[ch0 + s];
     }
+    // bf16 mode: the GroupNorm affine folded into one FMA (a = rstd w, c = b - mean a) on channel pairs
+    athd_f2v ga2[6], gc2[6];
+#pragma unroll
+    for (int sp = 0; sp < 6; ++sp) {
+        ga2[sp] = (athd_f2v){rstd * gw[2 * sp], rstd * gw[2 * sp + 1]};
+        gc2[sp] = (athd_f2v){gb[2 * sp], gb[2 * sp + 1]} - (athd_f2v){mean, mean} * ga2[sp];
+    }
     const float* F = d.fold;
     const float* cst = F + 6 * DL_C;
     const float* S = F + 6 * DL_C + 2;
@@ -390,13 +402,27 @@ __global__ __launch_bounds__(256) void fdec_tail_kernel(const DecLastDesc d, int
         const LinIdx li = lin_index(u, 4 * H, H);
         const LinIdx lj = lin_index(u, d.H_skip2, H);
         f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+        if constexpr (BF) {
+            const athd_f2v l0 = {li.l0, li.l0}, l1 = {li.l1, li.l1}, k0 = {lj.l0, lj.l0}, k1 = {lj.l1, lj.l1};
 #pragma unroll
-        for (int s = 0; s < 12; ++s) {
-            const float va = gn_act<BF>(r.get(0, s), mean, rstd, gw[s], gb[s]);
-            const float vb = gn_act<BF>(r.get(1, s), mean, rstd, gw[s], gb[s]);
-            const float sv = (lj.l0 * r.get(2, s) + lj.l1 * r.get(3, s)) * 0.1f;
-            const float x = (li.l0 * va + li.l1 * vb) + sv;
-            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wA[s], x, acc, 0, 0, 0);
+            for (int sp = 0; sp < 6; ++sp) {
+                const athd_f2v va = gelu_fast_pk(__builtin_elementwise_fma(r.get2(0, sp), ga2[sp], gc2[sp]));
+                const athd_f2v vb = gelu_fast_pk(__builtin_elementwise_fma(r.get2(1, sp), ga2[sp], gc2[sp]));
+                const athd_f2v sv = __builtin_elementwise_fma(k0, r.get2(2, sp), k1 * r.get2(3, sp)) *
+                                    (athd_f2v){0.1f, 0.1f};
+                const athd_f2v x = __builtin_elementwise_fma(l0, va, l1 * vb) + sv;
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wA[2 * sp], x.x, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wA[2 * sp + 1], x.y, acc, 0, 0, 0);
+            }
+        } else {
+#pragma unroll
+            for (int s = 0; s < 12; ++s) {
+                const float va = gn_act<BF>(r.get(0, s), mean, rstd, gw[s], gb[s]);
+                const float vb = gn_act<BF>(r.get(1, s), mean, rstd, gw[s], gb[s]);
+                const float sv = (lj.l0 * r.get(2, s) + lj.l1 * r.get(3, s)) * 0.1f;
+                const float x = (li.l0 * va + li.l1 * vb) + sv;
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wA[s], x, acc, 0, 0, 0);
+            }
         }
         return acc;
     };

@@ -122,6 +122,9 @@ struct FencRowDesc {
     const uint16_t* wr = nullptr; int wr_ld = 0; const float* br = nullptr;      // rewrite [2C][C] GLU-interleaved
     const float* row_add = nullptr;    // level 0: freq embedding [Fout][C]
     uint16_t* out = nullptr;           // [B][Fout][T][C] bf16
+    int probe = 0;                     // measurement probe (ATHD_FR_PROBE, fenc_row0_kernel): bit 0 no input loads,
+                                       // bit 1 no DConv, bit 2 no output stores, bit 3 no conv3 MFMAs, bit 4 no
+                                       // apply pass, bit 5 no workgroup reductions (results are garbage)
 };
 bool fenc_row_supported(int cin, int c, int T);
 int fenc_row_launch(const FencRowDesc& d, int cin, int c, hipStream_t s);

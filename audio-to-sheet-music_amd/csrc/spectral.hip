@@ -336,7 +336,8 @@ ATHD_DEV float* ola_part(float* part, int64_t item, int nwg, int k, int side, in
 
 // FAST (R = float, the bf16 throughput mode): the mask's sigmoid and phase division and the envelope division use
 // v_exp / v_rcp (~1 ulp) instead of the IEEE sequences; the f32 parity mode (R = double) keeps them exact.
-template <typename R, typename TW, int MINW>
+// PF: the next frame's spectrum is prefetched into registers during the current frame's FFT (32 VGPRs)
+template <typename R, typename TW, int MINW, bool PF = true>
 __global__ __launch_bounds__(256, MINW) void istft_ola_kernel(const float* __restrict__ fo, int Tspec, int P, int T,
                                                            const float* __restrict__ specT, const TW* __restrict__ tw,
                                                            const float* __restrict__ win,
@@ -399,7 +400,7 @@ __global__ __launch_bounds__(256, MINW) void istft_ola_kernel(const float* __res
 #pragma unroll
         for (int o = 0; o < 4; ++o) acc[3][o][0] = acc[3][o][1] = 0.f;
     };
-    load_spec(t0);
+    if constexpr (PF) load_spec(t0);
     __syncthreads();                                       // ltab
 #pragma unroll 1
     for (int t = t0; t < t1; ++t) {
@@ -419,7 +420,9 @@ __global__ __launch_bounds__(256, MINW) void istft_ola_kernel(const float* __res
             const float xd0 = l0 * ra.x + l1 * rb.x;
             const float xd1 = l0 * ra.y + l1 * rb.y;
             const float m0 = sigmoid<FAST>(xd0), m1 = sigmoid<FAST>(xd1);
-            const float4 z = zs[i];
+            float4 z;
+            if constexpr (PF) z = zs[i];
+            else z = *reinterpret_cast<const float4*>(specT + ((b * Tspec + t) * 2048LL + kb) * 4);
             const float ms0 = z.x * m0, ms1 = z.y * m1;
             const float d0 = z.x + 1e-8f, d1 = z.y + 1e-8f;
             cpx X0, X1;
@@ -440,7 +443,9 @@ __global__ __launch_bounds__(256, MINW) void istft_ola_kernel(const float* __res
             }
         }
         if (j == 0) buf[pidx(2048)] = {0.f, 0.f};
-        if (t + 1 < t1) load_spec(t + 1);                  // next frame's spectrum, in flight during the FFT
+        if constexpr (PF) {
+            if (t + 1 < t1) load_spec(t + 1);              // next frame's spectrum, in flight during the FFT
+        }
         __syncthreads();
         cx<R> v[16];
 #pragma unroll
@@ -512,20 +517,27 @@ void istft_ola_launch(const float* fo, int NI, int Tspec, int P, int64_t T, cons
             ks.begin("istft_ola_kernel", 0.0,
                      (double)NI * Tspec * Tspec * 2 * 4 + (double)(NI / P) * 2048 * Tspec * 4 * 4 + (double)NI * T * 2 * 4 +
                          (double)NI * 2 * T * 4);
-        static int minw = -1;
-        if (minw < 0) {
-            const char* e = std::getenv("ATHD_ISTFT_MINW");
-            minw = e && *e == '3' ? 3 : 2;      // 2 waves/SIMD (181 VGPRs, no spill): 1766 vs 1996 us at 3 (60 B spill)
+        static int var = -1;
+        if (var < 0) {
+            const char* e = std::getenv("ATHD_ISTFT_VAR");     // measurement override: 0 = <2, prefetch>,
+            var = e && *e ? std::atoi(e) : 2;                 // 1 = <3, prefetch>, 2 = <3, no prefetch> (default:
+                                                              // 1512 vs 1781 us for 0), 3 = <2, no pf>
         }
         if (tw64)
             hipLaunchKernelGGL((istft_ola_kernel<double, double2, 3>), grid, dim3(256), 0, s, fo, Tspec, P, (int)T, spec,
                                tw64, win, win2, xt2, tnorm, out, part, nwg, units);
-        else if (minw == 2)
-            hipLaunchKernelGGL((istft_ola_kernel<float, float2, 2>), grid, dim3(256), 0, s, fo, Tspec, P, (int)T, spec, tw,
-                               win, win2, xt2, tnorm, out, part, nwg, units);
+        else if (var == 1)
+            hipLaunchKernelGGL((istft_ola_kernel<float, float2, 3, true>), grid, dim3(256), 0, s, fo, Tspec, P, (int)T,
+                               spec, tw, win, win2, xt2, tnorm, out, part, nwg, units);
+        else if (var == 2)
+            hipLaunchKernelGGL((istft_ola_kernel<float, float2, 3, false>), grid, dim3(256), 0, s, fo, Tspec, P, (int)T,
+                               spec, tw, win, win2, xt2, tnorm, out, part, nwg, units);
+        else if (var == 3)
+            hipLaunchKernelGGL((istft_ola_kernel<float, float2, 2, false>), grid, dim3(256), 0, s, fo, Tspec, P, (int)T,
+                               spec, tw, win, win2, xt2, tnorm, out, part, nwg, units);
         else
-            hipLaunchKernelGGL((istft_ola_kernel<float, float2, 3>), grid, dim3(256), 0, s, fo, Tspec, P, (int)T, spec, tw,
-                               win, win2, xt2, tnorm, out, part, nwg, units);
+            hipLaunchKernelGGL((istft_ola_kernel<float, float2, 2, true>), grid, dim3(256), 0, s, fo, Tspec, P, (int)T,
+                               spec, tw, win, win2, xt2, tnorm, out, part, nwg, units);
     }
     if (nwg > 1) {
         const dim3 grid((unsigned)(3 * (nwg - 1)), (unsigned)NI);
