@@ -545,8 +545,19 @@ __global__ __launch_bounds__(TL_NT) void tdec_tail_kernel(const DecLastDesc d) {
         const int rr = i / (DL_C / 8), q = i % (DL_C / 8);
         float a[8];
         ld8(d.g, BF, gb + (int64_t)rr * DL_C + 8 * q, a);
+        if constexpr (BF) {            // GroupNorm affine folded into one FMA, GELU pairs on packed ops
 #pragma unroll
-        for (int j = 0; j < 8; ++j) a[j] = gn_act<BF>(a[j], mean, rstd, d.gn_w[8 * q + j], d.gn_b[8 * q + j]);
+            for (int j = 0; j < 8; j += 2) {
+                const athd_f2v ga = (athd_f2v){d.gn_w[8 * q + j], d.gn_w[8 * q + j + 1]} * (athd_f2v){rstd, rstd};
+                const athd_f2v gc = (athd_f2v){d.gn_b[8 * q + j], d.gn_b[8 * q + j + 1]} - (athd_f2v){mean, mean} * ga;
+                const athd_f2v v = gelu_fast_pk(__builtin_elementwise_fma((athd_f2v){a[j], a[j + 1]}, ga, gc));
+                a[j] = v.x;
+                a[j + 1] = v.y;
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) a[j] = gn_act<BF>(a[j], mean, rstd, d.gn_w[8 * q + j], d.gn_b[8 * q + j]);
+        }
         TtRow<BF>::put8(gsm, rr, 8 * q, a);
     }
     __syncthreads();

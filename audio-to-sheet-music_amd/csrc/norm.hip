@@ -486,10 +486,18 @@ __global__ __launch_bounds__(256) void dec_merge_w1_kernel(const MergeDesc d) {
         auto act_row = [&](int p, int row, float* x) {
             ldv<8>(d.src, d.src_bf16, (seg * P + p0 + p) * src_item + (int64_t)row * d.C + c, x);
             if (gn) {
+                if constexpr (FAST) {      // GroupNorm affine folded into one FMA, GELU pairs on packed ops
 #pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    const float u = (x[j] - mean[p]) * rstd[p] * gw[j] + gb[j];
-                    x[j] = FAST ? gelu_fast(u) : gelu_erf(u);
+                    for (int j = 0; j < 8; j += 2) {
+                        const athd_f2v ga = (athd_f2v){gw[j], gw[j + 1]} * (athd_f2v){rstd[p], rstd[p]};
+                        const athd_f2v gc = (athd_f2v){gb[j], gb[j + 1]} - (athd_f2v){mean[p], mean[p]} * ga;
+                        const athd_f2v v = gelu_fast_pk(__builtin_elementwise_fma((athd_f2v){x[j], x[j + 1]}, ga, gc));
+                        x[j] = v.x;
+                        x[j + 1] = v.y;
+                    }
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) x[j] = gelu_erf((x[j] - mean[p]) * rstd[p] * gw[j] + gb[j]);
                 }
             }
         };
