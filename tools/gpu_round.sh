@@ -6,6 +6,7 @@ O=gpurun_out
 mkdir -p $O
 export TMPDIR=/tmp
 step() { echo "== $1"; }
+if [ -z "$SKIP_PYTEST" ]; then
 step pytest
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -rA -p no:cacheprovider --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1
 rc=$?; grep -E "passed|failed" $O/pytest_gpu.log | tail -2
@@ -13,6 +14,7 @@ if [ $rc -gt 1 ]; then tail -30 $O/pytest_gpu.log; exit $rc; fi
 step bench
 timeout -k 10 600 python bench.py > $O/bench_full.log 2>&1 || { tail -20 $O/bench_full.log; exit 1; }
 tail -1 $O/bench_full.log
+fi
 step kernel-trace
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$TAG -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline > $O/prof_$TAG.log 2>&1 || { tail -20 $O/prof_$TAG.log; exit 1; }
 tail -1 $O/prof_$TAG.log

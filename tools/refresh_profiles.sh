@@ -12,5 +12,5 @@ python tools/prof_summary.py $O/prof_${TAG}_serial > $P/${TAG}_kernel_summary_se
 python tools/prof_sections.py $O/prof_${TAG}_serial > $P/${TAG}_sections_serial.txt
 cp $O/pmc_traffic.json $P/pmc_traffic.json
 python tools/pmc_traffic.py $O/pmc_fetch_$TAG $O/pmc_write_$TAG --batch 64 --dtype bf16 -o /tmp/pmc_traffic.json > $P/${TAG}_pmc_traffic_top.txt
-tail -1 $O/bench_full.log > $P/${TAG}_bench.json
+[ -f $O/bench_full.log ] && tail -1 $O/bench_full.log > $P/${TAG}_bench.json
 tail -1 $O/bench_traffic.log | sed 's#gpurun_out/pmc_traffic.json#profiles/pmc_traffic.json#' > $P/${TAG}_bench_traffic.json
