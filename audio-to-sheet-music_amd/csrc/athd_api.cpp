@@ -348,6 +348,21 @@ int athd_finalize(athd_ctx* c) {
                     }
                 }
                 dw.quad = c->up_gemm(q, co4, K3, qb);
+                if (c->mode == 1 && convt4_supported(dw.cin, dw.cout, 1)) {
+                    // convt4.hip: per row the residue pair's two input rows only (K = 2 cin)
+                    const int K2 = 2 * dw.cin;
+                    std::vector<uint16_t> q2((size_t)co4 * K2);
+                    for (int r = 0; r < 4; ++r) {
+                        const int ta = RES_OFF[r] + 1;
+                        for (int co = 0; co < dw.cout; ++co)
+                            for (int k = 0; k < K2; ++k)
+                                q2[(size_t)(r * dw.cout + co) * K2 + k] =
+                                    host_f2bf(q[(size_t)(r * dw.cout + co) * K3 + (size_t)ta * dw.cin + k]);
+                    }
+                    dw.ct4w = c->dalloc<uint16_t>(q2.size());
+                    c->h2d(dw.ct4w, q2.data(), q2.size() * 2);
+                    dw.ct4b = c->up_f32(b);
+                }
             }
             if (br == 0 && i == 1) {                  // [k*cout + co][ci] for the re-associated level 1
                 std::vector<float> tk((size_t)8 * dw.cout * dw.cin);

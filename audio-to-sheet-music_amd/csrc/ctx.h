@@ -53,6 +53,8 @@ struct DecW {
     int cin = 0, cout = 0;
     GemmW pair[2];          // ConvTranspose residue pairs {0,1} (taps u-1,u) and {2,3} (taps u,u+1), N = 2*cout
     GemmW quad;             // levels 2: all four residues in one GEMM, rows [rho * cout + co], K = [row u-1 | u | u+1]
+    uint16_t* ct4w = nullptr;   // level 2, bf16 mode: [rho * cout + co][2 cin] = the residue pair's two rows (convt4.hip)
+    float* ct4b = nullptr;      //   and the bias [cout]
     GemmW taps;             // freq level 1 only: every tap as its own column block, N = 8*cout, K = cin (fdec_lr.hip)
     float* bias = nullptr;  // freq level 1 only: ConvT bias [cout]
     float *gnw = nullptr, *gnb = nullptr;

@@ -530,9 +530,27 @@ void encode(Run& r, const Dims& d, const Bufs& b, const float* wav) {
 // u-1, u; rows 4u+{2,3} read u, u+1.  Each GEMM has N = 2*cout (columns >= cout belong to the odd residue).
 // keep < 0: store all rows (4*H_in rows).  keep > 0: store only rows 4u+1, 4u+2 as slots 2u, 2u+1 (the only
 // rows the following exact /4 bilinear resize reads); statistics (if st) still cover all four residues.
+// ATHD_CONVT4=0: the four-residue ConvT on the tiled GEMM (gemm3) instead of convt4.hip (A/B measurement)
+static bool conv_t4_off() {
+    static int off = -1;
+    if (off < 0) {
+        const char* e = std::getenv("ATHD_CONVT4");
+        off = e && *e == '0' ? 1 : 0;
+    }
+    return off == 1;
+}
+
 void conv_t(Run& r, const DecW& w, const void* A, int a_bf16, int nb, int H_in, int W, void* out, int out_bf16,
             double* st, int keep, const char* stage) {
     KStage kst(stage);
+    if (w.ct4w && a_bf16 && out_bf16 && convt4_supported(w.cin, w.cout, (int64_t)nb * H_in * W) && !conv_t4_off()) {
+        // dedicated pass (convt4.hip): weights resident in LDS, barrier-free waves over 32-row units
+        ConvT4Desc q;
+        q.x = (const uint16_t*)A; q.w = w.ct4w; q.bias = w.ct4b; q.out = (uint16_t*)out; q.stats = st;
+        q.nb = nb; q.H = H_in; q.W = W; q.keep = keep < 0 ? 0 : 1;
+        r.check(convt4_launch(q, r.s), "convt4");
+        return;
+    }
     if (w.quad.w) {
         // all four residues in one GEMM (N = 4 cout, K = rows u-1 | u | u+1): the input is read once
         GemmDesc g;

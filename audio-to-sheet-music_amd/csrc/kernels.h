@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "gemm.h"
+
 namespace athd {
 
 // demucs pad1d(reflect) plan for HTDemucs._spec: padded index p -> original sample (or 0)
@@ -153,6 +155,23 @@ int tdec_last_launch(const DecLastDesc& d, hipStream_t s);
 int fdec_tail_launch(const DecLastDesc& d, hipStream_t s);
 bool tdec_tail_supported(const DecLastDesc& d);     // 4 H == T and every block's g rows fit its LDS tile
 int tdec_tail_launch(const DecLastDesc& d, hipStream_t s);
+// convt4.hip: decoder level-2 ConvTranspose (96 -> 48, k8 s4 p2) over rows (b, u, w) of x [nb][H][W][96] bf16, all
+// four residues in one pass (bf16 mode).  w: [4 x 48 rows][192] bf16, row rho*48 + co, K = the residue pair's two
+// input rows (u-1 | u for rho 0/1, u | u+1 for rho 2/3) x 96 channels; bias [48].  keep = 1: residues 1, 2 stored as
+// rows 2t, 2t+1 of out [nb][2H][W][48]; keep = 0: out [nb][4H][W][48].  stats: per item fp64 {sum, sumsq} over all
+// four residues (accumulated).
+struct ConvT4Desc {
+    const uint16_t* x = nullptr;
+    const uint16_t* w = nullptr;
+    const float* bias = nullptr;
+    uint16_t* out = nullptr;
+    double* stats = nullptr;
+    int nb = 0, H = 0, W = 1, keep = 0;
+    uint32_t M = 0;                       // filled by convt4_launch
+    FastDivU fd_w, fd_h, fd_hw;           // filled by convt4_launch
+};
+bool convt4_supported(int cin, int cout, int64_t M);
+int convt4_launch(const ConvT4Desc& d, hipStream_t s);
 // dconv.hip: one DConv layer (conv3 -> GN -> GELU -> 1x1 -> GN -> GLU -> LayerScale -> residual) for C in {48, 96}
 // x: [nb][L][C] f32 or bf16 (x_bf16), updated in place; h: [nb][L][C/8] f32 scratch
 int dconv_small_launch(void* x, int x_bf16, float* h, int64_t nb, int64_t L, int C, int dil, const float* w3,

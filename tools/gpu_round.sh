@@ -16,15 +16,15 @@ timeout -k 10 600 python bench.py > $O/bench_full.log 2>&1 || { tail -20 $O/benc
 tail -1 $O/bench_full.log
 fi
 step kernel-trace
-timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$TAG -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline > $O/prof_$TAG.log 2>&1 || { tail -20 $O/prof_$TAG.log; exit 1; }
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$TAG -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-extras > $O/prof_$TAG.log 2>&1 || { tail -20 $O/prof_$TAG.log; exit 1; }
 tail -1 $O/prof_$TAG.log
 step kernel-trace-serial
-ATHD_SERIAL=1 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_${TAG}_serial -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline > $O/prof_${TAG}_serial.log 2>&1 || { tail -20 $O/prof_${TAG}_serial.log; exit 1; }
+ATHD_SERIAL=1 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_${TAG}_serial -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-extras > $O/prof_${TAG}_serial.log 2>&1 || { tail -20 $O/prof_${TAG}_serial.log; exit 1; }
 tail -1 $O/prof_${TAG}_serial.log | cut -c1-200
 step pmc-fetch
-timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch_$TAG -o run -- python bench.py --steps 1 --warmup 1 --no-cpu-baseline > $O/pmc_fetch_$TAG.log 2>&1 || { tail -20 $O/pmc_fetch_$TAG.log; exit 1; }
+timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch_$TAG -o run -- python bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-extras > $O/pmc_fetch_$TAG.log 2>&1 || { tail -20 $O/pmc_fetch_$TAG.log; exit 1; }
 step pmc-write
-timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write_$TAG -o run -- python bench.py --steps 1 --warmup 1 --no-cpu-baseline > $O/pmc_write_$TAG.log 2>&1 || { tail -20 $O/pmc_write_$TAG.log; exit 1; }
+timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write_$TAG -o run -- python bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-extras > $O/pmc_write_$TAG.log 2>&1 || { tail -20 $O/pmc_write_$TAG.log; exit 1; }
 python tools/pmc_traffic.py $O/pmc_fetch_$TAG $O/pmc_write_$TAG --batch 64 --dtype bf16 -o $O/pmc_traffic.json || exit 1
 step pmc-sq
 timeout -s KILL 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE --output-format csv -d $O/pmc_sqa_$TAG -o run -- python bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-extras > $O/pmc_sqa_$TAG.log 2>&1 || { tail -20 $O/pmc_sqa_$TAG.log; exit 1; }
