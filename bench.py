@@ -49,7 +49,13 @@ def pmc_traffic(kernel, batch, dtype):
         return None, None
     if d.get("batch") != batch or d.get("dtype") != dtype:
         return None, None
-    k = d.get("kernels", {}).get(kernel)
+    ks = d.get("kernels", {})
+    k = ks.get(kernel)
+    if k is None:
+        # the library labels some kernels without their template arguments (attn32_kernel); rocprofv3 names the
+        # instantiation: accept the one instantiation of that name
+        inst = [v for n, v in ks.items() if n.split("<", 1)[0] == kernel]
+        k = inst[0] if len(inst) == 1 else None
     return (k["hbm_bytes_per_launch"], os.path.relpath(PMC_FILE, REPO)) if k else (None, None)
 
 
