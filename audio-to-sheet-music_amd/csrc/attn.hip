@@ -471,10 +471,16 @@ __global__ __launch_bounds__(256, 3) void attn_bf16_kernel(const AttnDesc d) {
 //
 // LDS: K [key][72] (row reads, conflict-free per 8 lanes), V [key][64] with the 16-B chunk XOR-swizzled by
 // ((key >> 1) & 1) << 2 so that each 32-lane half of a transposed read (4 keys x 32 d) covers all 64 banks.  2-deep
-// ring, register-staged prefetch (issue before the tile's MFMAs, LDS write after), one barrier per tile.  The output
-// tile is staged through LDS and stored as whole 128-B rows.
+// ring filled by LDS-DMA for the next tile before the tile's MFMAs (register-staged variant: global loads before, LDS
+// writes after), one barrier per tile.  The output tile is staged through LDS and stored as whole 128-B rows.
 typedef __attribute__((ext_vector_type(16))) float f32x16_t;
 typedef __attribute__((ext_vector_type(4))) unsigned int u32x4_t;   // (arrays of these stay in registers)
+
+// s_setprio(1) around the QK^T and PV MFMA clusters (cdna_hip_programming.md T5): a wave in its MFMA cluster wins
+// issue arbitration over the co-resident waves' softmax VALU; kbench A/B on one box: +3.3 % (N=2072), +4.6 % (N=1034)
+#define A32_PRIO(x) __builtin_amdgcn_s_setprio(x)
+typedef __attribute__((address_space(3))) void a32_lds_void;
+typedef __attribute__((address_space(1))) void a32_gbl_void;
 
 constexpr int A32_KP = 72;                          // K row pitch (bf16)
 constexpr int A32_VP = 64;                          // V row pitch (bf16), swizzled chunks
@@ -505,7 +511,7 @@ ATHD_DEV float vmax3(float a, float b, float c) {
             _Pragma("unroll") for (int i = 0; i < 16; ++i) sc[kb][i] = init_;                                  \
         _Pragma("unroll") for (int ks = 0; ks < 4; ++ks)                                                      \
             _Pragma("unroll") for (int kb = 0; kb < NKB; ++kb) {                                              \
-                const bf16v8 a_ = *reinterpret_cast<const bf16v8*>(&K_[(32 * kb + r) * A32_KP + 16 * ks + 8 * hh]); \
+                const bf16v8 a_ = *reinterpret_cast<const bf16v8*>(&K_[a32_kidx<DMA>(32 * kb + r, 2 * ks + hh)]); \
                 sc[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_, qf[ks], sc[kb], 0, 0, 0);                 \
             }                                                                                                  \
         if (kt0 + KT > d.Nk) {                                                                                 \
@@ -514,13 +520,31 @@ ATHD_DEV float vmax3(float a, float b, float c) {
                     if (kt0 + 32 * kb + (i & 3) + 8 * (i >> 2) + 4 * hh >= d.Nk) sc[kb][i] = -INFINITY;        \
         }                                                                                                      \
     } while (0)
-template <int MINW, int NKB>
+// K tile element index of (key, 16-B chunk).  Register-staged: row pitch 72 (padding).  LDS-DMA staged: pitch 64,
+// chunk XOR-swizzled by (key >> 1) & 7 - the QK^T fragment reads (lanes = 32 consecutive keys, one chunk) then put the
+// 16 lanes of every ds_read_b128 group on 16 distinct 4-bank groups (key & 1 picks the bank half of the 128-B row).
+template <bool DMA>
+ATHD_DEV int a32_kidx(int key, int chunk) {
+    if constexpr (DMA) return key * 64 + 8 * (chunk ^ ((key >> 1) & 7));
+    else return key * A32_KP + 8 * chunk;
+}
+
+// DMA: K / V tiles staged by global_load_lds_dwordx4 straight into LDS (no VGPR round trip and none of the
+// ds_write_b128 transfer cost, which with 4 waves' 16 KB of fragment reads per tile kept the LDS ~90 % busy).  One
+// wave instruction fills 1 KB = 8 keys x 128 B, lane -> (key base + lane / 8, physical chunk lane % 8); the lane fetches
+// the logical chunk that the tile's swizzle places there.
+template <int MINW, int NKB, bool DMA = false>
 __global__ __launch_bounds__(256, MINW) void attn32_kernel(const AttnDesc d) {
     constexpr int KT = 32 * NKB;                                  // keys per tile
-    __shared__ __attribute__((aligned(16))) bf16_t Ks[2][KT * A32_KP];
-    __shared__ __attribute__((aligned(16))) bf16_t Vs[2][KT * A32_VP];
+    constexpr int KSZ = KT * (DMA ? 64 : A32_KP);                 // K slot elements
+    // K ring, V ring; the output staging (4 waves x 32 rows x 72) reuses the front
+    constexpr int SMEM_E = 2 * KSZ + 2 * KT * A32_VP;
+    static_assert(SMEM_E >= 4 * 32 * A32_KP, "output staging fits");
+    __shared__ __attribute__((aligned(16))) bf16_t smem_a32[SMEM_E];
+    bf16_t (*Ks)[KSZ] = reinterpret_cast<bf16_t (*)[KSZ]>(smem_a32);
+    bf16_t (*Vs)[KT * A32_VP] = reinterpret_cast<bf16_t (*)[KT * A32_VP]>(smem_a32 + 2 * KSZ);
 
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int r = lane & 31, hh = lane >> 5;
     int qblk, h;
     int64_t b;
@@ -551,8 +575,19 @@ __global__ __launch_bounds__(256, MINW) void attn32_kernel(const AttnDesc d) {
 #define ATHD_A32_STASH(ST)                                                                                     \
     _Pragma("unroll") for (int j = 0; j < NKB; ++j) {                                                         \
         const int key = skey + 32 * j;                                                                         \
-        *reinterpret_cast<u32x4_t*>(&Ks[ST][key * A32_KP + 8 * sch]) = kr[j];                                    \
+        *reinterpret_cast<u32x4_t*>(&Ks[ST][a32_kidx<false>(key, sch)]) = kr[j];                                 \
         *reinterpret_cast<u32x4_t*>(&Vs[ST][key * A32_VP + 8 * a32_vchunk(key, sch)]) = vr[j];                   \
+    }
+    // LDS-DMA staging of tile KT0 into slot ST: wave w fills keys 8 (w + 4 j) .. +7 of K and of V, j < KT / 32
+    const int dkey = lane >> 3, dph = lane & 7;
+#define ATHD_A32_DMA(KT0, ST)                                                                                  \
+    _Pragma("unroll") for (int j = 0; j < KT / 32; ++j) {                                                     \
+        const int kk = 8 * (wave + 4 * j) + dkey;                                                              \
+        const int ka = min((KT0) + kk, d.Nk - 1);                                                              \
+        __builtin_amdgcn_global_load_lds((a32_gbl_void*)(Kb + (int64_t)ka * d.k_ld + 8 * (dph ^ ((kk >> 1) & 7))), \
+                                         (a32_lds_void*)&Ks[ST][8 * (wave + 4 * j) * 64], 16, 0, 0);            \
+        __builtin_amdgcn_global_load_lds((a32_gbl_void*)(Vb + (int64_t)ka * d.v_ld + 8 * a32_vchunk(kk, dph)),  \
+                                         (a32_lds_void*)&Vs[ST][8 * (wave + 4 * j) * A32_VP], 16, 0, 0);       \
     }
 
     // transposed-read addresses (elements): lane 4q'+p of 16-lane group g' -> key row 4h + q' (+8, +16 s2, +32 kb),
@@ -572,7 +607,10 @@ __global__ __launch_bounds__(256, MINW) void attn32_kernel(const AttnDesc d) {
     float mrun = 0.f, lrun = 0.f;
 
     const int ntiles = (d.Nk + KT - 1) / KT;
-    {
+    if constexpr (DMA) {
+        ATHD_A32_DMA(0, 0)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
         u32x4_t kr[NKB], vr[NKB];
         ATHD_A32_FETCH(0)
         ATHD_A32_STASH(0)
@@ -584,7 +622,12 @@ __global__ __launch_bounds__(256, MINW) void attn32_kernel(const AttnDesc d) {
         const bool more = t + 1 < ntiles;
         u32x4_t kr[NKB], vr[NKB];
         if (more) {
-            ATHD_A32_FETCH(kt0 + KT)
+            // slot cur ^ 1 was last read in iteration t - 1, which ended with a barrier
+            if constexpr (DMA) {
+                ATHD_A32_DMA(kt0 + KT, cur ^ 1)
+            } else {
+                ATHD_A32_FETCH(kt0 + KT)
+            }
         }
         if (active) {
             const bf16_t* K_ = Ks[cur];
@@ -592,7 +635,9 @@ __global__ __launch_bounds__(256, MINW) void attn32_kernel(const AttnDesc d) {
             // ---- S^T = K Q^T - m ----
             f32x16_t sc[NKB];
             // (ATHD_A32_QK: key tail -> scores of keys >= Nk are -inf)
+            A32_PRIO(1);
             ATHD_A32_QK(-mrun);
+            A32_PRIO(0);
             // ---- online softmax (log2 units) ----
             float mxk[NKB];
 #pragma unroll
@@ -635,6 +680,7 @@ __global__ __launch_bounds__(256, MINW) void attn32_kernel(const AttnDesc d) {
 #pragma unroll
             for (int kb = 0; kb < NKB; ++kb) lrun += ls[kb];
             // ---- O^T += V^T P^T ----
+            A32_PRIO(1);
 #pragma unroll
             for (int kk = 0; kk < 2 * NKB; ++kk) {
                 const f32x16_t& sp = sc[kk >> 1];
@@ -654,8 +700,11 @@ __global__ __launch_bounds__(256, MINW) void attn32_kernel(const AttnDesc d) {
                     else o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, pb, o1, 0, 0, 0);
                 }
             }
+            A32_PRIO(0);
         }
-        if (more) {
+        if constexpr (DMA) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");    // this wave's DMA into slot cur ^ 1 landed
+        } else if (more) {
             ATHD_A32_STASH(cur ^ 1)
         }
         __syncthreads();
@@ -664,7 +713,7 @@ __global__ __launch_bounds__(256, MINW) void attn32_kernel(const AttnDesc d) {
     // ---- normalise; stage the wave's 32 x 64 output tile in LDS; store whole 128-B rows ----
     const float l = half_swap_sum(lrun);
     const float inv = 1.f / l;
-    bf16_t* stage = &Ks[0][0] + wave * 32 * A32_KP;                // 4 waves x 32 rows x 72 <= 2 x 64 x 72
+    bf16_t* stage = smem_a32 + wave * 32 * A32_KP;                 // 4 waves x 32 rows x 72 (static_assert above)
     if (active) {
 #pragma unroll
         for (int db = 0; db < 2; ++db) {
@@ -693,13 +742,18 @@ __global__ __launch_bounds__(256, MINW) void attn32_kernel(const AttnDesc d) {
 
 #undef ATHD_A32_FETCH
 #undef ATHD_A32_STASH
+#undef ATHD_A32_DMA
+
 #undef ATHD_A32_QK
 
-// kernel choice for the bf16 path: 0 = attn32_kernel<3, 2> (default: 3 waves per SIMD, 64-key tiles), 1 =
-// attn_bf16_kernel (16x16x32, ATHD_ATTN_V1=1), 2 = attn32_kernel<2, 2>, 3 = attn32_kernel<2, 4> (128-key tiles); set
-// by tools/kbench.hip for A/B timing.  Tried and dropped (kbench, B=64, N=2072): a software-pipelined form (QK^T of
-// tile t+1 issued before the softmax of tile t, 3-deep K/V ring: 761 vs 804 TFLOP/s) and 64 queries per wave
-// (256 VGPRs with spills: 757).
+// kernel choice for the bf16 path: 0 = attn32_kernel<3, 2, true> (default: 3 waves per SIMD, 64-key tiles, LDS-DMA
+// staging), 1 = attn_bf16_kernel (16x16x32, ATHD_ATTN_V1=1), 2 = attn32_kernel<2, 2>, 3 = attn32_kernel<2, 4> (128-key
+// tiles), 4 = attn32_kernel<3, 2, false> (register staging), 5 / 6 = attn32_kernel<2, 4> / <4, 2> with LDS-DMA staging;
+// set by tools/kbench.hip for A/B timing.  kbench (B=64, N=2072 / 1034, same box): register staging 722 / 730 TFLOP/s,
+// LDS-DMA staging 849 / 777.  Tried and dropped: a software-pipelined form (QK^T of tile t+1 issued before the
+// softmax of tile t, 3-deep K/V ring: 761 vs 804 TFLOP/s), 64 queries per wave on register staging (256 VGPRs with
+// spills: 757) and on LDS-DMA staging (two 32-query blocks sharing every K / V fragment read, 2 waves per workgroup,
+// 2 waves per SIMD at 255 VGPRs: 765 / 648 vs 845 / 776).
 int g_attn_variant = -1;
 static int attn_variant() {
     if (g_attn_variant < 0) {
@@ -731,9 +785,12 @@ int attn_launch(const AttnDesc& d, int mode, hipStream_t s) {
         ks.begin(a32 ? std::string("attn32_kernel") : v2 ? std::string("attn_bf16_kernel") : klabel("attn_kernel<%d>", mode),
                  fl, by);
     }
-    if (a32 && attn_variant() == 2) hipLaunchKernelGGL((attn32_kernel<2, 2>), grid, dim3(256), 0, s, d);
+    if (a32 && attn_variant() == 4) hipLaunchKernelGGL((attn32_kernel<3, 2, false>), grid, dim3(256), 0, s, d);
+    else if (a32 && attn_variant() == 5) hipLaunchKernelGGL((attn32_kernel<2, 4, true>), grid, dim3(256), 0, s, d);
+    else if (a32 && attn_variant() == 6) hipLaunchKernelGGL((attn32_kernel<4, 2, true>), grid, dim3(256), 0, s, d);
+    else if (a32 && attn_variant() == 2) hipLaunchKernelGGL((attn32_kernel<2, 2>), grid, dim3(256), 0, s, d);
     else if (a32 && attn_variant() == 3) hipLaunchKernelGGL((attn32_kernel<2, 4>), grid, dim3(256), 0, s, d);
-    else if (a32) hipLaunchKernelGGL((attn32_kernel<3, 2>), grid, dim3(256), 0, s, d);
+    else if (a32) hipLaunchKernelGGL((attn32_kernel<3, 2, true>), grid, dim3(256), 0, s, d);
     else if (mode == 1 && d.q_bf16 && d.k_bf16 && d.v_bf16) hipLaunchKernelGGL(attn_bf16_kernel, grid, dim3(256), 0, s, d);
     else if (mode == 1) hipLaunchKernelGGL(attn_kernel<1>, grid, dim3(256), 0, s, d);
     else hipLaunchKernelGGL(attn_kernel<0>, grid, dim3(256), 0, s, d);

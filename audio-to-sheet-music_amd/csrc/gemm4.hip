@@ -30,6 +30,7 @@ constexpr int G4_NSTAMP = 24;
 #include "gemm_epi.h"
 
 #include <climits>
+#include <cstdlib>
 
 namespace athd {
 
@@ -65,6 +66,14 @@ __device__ __attribute__((aligned(64))) uint4 g_zero_page4[4];
 // ATHD_G4_STAMP (tools/kbench build only): wave 0 lane 0 of each block records s_memtime at the phase points
 // (kernel start, prologue issued, phase 0 of K-tiles 0, 1 and the last, epilogue start / end) into g4_stamp.
 
+// ATHD_G4_PRIO (tools/kbench build only, A/B measurement): s_setprio(1) around each phase's MFMA cluster
+// (cdna_hip_programming.md T5: keeps hipcc from moving the MFMAs across the raw s_barriers)
+#ifdef ATHD_G4_PRIO
+#define G4_PRIO(x) __builtin_amdgcn_s_setprio(x)
+#else
+#define G4_PRIO(x)
+#endif
+
 template <unsigned F>
 __global__ __launch_bounds__(512) void gemm4_kernel(const GemmDesc d) {
     constexpr int TM = 8, TN = 4;
@@ -89,10 +98,14 @@ __global__ __launch_bounds__(512) void gemm4_kernel(const GemmDesc d) {
     auto mark = [&]() {};
 #endif
     mark();
-    // XCD-aware order (T1): the N tiles of one M tile are consecutive ids on one XCD, sharing its A rows in L2
-    const int id = xcd_remap4(blockIdx.x, gridDim.x);
-    const int64_t m0 = (int64_t)(id / ntn) * 256;
-    const int n0 = (id % ntn) * 256;
+    // Tiles: XCD-aware order (T1): the N tiles of one M tile are consecutive ids on one XCD, sharing its A rows in L2.
+    // PERSIST (epilogues without residual or statistics): the launch sizes the grid to the resident blocks (a
+    // multiple of 8, so tiles t, t + gridDim.x, ... of a block stay on its XCD) and each block walks its tiles, staging
+    // the next tile's first 1.5 K-tiles BEFORE this tile's epilogue so their load latency hides under the epilogue's
+    // VALU work and stores (gemm3's tile loop).  The residual / statistics epilogues keep one tile per block: around
+    // them the loop spills.
+    constexpr bool PERSIST = (F & (F_RES | F_STATS)) == 0;
+    const int ntiles = (int)((M + 255) / 256) * ntn;
     const int64_t a_bs = d.a_bs >= 0 ? d.a_bs : (int64_t)d.H_in * d.W * d.a_ld;
     const int64_t rowpitch = d.a_hs >= 0 ? d.a_hs : (int64_t)d.W * d.a_ld;
     const int lrow = lane >> 3;
@@ -102,26 +115,34 @@ __global__ __launch_bounds__(512) void gemm4_kernel(const GemmDesc d) {
     // this lane's slot rows: sr = 8 (wave + 8 q) + lrow, q = 0, 1 (both slot halves h use the same sr).
     // 32-bit element offsets (gemm4_supported: A < 2^31 elements; the weights hold whole 256-row tiles); a row past M
     // gets a_h0 = INT_MIN / 2, which fails the row >= 0 test for every tap.
+    int tile = blockIdx.x;
+    int64_t m0 = 0;
+    int n0 = 0;
     uint32_t a_base[2][2];
     int a_h0[2][2];
     uint32_t b_off[2];
+    auto setup = [&](int t) {
+        const int id = xcd_remap4(t, ntiles);
+        m0 = (int64_t)(id / ntn) * 256;
+        n0 = (id % ntn) * 256;
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
+        for (int h = 0; h < 2; ++h)
 #pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            const int sr = 8 * (wave + NW * q) + lrow;
-            const int r = (sr >> 6) * 128 + 64 * h + (sr & 63);
-            const uint32_t m = (uint32_t)(m0 + r);
-            const bool ok = m < (uint32_t)M;
-            const uint32_t mm = ok ? m : 0u;
-            const uint32_t t = fdiv(mm, d.fd_w);
-            const uint32_t w = mm - t * (uint32_t)d.W;
-            const uint32_t b = fdiv(t, d.fd_h);
-            const uint32_t ho = t - b * (uint32_t)d.H_out;
-            a_base[h][q] = (uint32_t)(b * a_bs + (int64_t)w * d.a_ld);
-            a_h0[h][q] = ok ? (int)ho * d.in_stride + d.in_off : (INT_MIN / 2);
-            if (h == 0) b_off[q] = (uint32_t)(((int64_t)(n0 + (sr >> 5) * 64 + (sr & 31)) * d.Kp + 8 * chunk) * 2);
-        }
+            for (int q = 0; q < 2; ++q) {
+                const int sr = 8 * (wave + NW * q) + lrow;
+                const int r = (sr >> 6) * 128 + 64 * h + (sr & 63);
+                const uint32_t m = (uint32_t)(m0 + r);
+                const bool ok = m < (uint32_t)M;
+                const uint32_t mm = ok ? m : 0u;
+                const uint32_t t2 = fdiv(mm, d.fd_w);
+                const uint32_t w = mm - t2 * (uint32_t)d.W;
+                const uint32_t b = fdiv(t2, d.fd_h);
+                const uint32_t ho = t2 - b * (uint32_t)d.H_out;
+                a_base[h][q] = (uint32_t)(b * a_bs + (int64_t)w * d.a_ld);
+                a_h0[h][q] = ok ? (int)ho * d.in_stride + d.in_off : (INT_MIN / 2);
+                if (h == 0) b_off[q] = (uint32_t)(((int64_t)(n0 + (sr >> 5) * 64 + (sr & 31)) * d.Kp + 8 * chunk) * 2);
+            }
+    };
     const uint32_t b_h1 = (uint32_t)(32 * d.Kp * 2);     // slot B1 rows are 32 columns further
     const int nk = d.Kp / 64;
 
@@ -145,6 +166,18 @@ __global__ __launch_bounds__(512) void gemm4_kernel(const GemmDesc d) {
         for (int q = 0; q < 2; ++q)
             __builtin_amdgcn_global_load_lds((gbl_void*)(wb + b_off[q]), (lds_void*)(dst + (wave + NW * q) * 1024), 16, 0, 0);
     };
+    // prologue of a tile: A0 B0 B1 (0), A1 (0), A0 B0 B1 (1)
+    auto prologue = [&]() {
+        issueA(0, 0);
+        issueB(0, 0);
+        issueB(0, 1);
+        issueA(0, 1);
+        if (nk > 1) {
+            issueA(1, 0);
+            issueB(1, 0);
+            issueB(1, 1);
+        }
+    };
 
     const int fr = lane & 15, g = lane >> 4;
     // fragments of slot A_mh: rows wr*64 + 16 i + fr; of slot B_nh: rows wc*32 + 16 j + fr
@@ -166,10 +199,6 @@ __global__ __launch_bounds__(512) void gemm4_kernel(const GemmDesc d) {
     };
 
     f32x4_t acc[TM][TN];
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
     auto quad = [&](int mh, int nh, const bf16v8 (&af)[4][2], const bf16v8 (&bf)[2][2]) {
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks)
@@ -181,6 +210,7 @@ __global__ __launch_bounds__(512) void gemm4_kernel(const GemmDesc d) {
                         __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][ks], af[i][ks], acc[4 * mh + i][2 * nh + j], 0, 0, 0);
     };
     if (d.stats && tid < 2 * EPI_MAXG) st_lds[tid] = 0.0;
+    setup(tile);
     float4 bias4[TN];                             // loaded now: retired long before the epilogue needs it
     load_bias4<TN>(d, n0, wn0, lane, bias4);
     // Desynchronise the first wave of workgroups (one per CU): with equal tiles everywhere every CU would reach its
@@ -199,57 +229,71 @@ __global__ __launch_bounds__(512) void gemm4_kernel(const GemmDesc d) {
     //   phase B(t): publish A1(t); restage A0, B0, B1 <- t+2 (last read in phase A(t)); read A1; MFMA (A1, B1),
     //               (A1, B0)
     // Issue order: ... A0B0B1(t) | A1(t) | A0B0B1(t+1) | A1(t+1) | ...  (each load gets ~1.5 K-tiles to land)
-    // prologue: A0 B0 B1 (0), A1 (0), A0 B0 B1 (1)
-    issueA(0, 0);
-    issueB(0, 0);
-    issueB(0, 1);
-    issueA(0, 1);
-    if (nk > 1) {
-        issueA(1, 0);
-        issueB(1, 0);
-        issueB(1, 1);
-    }
+    prologue();
     mark();
-    bf16v8 af[4][2], bf0[2][2], bf1[2][2];
-    for (int t = 0; t < nk; ++t) {
-        const int buf = t & 1;
-        const bool has1 = t + 1 < nk, has2 = t + 2 < nk;
-        // phase A: after A0B0B1(t): A1(t) [2] + A0B0B1(t+1) [6]
-        if (has1) vm_wait<8>();
-        else vm_wait<2>();
-        phase_barrier();
-        if (t < 2 || t == nk - 1) mark();
-        if (has1) issueA(t + 1, 1);
-        readA(buf, 0, af);
-        readB(buf, 0, bf0);
-        readB(buf, 1, bf1);
-        quad(0, 0, af, bf0);
-        quad(0, 1, af, bf1);
-        // phase B: after A1(t): A0B0B1(t+1) [6] + A1(t+1) [2]
-        if (has1) vm_wait<8>();
-        else vm_wait<0>();
-        phase_barrier();
-        if (has2) {
-            issueA(t + 2, 0);
-            issueB(t + 2, 0);
-            issueB(t + 2, 1);
-        }
-        readA(buf, 1, af);
-        quad(1, 1, af, bf1);
-        quad(1, 0, af, bf0);
-    }
-    mark();
-    // consume the bias registers once, unconditionally: the compiler places their (now free) vmcnt wait here instead
-    // of before every branch-guarded use
+    for (;;) {
 #pragma unroll
-    for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(bias4[j].x), "v"(bias4[j].y), "v"(bias4[j].z), "v"(bias4[j].w));
-    if constexpr ((F & F_RES) != 0 && (F & ~(F_RES | F_STATS)) == 0) {
-        if (epi_res_fast_ok(d)) {
-            gemm_epilogue_res<TM, TN, F>(d, acc, m0, n0, wm0, wn0, lane, st_lds, 256, bias4);
-            return;
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+        bf16v8 af[4][2], bf0[2][2], bf1[2][2];
+        for (int t = 0; t < nk; ++t) {
+            const int buf = t & 1;
+            const bool has1 = t + 1 < nk, has2 = t + 2 < nk;
+            // phase A: after A0B0B1(t): A1(t) [2] + A0B0B1(t+1) [6]
+            if (has1) vm_wait<8>();
+            else vm_wait<2>();
+            phase_barrier();
+            if (t < 2 || t == nk - 1) mark();
+            if (has1) issueA(t + 1, 1);
+            readA(buf, 0, af);
+            readB(buf, 0, bf0);
+            readB(buf, 1, bf1);
+            G4_PRIO(1);
+            quad(0, 0, af, bf0);
+            quad(0, 1, af, bf1);
+            G4_PRIO(0);
+            // phase B: after A1(t): A0B0B1(t+1) [6] + A1(t+1) [2]
+            if (has1) vm_wait<8>();
+            else vm_wait<0>();
+            phase_barrier();
+            if (has2) {
+                issueA(t + 2, 0);
+                issueB(t + 2, 0);
+                issueB(t + 2, 1);
+            }
+            readA(buf, 1, af);
+            G4_PRIO(1);
+            quad(1, 1, af, bf1);
+            quad(1, 0, af, bf0);
+            G4_PRIO(0);
         }
+        mark();
+        const int next = tile + (int)gridDim.x;
+        const int64_t m0_done = m0;
+        const int n0_done = n0;
+        if (PERSIST && next < ntiles) {
+            phase_barrier();                      // every wave's fragment reads of the last K-tile retired
+            setup(next);
+            prologue();
+        }
+        // consume the bias registers once, unconditionally: the compiler places their (now free) vmcnt wait here
+        // instead of before every branch-guarded use
+#pragma unroll
+        for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(bias4[j].x), "v"(bias4[j].y), "v"(bias4[j].z), "v"(bias4[j].w));
+        if constexpr ((F & F_RES) != 0 && (F & ~(F_RES | F_STATS)) == 0) {
+            if (epi_res_fast_ok(d)) {
+                gemm_epilogue_res<TM, TN, F>(d, acc, m0_done, n0_done, wm0, wn0, lane, st_lds, 256, bias4);
+                return;
+            }
+        }
+        gemm_epilogue<TM, TN, F, true>(d, acc, m0_done, n0_done, wm0, wn0, lane, st_lds, 256, bias4);
+        if (!PERSIST || next >= ntiles) break;
+        tile = next;
+        // the epilogue's stores sit behind the staged K-tiles on the VM counter: drain all, then the next tile's bias
+        vm_wait<0>();
+        load_bias4<TN>(d, n0, wn0, lane, bias4);
     }
-    gemm_epilogue<TM, TN, F, true>(d, acc, m0, n0, wm0, wn0, lane, st_lds, 256, bias4);
 #ifdef ATHD_G4_STAMP
     if (stamp) {
         mark();                                  // epilogue issued
@@ -270,17 +314,39 @@ bool gemm4_supported(const GemmDesc& d) {
            d.col_split % 4 == 0 && (d.act != ACT_GLU || d.N % 32 == 0);
 }
 
+// ATHD_G4_PERSIST=0: one tile per block for every epilogue (A/B measurement)
+int g_g4_persist = -1;
+static bool g4_persist() {
+    if (g_g4_persist < 0) {
+        const char* e = std::getenv("ATHD_G4_PERSIST");
+        g_g4_persist = e && *e == '0' ? 0 : 1;
+    }
+    return g_g4_persist == 1;
+}
+
 template <unsigned F>
 static void launch4f(const GemmDesc& d, hipStream_t s) {
     const int64_t M = (int64_t)d.nb * d.H_out * d.W;
     const int64_t tiles = ((M + 255) / 256) * ((d.N + 255) / 256);
+    int64_t grid = tiles;
+    if constexpr ((F & (F_RES | F_STATS)) == 0) {   // persistent: the resident blocks (one per CU), a multiple of 8
+        static int resident = 0;
+        if (resident == 0) {
+            int per_cu = 0, cus = 0, dev = 0;
+            (void)hipGetDevice(&dev);
+            (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+            (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, gemm4_kernel<F>, 512, 0);
+            resident = per_cu > 0 && cus > 0 ? per_cu * cus / 8 * 8 : -1;
+        }
+        if (g4_persist() && resident >= 8 && resident < tiles) grid = resident;
+    }
     KScope ks(s);
     if (ks.on()) {
         double fl, by;
         gemm_work(d, 1, fl, by);
         ks.begin(klabel("gemm4_kernel<%u>", F), fl, by);
     }
-    hipLaunchKernelGGL((gemm4_kernel<F>), dim3((unsigned)tiles), dim3(512), 0, s, with_fastdiv(d));
+    hipLaunchKernelGGL((gemm4_kernel<F>), dim3((unsigned)grid), dim3(512), 0, s, with_fastdiv(d));
 }
 
 #ifdef ATHD_G4_STAMP

@@ -7,7 +7,7 @@ import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 VARIANTS = (33, 40)
-lib = ctypes.CDLL(os.path.join(HERE, "libkbench.so"))
+lib = ctypes.CDLL(os.path.join(HERE, os.environ.get("KB_LIB", "libkbench.so")))
 vp = ctypes.c_void_p
 
 
