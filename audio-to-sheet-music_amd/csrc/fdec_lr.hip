@@ -439,6 +439,255 @@ __global__ __launch_bounds__(256) void fdec_lr_stats2_kernel(const LowRankDesc d
     }
 }
 
+// v3 statistics pass (bf16 mode, strict upsampling Hd > Hs, Hd > Hk): there every row change of a lerp moves (i0, i1)
+// to (i1, min(i1 + 1, H - 1)), so a change needs ONE new row, and that row is known at the previous change.  The pass
+// keeps the scaled i1 row (hi) and the row difference (dr) per tap, updates the lerp base incrementally (base += dr:
+// the i0 row becomes the old i1 row), and prefetches the next i1 row as raw bf16 pairs right after each change, so
+// its load latency hides under the ~Hd/H steps of VALU work before it is needed (v2 loads both rows at the change and
+// waits for them).  Half the Z / Zs loads; rounding differs from v2 by the incremental base only (bf16 mode).
+ATHD_DEV f2 bf2u(uint32_t q) { return (f2){__uint_as_float(q << 16), __uint_as_float(q & 0xFFFF0000u)}; }
+
+__global__ __launch_bounds__(256) void fdec_lr_stats3_kernel(const LowRankDesc d) {
+    const LrThread th = lr_thread(d);
+    const int N8 = 8 * d.Co;
+    const int64_t rp = (int64_t)d.W * N8;
+    const bf16_t* zb = (const bf16_t*)d.Z + (int64_t)th.item * d.Hs * rp + (int64_t)th.w * N8 + th.c;
+    const bf16_t* sb = (const bf16_t*)d.Zs + (int64_t)th.seg * d.Hk * rp + (int64_t)th.w * N8 + th.c;
+    const f2 bias = ld2(d.bias + th.c);
+    f2 zhi[8], zdr[8], shi[8], sdr[8], base[8];
+    uint32_t zpf[8], spf[8];
+    double s1 = 0.0, s2 = 0.0;
+    auto ldrow = [&](const bf16_t* p, int row, uint32_t (&r)[8]) {
+#pragma unroll
+        for (int t = 0; t < 8; ++t) r[t] = *reinterpret_cast<const uint32_t*>(p + (int64_t)row * rp + t * d.Co);
+    };
+    if (th.active) {
+        const LrStep s0 = lr_step(d.steps, 0);
+        int zr = (s0.zk >> 8) & 0xFF, kr = s0.zk >> 24;          // current i1 rows (wave-uniform)
+        {
+            uint32_t za[8], ka[8];
+            ldrow(zb, s0.zk & 0xFF, za);
+            ldrow(zb, zr, zpf);
+            ldrow(sb, (s0.zk >> 16) & 0xFF, ka);
+            ldrow(sb, kr, spf);
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                const f2 a = bf2u(za[t]), b = bf2u(zpf[t]);
+                const f2 ka2 = bf2u(ka[t]) * splat(0.1f), kb2 = bf2u(spf[t]) * splat(0.1f);
+                zhi[t] = b;
+                zdr[t] = b - a;
+                shi[t] = kb2;
+                sdr[t] = kb2 - ka2;
+                base[t] = a + ka2 + ((t >= 2 && t <= 5) ? bias : f2{});
+            }
+        }
+        ldrow(zb, min(zr + 1, d.Hs - 1), zpf);
+        ldrow(sb, min(kr + 1, d.Hk - 1), spf);
+        // T of step v from the current rows (row changes applied first)
+        auto tstep = [&](const LrStep& st, f2 (&T)[8]) {
+            if (st.flags & 1u) {                  // Z rows (i0, i1) -> (i1, i1 + 1)
+#pragma unroll
+                for (int t = 0; t < 8; ++t) {
+                    const f2 nb = bf2u(zpf[t]);
+                    base[t] += zdr[t];
+                    zdr[t] = nb - zhi[t];
+                    zhi[t] = nb;
+                }
+                zr = min(zr + 1, d.Hs - 1);
+                ldrow(zb, min(zr + 1, d.Hs - 1), zpf);
+            }
+            if (st.flags & 2u) {                  // Zs rows
+#pragma unroll
+                for (int t = 0; t < 8; ++t) {
+                    const f2 nb = bf2u(spf[t]) * splat(0.1f);
+                    base[t] += sdr[t];
+                    sdr[t] = nb - shi[t];
+                    shi[t] = nb;
+                }
+                kr = min(kr + 1, d.Hk - 1);
+                ldrow(sb, min(kr + 1, d.Hk - 1), spf);
+            }
+#pragma unroll
+            for (int t = 0; t < 8; ++t) T[t] = pfma(splat(st.lz), zdr[t], pfma(splat(st.lk), sdr[t], base[t]));
+        };
+        // step 0 (rows 0, 1 only; its rows were loaded above)
+        f2 pv[4];                                 // T[4..7] of the previous step
+        f2 a1 = {}, a2 = {};
+        {
+            f2 T[8];
+#pragma unroll
+            for (int t = 0; t < 8; ++t) T[t] = pfma(splat(s0.lz), zdr[t], pfma(splat(s0.lk), sdr[t], base[t]));
+            a1 += T[2] + T[3];
+            a2 = pfma(T[2], T[2], pfma(T[3], T[3], a2));
+#pragma unroll
+            for (int t = 0; t < 4; ++t) pv[t] = T[4 + t];
+        }
+        // steps 1 .. Hd-1: rows 4(v-1)+2, 4(v-1)+3 and 4v, 4v+1; no per-step conditions besides the row changes
+        LrStep nx = lr_step(d.steps, 1);
+        for (int v0 = 1; v0 < d.Hd; v0 += 16) {
+            const int v1 = min(v0 + 16, d.Hd);
+            for (int v = v0; v < v1; ++v) {
+                const LrStep st = nx;
+                nx = lr_step(d.steps, v + 1);
+                f2 T[8];
+                tstep(st, T);
+                const f2 y2 = pv[0] + T[0], y3 = pv[1] + T[1];
+                const f2 y0 = T[2] + pv[2], y1 = T[3] + pv[3];
+                a1 += (y2 + y3) + (y0 + y1);
+                a2 = pfma(y2, y2, pfma(y3, y3, a2));
+                a2 = pfma(y0, y0, pfma(y1, y1, a2));
+#pragma unroll
+                for (int t = 0; t < 4; ++t) pv[t] = T[4 + t];
+            }
+            s1 += (double)a1.x + (double)a1.y;
+            s2 += (double)a2.x + (double)a2.y;
+            a1 = f2{};
+            a2 = f2{};
+        }
+        // step Hd: rows 4(Hd-1)+2, 4(Hd-1)+3 only (T = 0)
+        a1 += pv[0] + pv[1];
+        a2 = pfma(pv[0], pv[0], pfma(pv[1], pv[1], a2));
+        s1 += (double)a1.x + (double)a1.y;
+        s2 += (double)a2.x + (double)a2.y;
+    }
+    s1 = wave_sum_d(s1);
+    s2 = wave_sum_d(s2);
+    __shared__ double sh[2][4];
+    const int wv = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) { sh[0][wv] = s1; sh[1][wv] = s2; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        atomicAdd(&d.stats[2 * th.item], sh[0][0] + sh[0][1] + sh[0][2] + sh[0][3]);
+        atomicAdd(&d.stats[2 * th.item + 1], sh[1][0] + sh[1][1] + sh[1][2] + sh[1][3]);
+    }
+}
+
+// v3 merge pass (bf16 mode, strict upsampling Hd > Hs, Hk, H_skip): the one-new-row updates and next-row prefetches
+// of fdec_lr_stats3_kernel for the Z / Zs rows (taps 0, 3, 4, 7) and the skip2 rows, and the first / last steps
+// peeled so that the step loop carries no per-step conditions besides the row changes.
+__global__ __launch_bounds__(256) void fdec_lr_merge3_kernel(const LowRankDesc d) {
+    const LrThread th = lr_thread(d);
+    if (!th.active) return;
+    constexpr int NT = 4;
+    const int N8 = 8 * d.Co;
+    const int64_t rp = (int64_t)d.W * N8;
+    const bf16_t* zb = (const bf16_t*)d.Z + (int64_t)th.item * d.Hs * rp + (int64_t)th.w * N8 + th.c;
+    const bf16_t* sb = (const bf16_t*)d.Zs + (int64_t)th.seg * d.Hk * rp + (int64_t)th.w * N8 + th.c;
+    float mean, rstd;
+    gn_params(d.stats, th.item, 4LL * d.Hd * d.W * d.Co, mean, rstd);
+    const f2 bias = ld2(d.bias + th.c);
+    const f2 gsc = ld2(d.gn_w + th.c) * splat(rstd);     // (y - mean) * rstd * w + b  as  (y - mean) * gsc + b
+    const f2 gb = ld2(d.gn_b + th.c) - splat(mean) * gsc; // ... as y * gsc + gb'
+    const int64_t kp = (int64_t)d.W * d.C_skip;
+    const bf16_t* kbp = (const bf16_t*)d.skip + (int64_t)th.seg * d.H_skip * kp + (int64_t)th.w * d.C_skip + th.c;
+    bf2_t* op = (bf2_t*)((bf16_t*)d.out + (int64_t)th.item * d.Hd * d.W * d.Co + (int64_t)th.w * d.Co + th.c);
+    const int64_t ostep = (int64_t)d.W * d.Co / 2;        // bf2 elements between output rows
+
+    auto ldrow = [&](const bf16_t* p, int row, uint32_t (&r)[NT]) {
+#pragma unroll
+        for (int t = 0; t < NT; ++t) r[t] = *reinterpret_cast<const uint32_t*>(p + (int64_t)row * rp + tap_of<NT>(t) * d.Co);
+    };
+    f2 zhi[NT], zdr[NT], shi[NT], sdr[NT], base[NT];
+    uint32_t zpf[NT], spf[NT];
+    const LrStep s0 = lr_step(d.steps, 0);
+    int zr = (s0.zk >> 8) & 0xFF, kr = s0.zk >> 24;
+    {
+        uint32_t za[NT], ka[NT];
+        ldrow(zb, s0.zk & 0xFF, za);
+        ldrow(zb, zr, zpf);
+        ldrow(sb, (s0.zk >> 16) & 0xFF, ka);
+        ldrow(sb, kr, spf);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            const f2 a = bf2u(za[t]), b = bf2u(zpf[t]);
+            const f2 ka2 = bf2u(ka[t]) * splat(0.1f), kb2 = bf2u(spf[t]) * splat(0.1f);
+            zhi[t] = b;
+            zdr[t] = b - a;
+            shi[t] = kb2;
+            sdr[t] = kb2 - ka2;
+            base[t] = a + ka2 + ((t == 1 || t == 2) ? bias : f2{});
+        }
+    }
+    ldrow(zb, min(zr + 1, d.Hs - 1), zpf);
+    ldrow(sb, min(kr + 1, d.Hk - 1), spf);
+    // skip2 rows of output row 0 (step 1's entry), then the next one prefetched
+    const LrStep s1e = lr_step(d.steps, 1);
+    int jr = (int)(s1e.jj >> 16);
+    f2 khi, kdr;
+    uint32_t jpf;
+    {
+        const f2 a = bf2u(*reinterpret_cast<const uint32_t*>(kbp + (int64_t)(s1e.jj & 0xFFFF) * kp)) * splat(0.1f);
+        khi = bf2u(*reinterpret_cast<const uint32_t*>(kbp + (int64_t)jr * kp)) * splat(0.1f);
+        kdr = khi - a;
+    }
+    jpf = *reinterpret_cast<const uint32_t*>(kbp + (int64_t)min(jr + 1, d.H_skip - 1) * kp);
+    f2 kbase = khi - kdr;                                 // 0.1 * skip row j0
+
+    auto tstep = [&](const LrStep& st, f2 (&T)[NT]) {
+        if (st.flags & 1u) {
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+                const f2 nb = bf2u(zpf[t]);
+                base[t] += zdr[t];
+                zdr[t] = nb - zhi[t];
+                zhi[t] = nb;
+            }
+            zr = min(zr + 1, d.Hs - 1);
+            ldrow(zb, min(zr + 1, d.Hs - 1), zpf);
+        }
+        if (st.flags & 2u) {
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+                const f2 nb = bf2u(spf[t]) * splat(0.1f);
+                base[t] += sdr[t];
+                sdr[t] = nb - shi[t];
+                shi[t] = nb;
+            }
+            kr = min(kr + 1, d.Hk - 1);
+            ldrow(sb, min(kr + 1, d.Hk - 1), spf);
+        }
+#pragma unroll
+        for (int t = 0; t < NT; ++t) T[t] = pfma(splat(st.lz), zdr[t], pfma(splat(st.lk), sdr[t], base[t]));
+    };
+    // output row dd = v - 1 from rows 4dd+1 (cur3 + prev7) and 4dd+2 (cur4 + T0): the exact /4 resize (0.5 / 0.5)
+    auto emit = [&](const LrStep& st, f2 y1, f2 y2, int dd) {
+        if (dd >= 1 && (st.flags & 4u)) {                 // skip2 rows (j0, j1) -> (j1, j1 + 1)
+            const f2 nb = bf2u(jpf) * splat(0.1f);
+            kbase += kdr;
+            kdr = nb - khi;
+            khi = nb;
+            jr = min(jr + 1, d.H_skip - 1);
+            jpf = *reinterpret_cast<const uint32_t*>(kbp + (int64_t)min(jr + 1, d.H_skip - 1) * kp);
+        }
+        const f2 g1 = gelu2_pk(pfma(y1, gsc, gb));
+        const f2 g2 = gelu2_pk(pfma(y2, gsc, gb));
+        const f2 o = pfma(g1 + g2, splat(0.5f), pfma(splat(st.lj), kdr, kbase));
+        op[(int64_t)dd * ostep] = __builtin_convertvector(o, bf2_t);
+    };
+    f2 cur3, cur4, cur7, prev7 = {};
+    {
+        f2 T[NT];
+#pragma unroll
+        for (int t = 0; t < NT; ++t) T[t] = pfma(splat(s0.lz), zdr[t], pfma(splat(s0.lk), sdr[t], base[t]));
+        cur3 = T[1];
+        cur4 = T[2];
+        cur7 = T[3];
+    }
+    LrStep nx = s1e;
+    for (int v = 1; v < d.Hd; ++v) {
+        const LrStep st = nx;
+        nx = lr_step(d.steps, v + 1);
+        f2 T[NT];
+        tstep(st, T);
+        emit(st, cur3 + prev7, cur4 + T[0], v - 1);
+        prev7 = cur7;
+        cur3 = T[1];
+        cur4 = T[2];
+        cur7 = T[3];
+    }
+    emit(nx, cur3 + prev7, cur4, d.Hd - 1);               // step Hd: T = 0
+}
+
 template <typename ZT, bool FAST>
 __global__ __launch_bounds__(256) void fdec_lr_merge2_kernel(const LowRankDesc d) {
     const LrThread th = lr_thread(d);
@@ -531,6 +780,16 @@ static bool lr_v1() {
     return v == 1;
 }
 
+// ATHD_LR_V3=0: the v2 statistics pass in the bf16 mode too (A/B measurement)
+static bool lr_v3() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = std::getenv("ATHD_LR_V3");
+        v = e && *e == '0' ? 0 : 1;
+    }
+    return v == 1;
+}
+
 int fdec_lr_steps_launch(LrStep* steps, int Hd, int Hs, int Hk, int H_skip, hipStream_t s) {
     if (!steps || Hd <= 0 || Hs <= 0 || Hs > 256 || Hk <= 0 || Hk > 256 || H_skip <= 0 || H_skip > 65536) return -1;
     KScope ks(s);
@@ -554,7 +813,9 @@ int fdec_lr_stats_launch(const LowRankDesc& d, hipStream_t s) {
         const double by = ze * 8.0 * d.Co * d.W * ((double)d.NI * d.Hs + (double)(d.NI / d.P) * d.Hk);
         ks.begin(d.z_bf16 ? "fdec_lr_stats_kernel<unsignedshort>" : "fdec_lr_stats_kernel<float>", 0.0, by);
     }
-    if (d.steps && !lr_v1()) {
+    if (d.steps && !lr_v1() && d.z_bf16 && d.Hd > d.Hs && d.Hd > d.Hk && lr_v3()) {
+        hipLaunchKernelGGL(fdec_lr_stats3_kernel, grid, dim3(256), 0, s, d);
+    } else if (d.steps && !lr_v1()) {
         if (d.z_bf16) hipLaunchKernelGGL(fdec_lr_stats2_kernel<bf16_t>, grid, dim3(256), 0, s, d);
         else hipLaunchKernelGGL(fdec_lr_stats2_kernel<float>, grid, dim3(256), 0, s, d);
     } else if (d.z_bf16) hipLaunchKernelGGL(fdec_lr_stats_kernel<bf16_t>, grid, dim3(256), 0, s, d);
@@ -578,7 +839,10 @@ int fdec_lr_merge_launch(const LowRankDesc& d, hipStream_t s) {
         ks.begin(klabel("fdec_lr_merge_kernel<%s,%s>", d.z_bf16 ? "unsignedshort" : "float",
                         d.fast_gelu ? "true" : "false"), 0.0, by);
     }
-    if (d.steps && !lr_v1()) {
+    if (d.steps && !lr_v1() && d.z_bf16 && d.skip_bf16 && d.out_bf16 && d.fast_gelu && d.Hd > d.Hs && d.Hd > d.Hk &&
+        d.Hd > d.H_skip && lr_v3()) {
+        hipLaunchKernelGGL(fdec_lr_merge3_kernel, grid, dim3(256), 0, s, d);
+    } else if (d.steps && !lr_v1()) {
         if (d.z_bf16) {
             if (d.fast_gelu) hipLaunchKernelGGL((fdec_lr_merge2_kernel<bf16_t, true>), grid, dim3(256), 0, s, d);
             else hipLaunchKernelGGL((fdec_lr_merge2_kernel<bf16_t, false>), grid, dim3(256), 0, s, d);
