@@ -529,9 +529,13 @@ template <> struct TtRow<true> {
 
 template <bool BF>
 __global__ __launch_bounds__(TL_NT) void tdec_tail_kernel(const DecLastDesc d) {
-    constexpr int GS_BYTES = TtRow<BF>::BYTES > TL_NT * 16 * 4 ? TtRow<BF>::BYTES : TL_NT * 16 * 4;
+    // phase 3: z rows [TL_NT][TZ_LD], over the dead phase-1 tile.  Row pitch 20 floats: the 16-lane groups of the
+    // b128 row writes (16 consecutive rows) and row reads (thread = row) then cover 16 distinct 4-bank sets (pitch 16
+    // put 4 rows on each set: 4-way conflicts on the writes, 16-way on the former per-float reads)
+    constexpr int TZ_LD = 20;
+    constexpr int GS_BYTES = TtRow<BF>::BYTES > TL_NT * TZ_LD * 4 ? TtRow<BF>::BYTES : TL_NT * TZ_LD * 4;
     __shared__ __attribute__((aligned(16))) char gsm[GS_BYTES];
-    float* zb = reinterpret_cast<float*>(gsm);  // phase 3: z rows [TL_NT][16], over the dead phase-1 tile
+    float* zb = reinterpret_cast<float*>(gsm);
     const int64_t item = blockIdx.y;
     const int64_t seg = item / d.P;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -596,7 +600,7 @@ __global__ __launch_bounds__(TL_NT) void tdec_tail_kernel(const DecLastDesc d) {
     __syncthreads();                             // every wave is done reading the phase-1 tile
 #pragma unroll
     for (int k = 0; k < 4; ++k)
-        *reinterpret_cast<float4*>(zb + (64 * k + 16 * wave + p) * 16 + 4 * cg) = make_float4(z[k][0], z[k][1], z[k][2], z[k][3]);
+        *reinterpret_cast<float4*>(zb + (64 * k + 16 * wave + p) * TZ_LD + 4 * cg) = make_float4(z[k][0], z[k][1], z[k][2], z[k][3]);
     __syncthreads();
     const int u = blockIdx.x * TL_IN - 1 + tid;
     if (!(tid > 0 && tid < TL_NT - 1 && u < Lin)) return;
@@ -617,18 +621,21 @@ __global__ __launch_bounds__(TL_NT) void tdec_tail_kernel(const DecLastDesc d) {
         sbv[r][0] = c0 + (S[0] * s[0] + S[1] * s[1] + S[2] * s[2] + S[3] * s[3]);
         sbv[r][1] = c1 + (S[4] * s[0] + S[5] * s[1] + S[6] * s[2] + S[7] * s[3]);
     }
-    const float* zc = zb + tid * 16;             // taps of row u:   [z0 z1 | z2 z3 | z4 z5 | z6 z7] x 2 channels
-    const float* zl = zc - 16;                   // row u - 1 feeds rows 4u + {0, 1} through taps 6, 7
-    const float* zh = zc + 16;                   // row u + 1 feeds rows 4u + {2, 3} through taps 0, 1
+    // taps of row u: [z0 z1 | z2 z3 | z4 z5 | z6 z7] x 2 channels; row u - 1 feeds rows 4u + {0, 1} through taps 6, 7,
+    // row u + 1 feeds rows 4u + {2, 3} through taps 0, 1
+    const float* zc = zb + tid * TZ_LD;
+    const float4 c4 = *reinterpret_cast<const float4*>(zc + 4), c8 = *reinterpret_cast<const float4*>(zc + 8);
+    const float4 l12 = *reinterpret_cast<const float4*>(zc - TZ_LD + 12);
+    const float4 h0 = *reinterpret_cast<const float4*>(zc + TZ_LD);
     float4 o0, o1;
-    o0.x = (zc[4] + zl[12]) + sbv[0][0];
-    o0.y = (zc[5] + zl[13]) + sbv[0][1];
-    o0.z = (zc[6] + zl[14]) + sbv[1][0];
-    o0.w = (zc[7] + zl[15]) + sbv[1][1];
-    o1.x = (zc[8] + zh[0]) + sbv[2][0];
-    o1.y = (zc[9] + zh[1]) + sbv[2][1];
-    o1.z = (zc[10] + zh[2]) + sbv[3][0];
-    o1.w = (zc[11] + zh[3]) + sbv[3][1];
+    o0.x = (c4.x + l12.x) + sbv[0][0];
+    o0.y = (c4.y + l12.y) + sbv[0][1];
+    o0.z = (c4.z + l12.z) + sbv[1][0];
+    o0.w = (c4.w + l12.w) + sbv[1][1];
+    o1.x = (c8.x + h0.x) + sbv[2][0];
+    o1.y = (c8.y + h0.y) + sbv[2][1];
+    o1.z = (c8.z + h0.z) + sbv[3][0];
+    o1.w = (c8.w + h0.w) + sbv[3][1];
     float4* o = reinterpret_cast<float4*>(d.out + (item * (int64_t)d.T + 4 * (int64_t)u) * 2);
     o[0] = o0;
     o[1] = o1;

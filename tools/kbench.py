@@ -245,6 +245,11 @@ if __name__ == "__main__":
         gemm_case(M, 512, 2048)
         gemm_case(M, 512, 512)
         sys.exit(0)
+    if "zgemm" in sys.argv[1:]:           # the decoder's level-1 tap GEMM (fdec1.z): M = 256 items x 32 x 259, K = 192
+        VARIANTS = (40, 38, 108, 37, 137, 33, 133)
+        gemm_case(256 * 32 * 259, 768, 192)
+        gemm_case(M, 1536, 512)
+        sys.exit(0)
     if "g4" in sys.argv[1:]:
         gemm_case(M, 1536, 512)
         gemm_case(M, 2048, 512, act=1)
