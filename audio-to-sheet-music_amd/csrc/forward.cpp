@@ -78,6 +78,9 @@ struct Bufs {
     float *U, *Yb, *x_cond, *xt_cond;
     uint16_t* Ub;       // bf16 copy of U (throughput mode: A operand of text.mlp0)
     void* Hm;
+    float *Ut, *Ybt;    // the time branch's text cross-attention scratch (it runs on the second stream)
+    uint16_t* Ubt;
+    void* Hmt;
     float *G, *D, *FO;
     float* ola_part;    // boundary partial sums of the fused iSTFT (spectral.hip)
     LrStep* lrsteps;    // level-1 low-rank decoder step table (fdec_lr.hip)
@@ -138,6 +141,10 @@ size_t plan(Arena& ar, const Dims& d, Bufs& b, bool actbf) {
     b.Ub = actbf ? ar.take<uint16_t>(NI * d.Nmax * 384) : nullptr;
     b.Hm = act(NI * d.Nmax * 384);
     b.Yb = ar.take<float>(NI * d.Nmax * 384);
+    b.Ut = ar.take<float>(NI * d.Nt * 384);
+    b.Ubt = actbf ? ar.take<uint16_t>(NI * d.Nt * 384) : nullptr;
+    b.Hmt = act(NI * d.Nt * 384);
+    b.Ybt = ar.take<float>(NI * d.Nt * 384);
     b.x_cond = ar.take<float>(NI * d.Nf * 384);
     b.xt_cond = ar.take<float>(NI * d.Nt * 384);
     int64_t g = std::max<int64_t>(32 * Ts * 192, 2 * Ts * Ts * 96);
@@ -511,19 +518,20 @@ void encode(Run& r, const Dims& d, const Bufs& b, const float* wav) {
             block(Lt, b.XT, d.Nt, b.H[2], b.H[1], d.Nf, &pt, true);
         }
     }
-    r.s = s_f;
     gn_apply_launch(b.X, (int)B, d.Nf, 512, pf.st, pf.w, pf.b, s_f);
     gn_apply_launch(b.XT, (int)B, d.Nt, 512, pt.st, pt.w, pt.b, s_t);
-    (void)hipEventRecord(c->ev_t, s_t);          // join: the caller's stream continues after the time branch
-    (void)hipStreamWaitEvent(s_f, c->ev_t, 0);
     {
-        GemmDesc g = r.lin(c->down, b.X, 0, (int)B, d.Nf, 512);
-        g.C = b.x_enc;
-        r.gemm(g, "downsampler");
+        r.s = s_t;                               // the time branch's channel downsampler on its own stream
         GemmDesc gt = r.lin(c->down_t, b.XT, 0, (int)B, d.Nt, 512);
         gt.C = b.xt_enc;
         r.gemm(gt, "downsampler_t");
+        r.s = s_f;
+        GemmDesc g = r.lin(c->down, b.X, 0, (int)B, d.Nf, 512);
+        g.C = b.x_enc;
+        r.gemm(g, "downsampler");
     }
+    (void)hipEventRecord(c->ev_t, s_t);          // join: the caller's stream continues after the time branch
+    (void)hipStreamWaitEvent(s_f, c->ev_t, 0);
 }
 
 // ConvTranspose (k8, s4, p2) along H as two GEMMs, one per residue pair: output rows 4u+{0,1} read input rows
@@ -595,27 +603,27 @@ void decode_chunk(Run& r, const Dims& d, const Bufs& b, int64_t s0, int64_t Bc, 
     // ---- text cross-attention, closed form (ATHTDemucs_v2.py:38-58) ----
     text_vec_launch(text_per_item ? text + s0 * 512 : text, NI, P, text_per_item ? 1 : 0, c->ta_vw, c->ta_vb, c->ta_ivw,
                     c->ta_ivb, c->ta_ow, c->ta_ob, b.avec, r.s);
-    auto text_attn = [&](const float* enc, int64_t ntok, float* cond) {
+    auto text_attn = [&](const float* enc, int64_t ntok, float* cond, float* U, uint16_t* Ub, void* Hm, float* Yb) {
         KStage kst(ntok == d.Nf ? "text_attn.freq" : "text_attn.time");
-        add_rowvec_launch(enc, b.avec, NI, P, ntok, 384, b.U, b.Ub, r.s);
-        GemmDesc g = b.Ub ? r.lin(c->mlp0, b.Ub, 1, NI, ntok, 384) : r.lin(c->mlp0, b.U, 0, NI, ntok, 384);
-        g.C = b.Hm; g.c_bf16 = ab; g.act = ACT_GELU;
+        add_rowvec_launch(enc, b.avec, NI, P, ntok, 384, U, Ub, r.s);
+        GemmDesc g = Ub ? r.lin(c->mlp0, Ub, 1, NI, ntok, 384) : r.lin(c->mlp0, U, 0, NI, ntok, 384);
+        g.C = Hm; g.c_bf16 = ab; g.act = ACT_GELU;
         r.gemm(g, "text.mlp0");
-        GemmDesc g2 = r.lin(c->mlp2, b.Hm, ab, NI, ntok, 384);
-        g2.C = b.Yb; g2.res = b.U;
+        GemmDesc g2 = r.lin(c->mlp2, Hm, ab, NI, ntok, 384);
+        g2.C = Yb; g2.res = U;
         r.gemm(g2, "text.mlp2");
         LnDesc l;
-        l.x = b.Yb; l.nb = NI; l.N = ntok; l.C = 384; l.w = c->ta_nw; l.b = c->ta_nb; l.out = cond; l.out_bf16 = ab;
+        l.x = Yb; l.nb = NI; l.N = ntok; l.C = 384; l.w = c->ta_nw; l.b = c->ta_nb; l.out = cond; l.out_bf16 = ab;
         layernorm_launch(l, r.s);
     };
-    text_attn(b.x_enc + s0 * d.Nf * 384, d.Nf, b.x_cond);
-    text_attn(b.xt_enc + s0 * d.Nt * 384, d.Nt, b.xt_cond);
-    // fork: the time decoder (below, own Gt / Dt buffers) runs on the second stream beside the frequency decoder and
-    // the iSTFT; the branches join before istft_ola_kernel, which reads both
+    // fork after the prompt vectors: the time branch (its text cross-attention with its own U / Hm / Yb scratch, then
+    // the time decoder with its own Gt / Dt buffers) runs on the second stream beside the frequency branch and the
+    // iSTFT; the branches join before istft_ola_kernel, which reads both
     if (!second_stream(r)) return;
     hipStream_t const s_main = r.s, s_t = serial_branches(r) ? r.s : c->s_time;   // (see encode)
     (void)hipEventRecord(c->ev_f, s_main);
     (void)hipStreamWaitEvent(s_t, c->ev_f, 0);
+    text_attn(b.x_enc + s0 * d.Nf * 384, d.Nf, b.x_cond, b.U, b.Ub, b.Hm, b.Yb);
 
     // ---- frequency decoder (ATHTDemucs_v2.py:82-104, 293-297) ----
     const int ea = b.ea;
@@ -677,6 +685,7 @@ void decode_chunk(Run& r, const Dims& d, const Bufs& b, int64_t s0, int64_t Bc, 
     // ---- time decoder (ATHTDemucs_v2.py:125-139, 313-321) ----
     float* xt2 = nullptr;                            // time_out(time decoder) [NI][T][2]
     r.s = s_t;
+    text_attn(b.xt_enc + s0 * d.Nt * 384, d.Nt, b.xt_cond, b.Ut, b.Ubt, b.Hmt, b.Ybt);
     {
         const void* svt[4] = {eoff(b.saved_t[0], s0 * d.L[1] * 48, ea), eoff(b.saved_t[1], s0 * d.L[2] * 96, ea),
                               eoff(b.saved_t[2], s0 * d.L[3] * 192, ea), eoff(b.saved_t[3], s0 * d.L[4] * 384, ea)};
