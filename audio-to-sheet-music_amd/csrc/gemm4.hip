@@ -281,13 +281,14 @@ __global__ __launch_bounds__(512) void gemm4_kernel(const GemmDesc d) {
         // instead of before every branch-guarded use
 #pragma unroll
         for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(bias4[j].x), "v"(bias4[j].y), "v"(bias4[j].z), "v"(bias4[j].w));
+        bool fast = false;
         if constexpr ((F & F_RES) != 0 && (F & ~(F_RES | F_STATS)) == 0) {
             if (epi_res_fast_ok(d)) {
                 gemm_epilogue_res<TM, TN, F>(d, acc, m0_done, n0_done, wm0, wn0, lane, st_lds, 256, bias4);
-                return;
+                fast = true;
             }
         }
-        gemm_epilogue<TM, TN, F, true>(d, acc, m0_done, n0_done, wm0, wn0, lane, st_lds, 256, bias4);
+        if (!fast) gemm_epilogue<TM, TN, F, true>(d, acc, m0_done, n0_done, wm0, wn0, lane, st_lds, 256, bias4);
         if (!PERSIST || next >= ntiles) break;
         tile = next;
         // the epilogue's stores sit behind the staged K-tiles on the VM counter: drain all, then the next tile's bias
