@@ -303,6 +303,9 @@ int athd_finalize(athd_ctx* c) {
     }
     c->ta_ow = c->up_key("text_attn.attn.out_proj.weight");
     c->ta_ob = c->up_key("text_attn.attn.out_proj.bias");
+    c->ta_m0w = c->up_key("text_attn.out_mlp.0.weight");
+    c->ta_m0b = c->up_key("text_attn.out_mlp.0.bias");
+    c->ta_m2b = c->up_key("text_attn.out_mlp.2.bias");
     c->mlp0 = c->lin_gemm("text_attn.out_mlp.0.weight", "text_attn.out_mlp.0.bias");
     c->mlp2 = c->lin_gemm("text_attn.out_mlp.2.weight", "text_attn.out_mlp.2.bias");
     c->ta_nw = c->up_key("text_attn.norm_out.weight");

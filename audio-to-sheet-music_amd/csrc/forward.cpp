@@ -74,12 +74,10 @@ struct Bufs {
     float *Gt, *Dt;                   // the time decoder's ConvT / merge buffers (second stream too)
     float *pos2d, *pos1d, *x_enc, *xt_enc;
     // decode (per chunk)
-    float* avec;
-    float *U, *Yb, *x_cond, *xt_cond;
-    uint16_t* Ub;       // bf16 copy of U (throughput mode: A operand of text.mlp0)
+    float *avec, *tc0, *tc2;         // per-prompt attention vector and out_mlp row biases (text_vec_kernel)
+    float *Yb, *x_cond, *xt_cond;
     void* Hm;
-    float *Ut, *Ybt;    // the time branch's text cross-attention scratch (it runs on the second stream)
-    uint16_t* Ubt;
+    float* Ybt;         // the time branch's text cross-attention scratch (it runs on the second stream)
     void* Hmt;
     float *G, *D, *FO;
     float* ola_part;    // boundary partial sums of the fused iSTFT (spectral.hip)
@@ -137,12 +135,10 @@ size_t plan(Arena& ar, const Dims& d, Bufs& b, bool actbf) {
     // decode chunk
     const int64_t NI = d.Bc * d.P;
     b.avec = ar.take<float>(NI * 384);
-    b.U = ar.take<float>(NI * d.Nmax * 384);
-    b.Ub = actbf ? ar.take<uint16_t>(NI * d.Nmax * 384) : nullptr;
-    b.Hm = act(NI * d.Nmax * 384);
-    b.Yb = ar.take<float>(NI * d.Nmax * 384);
-    b.Ut = ar.take<float>(NI * d.Nt * 384);
-    b.Ubt = actbf ? ar.take<uint16_t>(NI * d.Nt * 384) : nullptr;
+    b.tc0 = ar.take<float>(NI * 384);
+    b.tc2 = ar.take<float>(NI * 384);
+    b.Hm = act(NI * d.Nf * 384);
+    b.Yb = ar.take<float>(NI * d.Nf * 384);
     b.Hmt = act(NI * d.Nt * 384);
     b.Ybt = ar.take<float>(NI * d.Nt * 384);
     b.x_cond = ar.take<float>(NI * d.Nf * 384);
@@ -602,15 +598,20 @@ void decode_chunk(Run& r, const Dims& d, const Bufs& b, int64_t s0, int64_t Bc, 
     const int ab = r.actbf ? 1 : 0;
     // ---- text cross-attention, closed form (ATHTDemucs_v2.py:38-58) ----
     text_vec_launch(text_per_item ? text + s0 * 512 : text, NI, P, text_per_item ? 1 : 0, c->ta_vw, c->ta_vb, c->ta_ivw,
-                    c->ta_ivb, c->ta_ow, c->ta_ob, b.avec, r.s);
-    auto text_attn = [&](const float* enc, int64_t ntok, float* cond, float* U, uint16_t* Ub, void* Hm, float* Yb) {
+                    c->ta_ivb, c->ta_ow, c->ta_ob, c->ta_m0w, c->ta_m0b, c->ta_m2b, b.avec, b.tc0, b.tc2, r.s);
+    // The prompt enters only through the row vector a = attn_out (one key: softmax == 1), so with u = x + a
+    // (ATHTDemucs_v2.py:46-48):  h = GELU(W0 u + b0) = GELU(W0 x + c0),  y = u + W2 h + b2 = x + W2 h + c2  (c0, c2 per
+    // prompt, text_vec_kernel).  text.mlp0 multiplies the SEGMENT's x once and its epilogue writes the P prompts' h
+    // (F_PB, pfold = P); text.mlp2 adds the segment's x as the residual (res_div = P) and the prompt's c2.
+    auto text_attn = [&](const float* enc, int64_t ntok, float* cond, void* Hm, float* Yb) {
         KStage kst(ntok == d.Nf ? "text_attn.freq" : "text_attn.time");
-        add_rowvec_launch(enc, b.avec, NI, P, ntok, 384, U, Ub, r.s);
-        GemmDesc g = Ub ? r.lin(c->mlp0, Ub, 1, NI, ntok, 384) : r.lin(c->mlp0, U, 0, NI, ntok, 384);
+        GemmDesc g = r.lin(c->mlp0, enc, 0, (int)Bc, ntok, 384);
+        g.bias = nullptr; g.pbias = b.tc0; g.pfold = P;
         g.C = Hm; g.c_bf16 = ab; g.act = ACT_GELU;
         r.gemm(g, "text.mlp0");
         GemmDesc g2 = r.lin(c->mlp2, Hm, ab, NI, ntok, 384);
-        g2.C = Yb; g2.res = U;
+        g2.bias = nullptr; g2.pbias = b.tc2;
+        g2.C = Yb; g2.res = enc; g2.res_div = P; g2.res_bs = ntok * 384;
         r.gemm(g2, "text.mlp2");
         LnDesc l;
         l.x = Yb; l.nb = NI; l.N = ntok; l.C = 384; l.w = c->ta_nw; l.b = c->ta_nb; l.out = cond; l.out_bf16 = ab;
@@ -623,7 +624,7 @@ void decode_chunk(Run& r, const Dims& d, const Bufs& b, int64_t s0, int64_t Bc, 
     hipStream_t const s_main = r.s, s_t = serial_branches(r) ? r.s : c->s_time;   // (see encode)
     (void)hipEventRecord(c->ev_f, s_main);
     (void)hipStreamWaitEvent(s_t, c->ev_f, 0);
-    text_attn(b.x_enc + s0 * d.Nf * 384, d.Nf, b.x_cond, b.U, b.Ub, b.Hm, b.Yb);
+    text_attn(b.x_enc + s0 * d.Nf * 384, d.Nf, b.x_cond, b.Hm, b.Yb);
 
     // ---- frequency decoder (ATHTDemucs_v2.py:82-104, 293-297) ----
     const int ea = b.ea;
@@ -685,7 +686,7 @@ void decode_chunk(Run& r, const Dims& d, const Bufs& b, int64_t s0, int64_t Bc, 
     // ---- time decoder (ATHTDemucs_v2.py:125-139, 313-321) ----
     float* xt2 = nullptr;                            // time_out(time decoder) [NI][T][2]
     r.s = s_t;
-    text_attn(b.xt_enc + s0 * d.Nt * 384, d.Nt, b.xt_cond, b.Ut, b.Ubt, b.Hmt, b.Ybt);
+    text_attn(b.xt_enc + s0 * d.Nt * 384, d.Nt, b.xt_cond, b.Hmt, b.Ybt);
     {
         const void* svt[4] = {eoff(b.saved_t[0], s0 * d.L[1] * 48, ea), eoff(b.saved_t[1], s0 * d.L[2] * 96, ea),
                               eoff(b.saved_t[2], s0 * d.L[3] * 192, ea), eoff(b.saved_t[3], s0 * d.L[4] * 384, ea)};

@@ -78,6 +78,13 @@ struct GemmDesc {
     int64_t gn_count = 0;             //   statistics {sum, sumsq} over gn_count elements and per-column
     const float* gn_w = nullptr;      //   affine (packed in the same column order as the weights)
     const float* gn_b = nullptr;
+    // per-batch bias (epilogue flag F_PB): v += pbias[ob][n] for output batch ob.  pfold > 1: every input batch b
+    // (M rows) yields pfold output batches ob = b * pfold + p (the P prompts of one segment), each with its own
+    // pbias row, stored at C + ob * c_bs.  res_div > 1: the residual of output batch ob is read from res batch
+    // ob / res_div at stride res_bs (a per-segment residual shared by its P prompts).
+    const float* pbias = nullptr;
+    int pfold = 1, res_div = 1;
+    int64_t res_bs = 0;
 };
 
 // Algorithmic work of one launch (prof.h): 2 M N K flops; bytes = unique activations read once + packed weights +
@@ -87,8 +94,9 @@ inline void gemm_work(const GemmDesc& d, int mode, double& flops, double& bytes)
     flops = 2.0 * M * d.N * d.K;
     const double nout = d.act == ACT_GLU ? d.N / 2 : d.N;
     bytes = (double)d.nb * d.H_in * d.W * d.C_in * (d.a_bf16 ? 2 : 4) + (double)d.N * d.K * (mode == 1 ? 2 : 4);
-    if (d.store) bytes += M * nout * (d.c_bf16 ? 2 : 4);
-    if (d.res) bytes += M * nout * 4;
+    if (d.store) bytes += M * nout * (d.c_bf16 ? 2 : 4) * (d.pfold > 1 ? d.pfold : 1);
+    if (d.res) bytes += M * nout * 4 / (d.res_div > 1 ? d.res_div : 1);
+    if (d.pbias) bytes += (double)d.nb * (d.pfold > 1 ? d.pfold : 1) * d.N * 4;
 }
 
 // mode: 0 = exact fp32 (v_mfma_f32_16x16x4_f32), 1 = bf16 (v_mfma_f32_16x16x32_bf16, fp32 accumulate)

@@ -19,7 +19,7 @@ constexpr int EPI_MAXG = 32;   // GroupNorm groups tracked per block in LDS
 
 enum EpiFlag : unsigned {
     F_GELU = 1u, F_GLU = 2u, F_RES = 4u, F_STATS = 8u, F_GN = 16u, F_ROWADD = 32u, F_SPLIT = 64u, F_CBF16 = 128u,
-    F_NOSTORE = 256u, F_ALL = 0xFFFFu
+    F_NOSTORE = 256u, F_PB = 512u, F_ALL = 0xFFFFu
 };
 
 inline unsigned epi_flags(const GemmDesc& d) {
@@ -33,6 +33,7 @@ inline unsigned epi_flags(const GemmDesc& d) {
     if (d.col_split) f |= F_SPLIT;
     if (d.c_bf16 && d.store) f |= F_CBF16;     // the output dtype is irrelevant when nothing is stored
     if (!d.store) f |= F_NOSTORE;
+    if (d.pbias) f |= F_PB;
     return f;
 }
 
@@ -41,7 +42,7 @@ inline unsigned epi_flags(const GemmDesc& d) {
     X(0u) X(F_CBF16) X(F_GELU) X(F_GELU | F_CBF16) X(F_RES) X(F_RES | F_STATS) X(F_GLU) X(F_GLU | F_ROWADD)    \
     X(F_STATS | F_NOSTORE) X(F_GN | F_GLU | F_RES) X(F_STATS) X(F_SPLIT | F_STATS) X(F_SPLIT)                  \
     X(F_SPLIT | F_STATS | F_CBF16) X(F_SPLIT | F_CBF16) X(F_GLU | F_CBF16) X(F_GLU | F_ROWADD | F_CBF16)         \
-    X(F_GN | F_GLU | F_RES | F_CBF16)
+    X(F_GN | F_GLU | F_RES | F_CBF16) X(F_GELU | F_CBF16 | F_PB) X(F_GELU | F_PB) X(F_RES | F_PB)
 
 // Publishes the LDS statistics partials before the per-block flush: the LDS atomics retired (lgkmcnt) + s_barrier.
 // Not __syncthreads(): that also waits vmcnt(0), i.e. for every output store of the tile to be acknowledged,
@@ -103,6 +104,7 @@ ATHD_DEV void gemm_epilogue(const GemmDesc& d, const f32x4_t (&acc)[TM][TN], int
     const bool f_split = GEN ? d.col_split != 0 : on<F>(F_SPLIT);
     const bool f_cbf = GEN ? d.c_bf16 != 0 : on<F>(F_CBF16);
     const bool f_store = GEN ? d.store != 0 : !on<F>(F_NOSTORE);
+    const bool f_pb = GEN ? d.pbias != nullptr : on<F>(F_PB);
 
     const int fr = lane & 15, fg = lane >> 4;
     const uint32_t M = (uint32_t)d.nb * d.H_out * d.W;       // < 2^31 on every use
@@ -194,12 +196,23 @@ ATHD_DEV void gemm_epilogue(const GemmDesc& d, const f32x4_t (&acc)[TM][TN], int
                     }
                 }
             } else {
+                // F_PB: per-batch bias; pfold output batches per input batch; residual batch = output batch / res_div
+                const int np = f_pb && d.pfold > 1 ? d.pfold : 1;
+                const int64_t inb = obase - (int64_t)b * c_bs;          // offset within the batch
+                for (int pp = 0; pp < np; ++pp) {
+                const int64_t bo = f_pb && d.pfold > 1 ? (int64_t)b * d.pfold + pp : (int64_t)b;   // output batch
+                const int64_t ob = bo * c_bs + inb;
+                const int64_t rbase = f_pb && d.res_div > 1 ? (bo / d.res_div) * d.res_bs + inb : ob;
                 uint2 pk_even = make_uint2(0u, 0u);
 #pragma unroll
                 for (int j = 0; j < TN; ++j) {
                     const int n = n0 + wn0 + 16 * j + 4 * fg;
                     if (n >= d.N) continue;
-                    const float bv[4] = {bj[j].x, bj[j].y, bj[j].z, bj[j].w};
+                    float bv[4] = {bj[j].x, bj[j].y, bj[j].z, bj[j].w};
+                    if (f_pb) {
+                        const float4 pq = *reinterpret_cast<const float4*>(d.pbias + bo * d.N + n);
+                        bv[0] += pq.x; bv[1] += pq.y; bv[2] += pq.z; bv[3] += pq.w;
+                    }
                     float o[4];
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
@@ -211,7 +224,7 @@ ATHD_DEV void gemm_epilogue(const GemmDesc& d, const f32x4_t (&acc)[TM][TN], int
                     }
                     if (f_res) {
                         float rr[4];
-                        ld_res4(d, obase + n, rr);
+                        ld_res4(d, rbase + n, rr);
 #pragma unroll
                         for (int q = 0; q < 4; ++q) o[q] = rr[q] + (d.res_scale ? d.res_scale[n + q] : 1.f) * o[q];
                     }
@@ -223,7 +236,7 @@ ATHD_DEV void gemm_epilogue(const GemmDesc& d, const f32x4_t (&acc)[TM][TN], int
                         }
                     }
                     if (f_store) {
-                        int64_t off = obase + n;
+                        int64_t off = ob + n;
                         bool st = true;
                         if (f_split) {
                             st = (d.store_mask >> grp[j]) & 1;
@@ -241,7 +254,7 @@ ATHD_DEV void gemm_epilogue(const GemmDesc& d, const f32x4_t (&acc)[TM][TN], int
                                     const auto rx = __builtin_amdgcn_permlane16_swap(pk_even.x, pk.x, false, false);
                                     const auto ry = __builtin_amdgcn_permlane16_swap(pk_even.y, pk.y, false, false);
                                     const int col = n0 + wn0 + 16 * (j - 1) + 16 * (fg & 1) + 8 * (fg >> 1);
-                                    *reinterpret_cast<uint4*>((bf16_t*)d.C + obase + col) = make_uint4(rx[0], ry[0], rx[1], ry[1]);
+                                    *reinterpret_cast<uint4*>((bf16_t*)d.C + ob + col) = make_uint4(rx[0], ry[0], rx[1], ry[1]);
                                 }
                             } else if (f_cbf) {
                                 *reinterpret_cast<uint2*>((bf16_t*)d.C + off) = make_uint2(pack2bf(o[0], o[1]), pack2bf(o[2], o[3]));
@@ -251,6 +264,7 @@ ATHD_DEV void gemm_epilogue(const GemmDesc& d, const f32x4_t (&acc)[TM][TN], int
                         }
                     }
                 }
+                }  // pp
             }
         }  // m < M
         if (f_stats && one_group) {
@@ -304,7 +318,7 @@ ATHD_DEV void gemm_epilogue(const GemmDesc& d, const f32x4_t (&acc)[TM][TN], int
 __device__ __attribute__((weak)) float4 g_epi_sink[64];
 
 ATHD_HD bool epi_res_fast_ok(const GemmDesc& d) {
-    return d.res && !d.res_bf16 && !d.c_bf16 && d.store && d.act == ACT_NONE && !d.gn_stats && !d.row_add &&
+    return d.res && !d.res_bf16 && !d.c_bf16 && d.store && d.act == ACT_NONE && !d.gn_stats && !d.row_add && !d.pbias &&
            !d.col_split && d.o_stride == 1 && d.o_off == 0 && d.H_out_total == d.H_out && d.c_bs < 0 && d.N % 4 == 0;
 }
 

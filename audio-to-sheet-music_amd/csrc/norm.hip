@@ -244,44 +244,18 @@ void layernorm_launch(const LnDesc& d, hipStream_t s) {
 // --------------------------------------------------------------------------------------------- text conditioning
 // U[item] = X[item / P] + a[item] (row vector over C); float4 lanes.  Ub (optional, throughput mode): a bf16 copy of U,
 // the A operand of the text MLP's first GEMM (U itself stays f32 for the residual of the second)
-__global__ __launch_bounds__(256) void add_rowvec_kernel(const float* __restrict__ X, const float* __restrict__ a,
-                                                         int P, int64_t ntok, int C, float* __restrict__ U,
-                                                         uint16_t* __restrict__ Ub) {
-    const int64_t item = blockIdx.y;
-    const int64_t b = item / P;
-    const int n4 = (int)(ntok * C / 4);
-    const float4* xp = reinterpret_cast<const float4*>(X + b * ntok * C);
-    float4* up = reinterpret_cast<float4*>(U + item * ntok * C);
-    uint2* ubp = Ub ? reinterpret_cast<uint2*>(Ub + item * ntok * C) : nullptr;
-    const float* ap = a + item * C;
-    const int C4 = C / 4;
-    for (int i = blockIdx.x * 256 + threadIdx.x; i < n4; i += gridDim.x * 256) {
-        const float4 x = xp[i];
-        const float4 av = *reinterpret_cast<const float4*>(ap + 4 * (i % C4));
-        const float4 u = make_float4(x.x + av.x, x.y + av.y, x.z + av.z, x.w + av.w);
-        up[i] = u;
-        if (ubp) ubp[i] = make_uint2(pack2bf(u.x, u.y), pack2bf(u.z, u.w));
-    }
-}
-
-void add_rowvec_launch(const float* X, const float* a, int NI, int P, int64_t ntok, int C, float* U, uint16_t* Ub,
-                       hipStream_t s) {
-    int blocks = (int)((ntok * C / 4 + 255) / 256);
-    if (blocks > 1024) blocks = 1024;
-    KScope ks(s);
-    if (ks.on()) ks.begin("add_rowvec_kernel", 0.0, (double)(NI / P + NI) * ntok * C * 4 + (Ub ? (double)NI * ntok * C * 2 : 0.0));
-    hipLaunchKernelGGL(add_rowvec_kernel, dim3(blocks, NI), dim3(256), 0, s, X, a, P, ntok, C, U, Ub);
-}
-
 __global__ __launch_bounds__(256) void text_vec_kernel(const float* __restrict__ text, int P, int per_item,
                                                        const float* __restrict__ wv, const float* __restrict__ bv,
                                                        const float* __restrict__ wiv, const float* __restrict__ biv,
                                                        const float* __restrict__ wo, const float* __restrict__ bo,
-                                                       float* __restrict__ a) {
+                                                       const float* __restrict__ w0, const float* __restrict__ b0,
+                                                       const float* __restrict__ b2, float* __restrict__ a,
+                                                       float* __restrict__ c0, float* __restrict__ c2) {
     constexpr int D = 384, TD = 512;
     __shared__ float t[TD];
     __shared__ float v[D];
     __shared__ float vi[D];
+    __shared__ float av[D];
     const int item = blockIdx.x;
     const float* tp = text + (int64_t)(per_item ? item : (item % P)) * TD;
     for (int i = threadIdx.x; i < TD; i += 256) t[i] = tp[i];
@@ -301,15 +275,29 @@ __global__ __launch_bounds__(256) void text_vec_kernel(const float* __restrict__
     for (int o = threadIdx.x; o < D; o += 256) {
         float s = 0.f;
         for (int k = 0; k < D; ++k) s += wo[(int64_t)o * D + k] * vi[k];
-        a[(int64_t)item * D + o] = s + bo[o];
+        av[o] = s + bo[o];
+        a[(int64_t)item * D + o] = av[o];
+    }
+    if (!c0) return;                      // (block-uniform)
+    __syncthreads();
+    // the prompt's row biases of the out_mlp (ATHTDemucs_v2.py:46-48 with queries + a, a constant over tokens):
+    //   mlp0(x + a) = W0 x + (W0 a + b0)   ->  c0 = W0 a + b0
+    //   (x + a) + mlp2(h) = x + W2 h + (a + b2)   ->  c2 = a + b2
+    for (int o = threadIdx.x; o < D; o += 256) {
+        float s = 0.f;
+        for (int k = 0; k < D; ++k) s += w0[(int64_t)o * D + k] * av[k];
+        c0[(int64_t)item * D + o] = s + b0[o];
+        c2[(int64_t)item * D + o] = av[o] + b2[o];
     }
 }
 
 void text_vec_launch(const float* text, int NI, int P, int text_per_item, const float* wv, const float* bv,
-                     const float* wiv, const float* biv, const float* wo, const float* bo, float* a, hipStream_t s) {
+                     const float* wiv, const float* biv, const float* wo, const float* bo, const float* w0,
+                     const float* b0, const float* b2, float* a, float* c0, float* c2, hipStream_t s) {
     KScope ks(s);
-    if (ks.on()) ks.begin("text_vec_kernel", 2.0 * NI * (512.0 * 512 * 2 + 384.0 * 512), (512.0 * 512 * 2 + 384.0 * 512) * 4);
-    hipLaunchKernelGGL(text_vec_kernel, dim3(NI), dim3(256), 0, s, text, P, text_per_item, wv, bv, wiv, biv, wo, bo, a);
+    if (ks.on()) ks.begin("text_vec_kernel", 2.0 * NI * (512.0 * 384 + 384.0 * 384 * 3), (512.0 * 384 + 384.0 * 384 * 3) * 4);
+    hipLaunchKernelGGL(text_vec_kernel, dim3(NI), dim3(256), 0, s, text, P, text_per_item, wv, bv, wiv, biv, wo, bo, w0,
+                       b0, b2, a, c0, c2);
 }
 
 // --------------------------------------------------------------------------------------------- decoder merge
