@@ -73,6 +73,7 @@ struct Bufs {
     void *QKVt, *Ot, *F1t;            // the time branch's scratch (it runs on its own stream beside the freq branch)
     float *Gt, *Dt;                   // the time decoder's ConvT / merge buffers (second stream too)
     float *pos2d, *pos1d, *x_enc, *xt_enc;
+    uint16_t *x_enc_b, *xt_enc_b;     // bf16 copies (throughput mode): the A operand of text.mlp0
     // decode (per chunk)
     float *avec, *tc0, *tc2;         // per-prompt attention vector and out_mlp row biases (text_vec_kernel)
     float *Yb, *x_cond, *xt_cond;
@@ -132,6 +133,8 @@ size_t plan(Arena& ar, const Dims& d, Bufs& b, bool actbf) {
     b.pos1d = ar.take<float>(d.Nt * 512);
     b.x_enc = ar.take<float>(B * d.Nf * 384);
     b.xt_enc = ar.take<float>(B * d.Nt * 384);
+    b.x_enc_b = actbf ? ar.take<uint16_t>(B * d.Nf * 384) : nullptr;
+    b.xt_enc_b = actbf ? ar.take<uint16_t>(B * d.Nt * 384) : nullptr;
     // decode chunk
     const int64_t NI = d.Bc * d.P;
     b.avec = ar.take<float>(NI * 384);
@@ -521,10 +524,12 @@ void encode(Run& r, const Dims& d, const Bufs& b, const float* wav) {
         GemmDesc gt = r.lin(c->down_t, b.XT, 0, (int)B, d.Nt, 512);
         gt.C = b.xt_enc;
         r.gemm(gt, "downsampler_t");
+        if (b.xt_enc_b) to_bf16_launch(b.xt_enc, b.xt_enc_b, B * d.Nt * 384, s_t);
         r.s = s_f;
         GemmDesc g = r.lin(c->down, b.X, 0, (int)B, d.Nf, 512);
         g.C = b.x_enc;
         r.gemm(g, "downsampler");
+        if (b.x_enc_b) to_bf16_launch(b.x_enc, b.x_enc_b, B * d.Nf * 384, s_f);
     }
     (void)hipEventRecord(c->ev_t, s_t);          // join: the caller's stream continues after the time branch
     (void)hipStreamWaitEvent(s_f, c->ev_t, 0);
@@ -603,9 +608,9 @@ void decode_chunk(Run& r, const Dims& d, const Bufs& b, int64_t s0, int64_t Bc, 
     // (ATHTDemucs_v2.py:46-48):  h = GELU(W0 u + b0) = GELU(W0 x + c0),  y = u + W2 h + b2 = x + W2 h + c2  (c0, c2 per
     // prompt, text_vec_kernel).  text.mlp0 multiplies the SEGMENT's x once and its epilogue writes the P prompts' h
     // (F_PB, pfold = P); text.mlp2 adds the segment's x as the residual (res_div = P) and the prompt's c2.
-    auto text_attn = [&](const float* enc, int64_t ntok, float* cond, void* Hm, float* Yb) {
+    auto text_attn = [&](const float* enc, const uint16_t* enc_b, int64_t ntok, float* cond, void* Hm, float* Yb) {
         KStage kst(ntok == d.Nf ? "text_attn.freq" : "text_attn.time");
-        GemmDesc g = r.lin(c->mlp0, enc, 0, (int)Bc, ntok, 384);
+        GemmDesc g = enc_b ? r.lin(c->mlp0, enc_b, 1, (int)Bc, ntok, 384) : r.lin(c->mlp0, enc, 0, (int)Bc, ntok, 384);
         g.bias = nullptr; g.pbias = b.tc0; g.pfold = P;
         g.C = Hm; g.c_bf16 = ab; g.act = ACT_GELU;
         r.gemm(g, "text.mlp0");
@@ -624,7 +629,7 @@ void decode_chunk(Run& r, const Dims& d, const Bufs& b, int64_t s0, int64_t Bc, 
     hipStream_t const s_main = r.s, s_t = serial_branches(r) ? r.s : c->s_time;   // (see encode)
     (void)hipEventRecord(c->ev_f, s_main);
     (void)hipStreamWaitEvent(s_t, c->ev_f, 0);
-    text_attn(b.x_enc + s0 * d.Nf * 384, d.Nf, b.x_cond, b.Hm, b.Yb);
+    text_attn(b.x_enc + s0 * d.Nf * 384, b.x_enc_b ? b.x_enc_b + s0 * d.Nf * 384 : nullptr, d.Nf, b.x_cond, b.Hm, b.Yb);
 
     // ---- frequency decoder (ATHTDemucs_v2.py:82-104, 293-297) ----
     const int ea = b.ea;
@@ -686,7 +691,7 @@ void decode_chunk(Run& r, const Dims& d, const Bufs& b, int64_t s0, int64_t Bc, 
     // ---- time decoder (ATHTDemucs_v2.py:125-139, 313-321) ----
     float* xt2 = nullptr;                            // time_out(time decoder) [NI][T][2]
     r.s = s_t;
-    text_attn(b.xt_enc + s0 * d.Nt * 384, d.Nt, b.xt_cond, b.Hmt, b.Ybt);
+    text_attn(b.xt_enc + s0 * d.Nt * 384, b.xt_enc_b ? b.xt_enc_b + s0 * d.Nt * 384 : nullptr, d.Nt, b.xt_cond, b.Hmt, b.Ybt);
     {
         const void* svt[4] = {eoff(b.saved_t[0], s0 * d.L[1] * 48, ea), eoff(b.saved_t[1], s0 * d.L[2] * 96, ea),
                               eoff(b.saved_t[2], s0 * d.L[3] * 192, ea), eoff(b.saved_t[3], s0 * d.L[4] * 384, ea)};

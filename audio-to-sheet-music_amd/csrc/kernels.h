@@ -63,6 +63,8 @@ struct LnDesc {
     void* out = nullptr; int out_bf16 = 0;
 };
 void layernorm_launch(const LnDesc& d, hipStream_t s);
+// y = bf16(x), n % 8 == 0 (round to nearest even)
+void to_bf16_launch(const float* x, uint16_t* y, int64_t n, hipStream_t s);
 // a[item] = out_proj(in_v(v_proj(text[item])))   (TextCrossAttention closed form, 384 <- 512), and the prompt's
 // out_mlp row biases c0[item] = W0 a + b0, c2[item] = a + b2 (c0 == nullptr: a only)
 void text_vec_launch(const float* text, int NI, int P, int text_per_item, const float* wv, const float* bv,

@@ -1,3 +1,4 @@
+#include <algorithm>
 // Normalisation, elementwise, resize/merge and table kernels of the hot path (gfx950).
 // GroupNorm/LayerNorm statistics are accumulated in fp64 (sum, sum of squares) so that the one-pass
 // variance matches PyTorch's fp32 two-pass/Welford results to rounding.
@@ -244,6 +245,23 @@ void layernorm_launch(const LnDesc& d, hipStream_t s) {
 // --------------------------------------------------------------------------------------------- text conditioning
 // U[item] = X[item / P] + a[item] (row vector over C); float4 lanes.  Ub (optional, throughput mode): a bf16 copy of U,
 // the A operand of the text MLP's first GEMM (U itself stays f32 for the residual of the second)
+// bf16 copy of an fp32 tensor (n % 8 == 0), round-to-nearest-even as every GEMM's fp32-A conversion (f2bf): the
+// segment features x_enc / xt_enc for the bf16-A text.mlp0 GEMM (numerically what gemm2's fp32-A path multiplies)
+__global__ __launch_bounds__(256) void to_bf16_kernel(const float* __restrict__ x, uint16_t* __restrict__ y, int64_t n8) {
+    for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n8; i += (int64_t)gridDim.x * 256) {
+        const float4 a = reinterpret_cast<const float4*>(x)[2 * i], b = reinterpret_cast<const float4*>(x)[2 * i + 1];
+        reinterpret_cast<uint4*>(y)[i] = make_uint4(pack2bf(a.x, a.y), pack2bf(a.z, a.w), pack2bf(b.x, b.y), pack2bf(b.z, b.w));
+    }
+}
+
+void to_bf16_launch(const float* x, uint16_t* y, int64_t n, hipStream_t s) {
+    const int64_t n8 = n / 8;
+    const int blocks = (int)std::min<int64_t>((n8 + 255) / 256, 4096);
+    KScope ks(s);
+    if (ks.on()) ks.begin("to_bf16_kernel", 0.0, (double)n * 6);
+    hipLaunchKernelGGL(to_bf16_kernel, dim3(blocks), dim3(256), 0, s, x, y, n8);
+}
+
 __global__ __launch_bounds__(256) void text_vec_kernel(const float* __restrict__ text, int P, int per_item,
                                                        const float* __restrict__ wv, const float* __restrict__ bv,
                                                        const float* __restrict__ wiv, const float* __restrict__ biv,
