@@ -593,6 +593,16 @@ void conv_t(Run& r, const DecW& w, const void* A, int a_bf16, int nb, int H_in, 
     }
 }
 
+// ATHD_TEXT_LN=0: the text cross-attention's norm_out as a separate LayerNorm pass in the bf16 mode too (A/B)
+static bool text_ln_off() {
+    static int off = -1;
+    if (off < 0) {
+        const char* e = std::getenv("ATHD_TEXT_LN");
+        off = e && *e == '0' ? 1 : 0;
+    }
+    return off == 1;
+}
+
 void decode_chunk(Run& r, const Dims& d, const Bufs& b, int64_t s0, int64_t Bc, const float* text, bool text_per_item,
                   float* out) {
     athd_ctx* c = r.c;
@@ -617,6 +627,13 @@ void decode_chunk(Run& r, const Dims& d, const Bufs& b, int64_t s0, int64_t Bc, 
         GemmDesc g2 = r.lin(c->mlp2, Hm, ab, NI, ntok, 384);
         g2.bias = nullptr; g2.pbias = b.tc2;
         g2.C = Yb; g2.res = enc; g2.res_div = P; g2.res_bs = ntok * 384;
+        if (r.actbf && !text_ln_off()) {
+            // bf16 mode: norm_out in the GEMM's epilogue (gemm3 row-LayerNorm variant: 128 x 384 tiles hold whole
+            // rows), x_cond written directly; Yb is not used
+            g2.C = cond; g2.c_bf16 = 1; g2.ln_w = c->ta_nw; g2.ln_b = c->ta_nb;
+            r.gemm(g2, "text.mlp2.ln");
+            return;
+        }
         r.gemm(g2, "text.mlp2");
         LnDesc l;
         l.x = Yb; l.nb = NI; l.N = ntok; l.C = 384; l.w = c->ta_nw; l.b = c->ta_nb; l.out = cond; l.out_bf16 = ab;

@@ -85,6 +85,10 @@ struct GemmDesc {
     const float* pbias = nullptr;
     int pfold = 1, res_div = 1;
     int64_t res_bs = 0;
+    // LayerNorm over each output row (epilogue flag F_LN; gemm3 with one N tile per row, N == BN): the row's values
+    // v are stored as (v - mean) * rstd * ln_w[n] + ln_b[n] (eps 1e-5, two-pass statistics as layernorm_kernel)
+    const float* ln_w = nullptr;
+    const float* ln_b = nullptr;
 };
 
 // Algorithmic work of one launch (prof.h): 2 M N K flops; bytes = unique activations read once + packed weights +

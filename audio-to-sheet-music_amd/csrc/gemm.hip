@@ -281,6 +281,7 @@ bool gemm2_supported(const GemmDesc& d);
 int gemm2_launch(const GemmDesc& d, hipStream_t s);
 bool gemm3_supported(const GemmDesc& d);
 int gemm3_launch(const GemmDesc& d, hipStream_t s, int variant);
+int gemm3_ln_launch(const GemmDesc& d, hipStream_t s);
 bool gemm4_supported(const GemmDesc& d);
 int gemm4_launch(const GemmDesc& d, hipStream_t s);
 
@@ -288,6 +289,7 @@ int gemm_launch(const GemmDesc& d0, int mode, hipStream_t s) {
     if (d0.Kp % BK != 0 || d0.Kp < d0.K || d0.C_in <= 0 || d0.N <= 0) return -2;
     const GemmDesc d = with_fastdiv(d0);
     if (d.act == ACT_GLU && (d.N % 32 != 0)) return -2;
+    if (d.ln_w) return mode == 1 ? gemm3_ln_launch(d, s) : -2;      // row-LayerNorm epilogue: gemm3 only
     // bf16 activations, N a multiple of 256: 256x256 tile, half-tile staged pipeline (gemm4.hip).  (Measured on
     // N = 192 / 384: slower than gemm3's 256x192 tiles, which waste no columns.)
     if (mode == 1 && gemm4_supported(d) && d.N % 256 == 0) return gemm4_launch(d, s);

@@ -29,6 +29,94 @@ ATHD_DEV int xcd_remap(int i, int n) {
     return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i / 8;
 }
 
+// F_LN epilogue (the text cross-attention's mlp2 + norm_out, ATHTDemucs_v2.py:47-49): BN == N, so a tile holds whole
+// output rows.  v = acc + pbias[batch] (+ bias) + residual (batch / res_div, f32), then LayerNorm over the row: the
+// row's partial sums over each wave's BN / WN columns meet in LDS (red: [2][BM][WN] floats), mean first, then the
+// sum of squared deviations (layernorm_kernel's two-pass form), and the normalised row leaves as bf16.
+template <int BM, int BN, int WM, int WN, int TM, int TN>
+ATHD_DEV void gemm3_epilogue_ln(const GemmDesc& d, f32x4_t (&acc)[TM][TN], int64_t m0, int wm0, int wn0, int lane,
+                                int wcol, float* red, const float4 (&bj)[TN]) {
+    const int fr = lane & 15, fg = lane >> 4;
+    const uint32_t M = (uint32_t)d.nb * d.H_out * d.W;
+    float rs[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+        const uint32_t m = (uint32_t)m0 + wm0 + 16 * i + fr;
+        const uint32_t mm = m < M ? m : M - 1;
+        const uint32_t b = fdiv(mm, d.fd_hw);
+        const int64_t inb = (int64_t)(mm - b * (uint32_t)d.H_out * (uint32_t)d.W) * d.ldo;
+        const int64_t rbase = (d.res_div > 1 ? (int64_t)(b / d.res_div) * d.res_bs : (int64_t)b * d.H_out * d.W * d.ldo) + inb;
+        float s = 0.f;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int n = wn0 + 16 * j + 4 * fg;
+            float4 pb = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (d.pbias) pb = *reinterpret_cast<const float4*>(d.pbias + (int64_t)b * d.N + n);
+            float4 rr = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (d.res) rr = *reinterpret_cast<const float4*>((const float*)d.res + rbase + n);
+            acc[i][j][0] = rr.x + (acc[i][j][0] + bj[j].x + pb.x);
+            acc[i][j][1] = rr.y + (acc[i][j][1] + bj[j].y + pb.y);
+            acc[i][j][2] = rr.z + (acc[i][j][2] + bj[j].z + pb.z);
+            acc[i][j][3] = rr.w + (acc[i][j][3] + bj[j].w + pb.w);
+            s += (acc[i][j][0] + acc[i][j][1]) + (acc[i][j][2] + acc[i][j][3]);
+        }
+        s += __shfl_xor(s, 16, 64);
+        s += __shfl_xor(s, 32, 64);
+        rs[i] = s;
+    }
+    if (fg == 0) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) red[(wm0 + 16 * i + fr) * WN + wcol] = rs[i];
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    float mean[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+        float t = 0.f;
+#pragma unroll
+        for (int c = 0; c < WN; ++c) t += red[(wm0 + 16 * i + fr) * WN + c];
+        mean[i] = t * (1.f / (float)BN);
+        float q = 0.f;
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const float dv = acc[i][j][e] - mean[i];
+                q += dv * dv;
+            }
+        q += __shfl_xor(q, 16, 64);
+        q += __shfl_xor(q, 32, 64);
+        rs[i] = q;
+    }
+    float* red2 = red + BM * WN;
+    if (fg == 0) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) red2[(wm0 + 16 * i + fr) * WN + wcol] = rs[i];
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+        const uint32_t m = (uint32_t)m0 + wm0 + 16 * i + fr;
+        float t = 0.f;
+#pragma unroll
+        for (int c = 0; c < WN; ++c) t += red2[(wm0 + 16 * i + fr) * WN + c];
+        const float rstd = 1.f / sqrtf(t * (1.f / (float)BN) + 1e-5f);
+        if (m >= M) continue;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int n = wn0 + 16 * j + 4 * fg;
+            const float4 lw = *reinterpret_cast<const float4*>(d.ln_w + n), lb = *reinterpret_cast<const float4*>(d.ln_b + n);
+            const float y0 = (acc[i][j][0] - mean[i]) * rstd * lw.x + lb.x;
+            const float y1 = (acc[i][j][1] - mean[i]) * rstd * lw.y + lb.y;
+            const float y2 = (acc[i][j][2] - mean[i]) * rstd * lw.z + lb.z;
+            const float y3 = (acc[i][j][3] - mean[i]) * rstd * lw.w + lb.w;
+            *reinterpret_cast<uint2*>((bf16_t*)d.C + (int64_t)m * d.ldo + n) = make_uint2(pack2bf(y0, y1), pack2bf(y2, y3));
+        }
+    }
+}
+
 template <int BM, int BN, int WM, int WN, int STAGES, unsigned F>
 __global__ __launch_bounds__(WM * WN * 64) void gemm3_kernel(const GemmDesc d) {
     constexpr int NW = WM * WN;
@@ -178,7 +266,13 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm3_kernel(const GemmDesc d) {
         }
 #pragma unroll
         for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(bias4[j].x), "v"(bias4[j].y), "v"(bias4[j].z), "v"(bias4[j].w));
-        gemm_epilogue<TM, TN, F, true>(d, acc, m0_done, n0, wm0, wn0, lane, st_lds, BM, bias4);
+        if constexpr ((F & F_LN) != 0) {
+            // the last ring stage is free here (the next tile's prologue filled stages 0 .. STAGES-2)
+            gemm3_epilogue_ln<BM, BN, WM, WN, TM, TN>(d, acc, m0_done, wm0, wn0, lane, wave % WN,
+                                                      reinterpret_cast<float*>(smem + (STAGES - 1) * STAGE), bias4);
+        } else {
+            gemm_epilogue<TM, TN, F, true>(d, acc, m0_done, n0, wm0, wn0, lane, st_lds, BM, bias4);
+        }
         if (next >= ntm) break;
         tile = next;
 #pragma unroll
@@ -238,10 +332,20 @@ static void launch3(const GemmDesc& d, hipStream_t s, bool persist) {
     }
 }
 
+// the row-LayerNorm epilogue exists only here (gemm3_ln_launch): BN == N
+static constexpr unsigned F_TEXT_LN = F_RES | F_PB | F_LN | F_CBF16;
+
 // variant: 0 = auto, 1 = 256x128 (8 waves, 3 stages), 2 = 128x128 (4 waves, 3 stages), 3 = 256x192 (8 waves, 2 st),
 // 4 = 128x192 (4 waves, 2 stages: 80 KB LDS, 2 blocks/CU), 5 = 128x192 (4 waves, 3 stages), 6 = 128x96 (4 waves, 3 st),
 // 7 = 192x192 (8 waves, 3 stages: 144 KB LDS), 8 = 128x192 (8 waves, 2 stages: 80 KB, 2 blocks/CU); + 100: persistent
 // grid (resident blocks walk the M tiles)
+int gemm3_ln_launch(const GemmDesc& d, hipStream_t s) {
+    if (epi_flags(d) != F_TEXT_LN || d.N != 384 || !gemm3_supported(d) || d.ldo != 384 || d.res_bf16 || d.col_off != 0)
+        return -2;
+    launch3f<128, 384, 2, 4, 2, F_TEXT_LN>(d, s, true);
+    return (int)hipGetLastError();
+}
+
 int gemm3_launch(const GemmDesc& d, hipStream_t s, int variant) {
     const bool persist = variant >= 100;
     if (persist) variant -= 100;

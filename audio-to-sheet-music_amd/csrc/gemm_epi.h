@@ -19,7 +19,7 @@ constexpr int EPI_MAXG = 32;   // GroupNorm groups tracked per block in LDS
 
 enum EpiFlag : unsigned {
     F_GELU = 1u, F_GLU = 2u, F_RES = 4u, F_STATS = 8u, F_GN = 16u, F_ROWADD = 32u, F_SPLIT = 64u, F_CBF16 = 128u,
-    F_NOSTORE = 256u, F_PB = 512u, F_ALL = 0xFFFFu
+    F_NOSTORE = 256u, F_PB = 512u, F_LN = 1024u, F_ALL = 0xFFFFu
 };
 
 inline unsigned epi_flags(const GemmDesc& d) {
@@ -34,6 +34,7 @@ inline unsigned epi_flags(const GemmDesc& d) {
     if (d.c_bf16 && d.store) f |= F_CBF16;     // the output dtype is irrelevant when nothing is stored
     if (!d.store) f |= F_NOSTORE;
     if (d.pbias) f |= F_PB;
+    if (d.ln_w) f |= F_LN;
     return f;
 }
 
