@@ -656,10 +656,13 @@ void decode_chunk(Run& r, const Dims& d, const Bufs& b, int64_t s0, int64_t Bc, 
         // level 0: 8 -> 32 rows, GN+GELU (in place, fp32: every source row feeds ~Ts/32 output rows), resize to
         // Tspec rows, + 0.1 * resize(saved[3][:, :192])
         double* st = r.stats(NI);
-        conv_t(r, c->fdec[0], b.x_cond, ab, NI, 8, (int)Ts, b.G, 0, st, -1, "fdec0");
+        // (bf16 mode: the ConvT output G as bf16, its GroupNorm statistics taken by the GEMM epilogue before rounding)
+        conv_t(r, c->fdec[0], b.x_cond, ab, NI, 8, (int)Ts, b.G, ab, st, -1, "fdec0");
         KStage kst("fdec0");
         // S = GELU(GN(ConvT0)): in place (fp32 mode) or as a bf16 copy, the A operand of the level-1 tap GEMM
-        if (r.actbf) gn_gelu_bf16_launch(b.G, (uint16_t*)b.S, NI, 32 * Ts * 192, 192, st, c->fdec[0].gnw, c->fdec[0].gnb, r.s);
+        if (r.actbf)
+            gn_gelu_bf16in_launch((const uint16_t*)b.G, (uint16_t*)b.S, NI, 32 * Ts * 192, 192, st, c->fdec[0].gnw,
+                                  c->fdec[0].gnb, r.s);
         else gn_gelu_launch(b.G, NI, 32 * Ts * 192, 192, st, c->fdec[0].gnw, c->fdec[0].gnb, r.s, false);
         // level 1 from the 32-row S = GELU(GN(ConvT0)) without materialising the resized 259-row input
         // (fdec_lr.hip): Z = S @ [W_0 .. W_7], Zs = skip3[:, :192] @ [W_0 .. W_7], then stats + merge passes

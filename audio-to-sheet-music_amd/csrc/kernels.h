@@ -50,6 +50,8 @@ void gn_gelu_launch(float* h, int nb, int64_t per_batch, int H, const double* st
 // out[nb][per_batch] (bf16) = GELU_fast(GN(h)); per_batch % 8 == 0, H % 8 == 0
 void gn_gelu_bf16_launch(const float* h, uint16_t* out, int nb, int64_t per_batch, int H, const double* stats,
                          const float* w, const float* b, hipStream_t s);
+void gn_gelu_bf16in_launch(const uint16_t* h, uint16_t* out, int nb, int64_t per_batch, int H, const double* stats,
+                           const float* w, const float* b, hipStream_t s);
 // x[nb][N][C] = GN(x) in place
 void gn_apply_launch(float* x, int nb, int64_t N, int C, const double* stats, const float* w, const float* b,
                      hipStream_t s);

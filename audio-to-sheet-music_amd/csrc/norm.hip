@@ -74,20 +74,33 @@ __global__ __launch_bounds__(256) void gn_gelu_kernel(float* __restrict__ h, int
     }
 }
 
-// bf16-mode variant writing a separate bf16 copy (the fp32 input stays intact): 8 elements per thread
-__global__ __launch_bounds__(256) void gn_gelu_bf16_kernel(const float* __restrict__ h, bf16_t* __restrict__ out,
+// bf16-mode variant writing a separate bf16 copy (the input stays intact): 8 elements per thread; the input is fp32,
+// or bf16 (IB: the decoder's level-0 ConvT output, whose statistics its GEMM epilogue took before rounding)
+template <bool IB>
+__global__ __launch_bounds__(256) void gn_gelu_bf16_kernel(const void* __restrict__ h, bf16_t* __restrict__ out,
                                                            int64_t per_batch, int H, const double* __restrict__ st,
                                                            const float* __restrict__ w, const float* __restrict__ bb) {
     const int64_t b = blockIdx.y;
     float mean, rstd;
     gn_params(st, b, per_batch, mean, rstd);
-    const float* p = h + b * per_batch;
     bf16_t* o = out + b * per_batch;
     const int n8 = (int)(per_batch / 8);
     for (int i = blockIdx.x * 256 + threadIdx.x; i < n8; i += gridDim.x * 256) {
-        const float4 u = *reinterpret_cast<const float4*>(p + 8 * (int64_t)i);
-        const float4 v = *reinterpret_cast<const float4*>(p + 8 * (int64_t)i + 4);
-        const float x[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
+        float x[8];
+        if constexpr (IB) {
+            const uint4 q = *reinterpret_cast<const uint4*>((const bf16_t*)h + b * per_batch + 8 * (int64_t)i);
+            const uint32_t qq[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                x[2 * k] = __uint_as_float(qq[k] << 16);
+                x[2 * k + 1] = __uint_as_float(qq[k] & 0xFFFF0000u);
+            }
+        } else {
+            const float* p = (const float*)h + b * per_batch;
+            const float4 u = *reinterpret_cast<const float4*>(p + 8 * (int64_t)i);
+            const float4 v = *reinterpret_cast<const float4*>(p + 8 * (int64_t)i + 4);
+            x[0] = u.x; x[1] = u.y; x[2] = u.z; x[3] = u.w; x[4] = v.x; x[5] = v.y; x[6] = v.z; x[7] = v.w;
+        }
         const int c0 = (8 * i) % H;
         bf16_t r[8];
 #pragma unroll
@@ -101,8 +114,17 @@ void gn_gelu_bf16_launch(const float* h, bf16_t* out, int nb, int64_t per_batch,
     int blocks = (int)((per_batch / 8 + 255) / 256);
     if (blocks > 1024) blocks = 1024;
     KScope ks(s);
-    if (ks.on()) ks.begin("gn_gelu_bf16_kernel", 0.0, (double)nb * per_batch * (4 + 2));
-    hipLaunchKernelGGL(gn_gelu_bf16_kernel, dim3(blocks, nb), dim3(256), 0, s, h, out, per_batch, H, stats, w, b);
+    if (ks.on()) ks.begin("gn_gelu_bf16_kernel<false>", 0.0, (double)nb * per_batch * (4 + 2));
+    hipLaunchKernelGGL(gn_gelu_bf16_kernel<false>, dim3(blocks, nb), dim3(256), 0, s, h, out, per_batch, H, stats, w, b);
+}
+
+void gn_gelu_bf16in_launch(const uint16_t* h, uint16_t* out, int nb, int64_t per_batch, int H, const double* stats,
+                           const float* w, const float* b, hipStream_t s) {
+    int blocks = (int)((per_batch / 8 + 255) / 256);
+    if (blocks > 1024) blocks = 1024;
+    KScope ks(s);
+    if (ks.on()) ks.begin("gn_gelu_bf16_kernel<true>", 0.0, (double)nb * per_batch * (2 + 2));
+    hipLaunchKernelGGL(gn_gelu_bf16_kernel<true>, dim3(blocks, nb), dim3(256), 0, s, h, out, per_batch, H, stats, w, b);
 }
 
 void gn_gelu_launch(float* h, int nb, int64_t per_batch, int H, const double* stats, const float* w, const float* b,
