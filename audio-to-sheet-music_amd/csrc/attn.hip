@@ -753,7 +753,8 @@ __global__ __launch_bounds__(256, MINW) void attn32_kernel(const AttnDesc d) {
 // LDS-DMA staging 849 / 777.  Tried and dropped: a software-pipelined form (QK^T of tile t+1 issued before the
 // softmax of tile t, 3-deep K/V ring: 761 vs 804 TFLOP/s), 64 queries per wave on register staging (256 VGPRs with
 // spills: 757) and on LDS-DMA staging (two 32-query blocks sharing every K / V fragment read, 2 waves per workgroup,
-// 2 waves per SIMD at 255 VGPRs: 765 / 648 vs 845 / 776).
+// 2 waves per SIMD at 255 VGPRs: 765 / 648 vs 845 / 776), and 192-query workgroups (6 waves; 2 % tail waste at
+// N = 2072 instead of 5 %, DMA pieces shared by 6 waves): 729-739 / 614-630 vs 853 / 781 on one box.
 int g_attn_variant = -1;
 static int attn_variant() {
     if (g_attn_variant < 0) {
