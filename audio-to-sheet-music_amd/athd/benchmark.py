@@ -190,22 +190,38 @@ class TrackResult:
     sisdr_avg: float
 
 
+def track_result(track_name: str, model_name: str, estimates: Dict[str, torch.Tensor],
+                 reference_stems: Dict[str, torch.Tensor],
+                 metric_fn: Optional[Callable] = None) -> TrackResult:
+    """Per stem SDR / SI-SDR on the common length and their averages (`benchmark.py:655-688`).  metric_fn(est,
+    ref) -> (sdr, sisdr) defaults to the native kernels (compute_sdr / compute_sisdr)."""
+    sdr, sisdr = {}, {}
+    for stem in STEMS:
+        e = estimates[stem]
+        r = torch.as_tensor(reference_stems[stem]).to(e.device)
+        n = min(e.shape[-1], r.shape[-1])
+        e, r = e[:, :n].contiguous(), r[:, :n].contiguous()
+        if metric_fn is None:
+            sdr[stem], sisdr[stem] = compute_sdr(e, r), compute_sisdr(e, r)
+        else:
+            sdr[stem], sisdr[stem] = metric_fn(e, r)
+    return TrackResult(track_name, model_name, sdr["drums"], sdr["bass"], sdr["other"], sdr["vocals"],
+                       sum(sdr.values()) / len(sdr), sisdr["drums"], sisdr["bass"], sisdr["other"],
+                       sisdr["vocals"], sum(sisdr.values()) / len(sisdr))
+
+
 def evaluate_model_on_track(model: OurModel, mixture: torch.Tensor, reference_stems: Dict[str, torch.Tensor],
                             track_name: str) -> Tuple[TrackResult, Dict[str, torch.Tensor]]:
     """`benchmark.py:637-739` without plotting: per stem SDR / SI-SDR on the common length."""
     est = model.separate_all(mixture)
-    sdr, sisdr = {}, {}
-    for stem in STEMS:
-        e = est[stem]
-        r = torch.as_tensor(reference_stems[stem]).to(e.device)
-        n = min(e.shape[-1], r.shape[-1])
-        e, r = e[:, :n].contiguous(), r[:, :n].contiguous()
-        sdr[stem] = compute_sdr(e, r)
-        sisdr[stem] = compute_sisdr(e, r)
-    res = TrackResult(track_name, model.name, sdr["drums"], sdr["bass"], sdr["other"], sdr["vocals"],
-                      sum(sdr.values()) / len(sdr), sisdr["drums"], sisdr["bass"], sisdr["other"], sisdr["vocals"],
-                      sum(sisdr.values()) / len(sisdr))
-    return res, est
+    return track_result(track_name, model.name, est, reference_stems), est
+
+
+def log_track(r: TrackResult, log: Callable[[str], None] = print) -> None:
+    """The per-track lines of `benchmark.py:766-773`."""
+    log(f"  {r.track_name}:\n    SDR:   avg={r.sdr_avg:.2f} dB (D={r.sdr_drums:.1f}, B={r.sdr_bass:.1f}, "
+        f"O={r.sdr_other:.1f}, V={r.sdr_vocals:.1f})\n    SISDR: avg={r.sisdr_avg:.2f} dB "
+        f"(D={r.sisdr_drums:.1f}, B={r.sisdr_bass:.1f}, O={r.sisdr_other:.1f}, V={r.sisdr_vocals:.1f})")
 
 
 def evaluate_model(model: OurModel, tracks: Iterable[Tuple[str, torch.Tensor, Dict[str, torch.Tensor]]],
@@ -222,9 +238,7 @@ def evaluate_model(model: OurModel, tracks: Iterable[Tuple[str, torch.Tensor, Di
             continue
         results.append(r)
         if log:
-            log(f"  {name}:\n    SDR:   avg={r.sdr_avg:.2f} dB (D={r.sdr_drums:.1f}, B={r.sdr_bass:.1f}, "
-                f"O={r.sdr_other:.1f}, V={r.sdr_vocals:.1f})\n    SISDR: avg={r.sisdr_avg:.2f} dB "
-                f"(D={r.sisdr_drums:.1f}, B={r.sisdr_bass:.1f}, O={r.sisdr_other:.1f}, V={r.sisdr_vocals:.1f})")
+            log_track(r, log)
     return results
 
 

@@ -17,7 +17,12 @@ separated waveforms to rank `dst`:
         track bit for bit;
       - "benchmark" (benchmark.py:155-204, weighted OLA, athd_overlap_add_weighted): the partial spans carry the
         unnormalised sum and the weight sum, added in rank order the same way, then normalised once on `dst`.
-Block, batch and span sizes follow from (N, W) or the window plan, so no size exchange is needed.
+  * `separate_dataset`: a whole MUSDB18 split (athd.musdb.MusDBTracks): every window of every track is a unit of
+    `separate_segments`; `dst` reassembles each track from its rows (weighted overlap-add), scores it against the
+    reference stems and writes evaluation_results.json (benchmark.py:742-781, :853-888).
+Block, batch and span sizes follow from (N, W) or the window plan, so no size exchange is needed.  Before its first
+exchange each runner makes one barrier per process group, so a lazily created NCCL communicator (no `device_id`
+in init_process_group) exists on every rank even when some rank's block is empty.
 
 `forward_fn` / `window_fn` / `ola_fn` default to the native path; tests substitute CPU stand-ins to exercise the
 sharding and exchange logic with the gloo backend.
@@ -47,6 +52,22 @@ def _world(group) -> Tuple[int, int]:
 
 def _global(group, r: int) -> int:
     return dist.get_global_rank(group, r) if group is not None else r
+
+
+_READY: List = []          # process-group objects whose communicator is known to exist
+
+
+def _ensure_comm(group, world: int) -> None:
+    """Initialise the group's communicator with one collective before its first point-to-point exchange.  With a
+    lazily created NCCL communicator (init_process_group without device_id) the first batch_isend_irecv must be
+    made by every rank of the group, but a rank whose block is empty makes none; one barrier per group (every rank
+    calls the runner) creates the communicator on all of them."""
+    if world <= 1:
+        return
+    pg = group if group is not None else dist.group.WORLD
+    if not any(g is pg for g in _READY):
+        dist.barrier(group)
+        _READY.append(pg)
 
 
 class PendingSends:
@@ -97,6 +118,7 @@ def separate_segments(model, segments: torch.Tensor, prompts: Sequence[str] = ST
             out = torch.empty((N, P, 2, T), dtype=torch.float32, device=dev)
         elif tuple(out.shape) != (N, P, 2, T) or not out.is_contiguous():
             raise ValueError(f"out must be a contiguous {(N, P, 2, T)} tensor")
+    _ensure_comm(group, world)
     own = pending is None
     pend = pending if pending is not None else PendingSends()
     per = -(-N // world) if N else 0
@@ -113,6 +135,11 @@ def separate_segments(model, segments: torch.Tensor, prompts: Sequence[str] = ST
             wav = segments[b0 - base:b1 - base].to(dev, non_blocking=True).contiguous()
             if rank == dst:
                 res = fwd(wav, out[b0:b1])
+                # forward_fn(wav, o) fills `o` (and may return it); a new result tensor is copied in
+                if res is not None and res.data_ptr() != out[b0:b1].data_ptr():
+                    if tuple(res.shape) != (b1 - b0, P, 2, T):
+                        raise ValueError(f"forward_fn returned {tuple(res.shape)}, expected {(b1 - b0, P, 2, T)}")
+                    out[b0:b1].copy_(res)
             else:
                 res = fwd(wav, None).contiguous()
                 pend.add(dist.batch_isend_irecv([dist.P2POp(dist.isend, res, _global(group, dst), group)]), res)
@@ -121,6 +148,98 @@ def separate_segments(model, segments: torch.Tensor, prompts: Sequence[str] = ST
     if own:
         pend.wait()
     return out if rank == dst else None
+
+
+def dataset_plan(lengths: Sequence[int], chunk_len: int, overlap_frames: int) -> List[Tuple[int, int]]:
+    """Units of a whole split: (track index, window index) in track order.  Track i has ceil(L_i / hop) windows
+    starting at k * hop, hop = chunk_len - overlap_frames (the `while start < T` loop of benchmark.py:164-198; with
+    overlap 0 these are the dataloader's deterministic segments, dataloader.py:67,104-121)."""
+    hop = chunk_len - overlap_frames
+    if hop <= 0:
+        raise ValueError("overlap must be shorter than the window")
+    return [(ti, k) for ti, L in enumerate(lengths) for k in range(-(-int(L) // hop))]
+
+
+def dataset_windows(tracks, units: Sequence[Tuple[int, int]], chunk_len: int, overlap_frames: int) -> torch.Tensor:
+    """Model inputs of `units` (consecutive entries of dataset_plan): (n, 2, chunk_len), each window zero-padded
+    past the end of its track (benchmark.py:167-172).  Only the tracks the units touch are read (mixture only)."""
+    hop = chunk_len - overlap_frames
+    out = torch.zeros((len(units), 2, chunk_len), dtype=torch.float32)
+    cur, mix = None, None
+    for j, (ti, k) in enumerate(units):
+        if ti != cur:
+            cur, mix = ti, tracks.mixture(ti)
+        s = k * hop
+        e = min(s + chunk_len, mix.shape[-1])
+        out[j, :, :e - s] = mix[:, s:e]
+    return out.pin_memory() if torch.cuda.is_available() else out
+
+
+@torch.no_grad()
+def separate_dataset(model, tracks, stems: Sequence[str] = STEMS, segment_seconds: float = 6.0,
+                     overlap: float = 1.5, sample_rate: int = 44100, dst: int = 0, group=None, max_batch: int = 64,
+                     output_dir=None, forward_fn: Optional[Callable] = None, ola_fn: Optional[Callable] = None,
+                     metric_fn: Optional[Callable] = None, model_name: str = "AudioTextHTDemucs (Ours)",
+                     keep_estimates: bool = False, log: Optional[Callable[[str], None]] = print):
+    """A whole MUSDB18 split through the sharded runner -> per-track stems and metrics on rank `dst`.
+
+    The reference evaluates a split track by track, one 6 s window and one stem at a time
+    (test_inference.py:75-88 -> dataloader.py:56-84 -> benchmark.py:742-781, OurModel._chunked_inference
+    :155-204).  Here every window of every track is one unit of `separate_segments`: the units are sharded in
+    contiguous blocks over the ranks (each rank reads only the tracks its block touches), each rank separates its
+    block into all stems (encode once, decode len(stems) times, batches of `max_batch` windows spanning tracks) and
+    the separated windows are gathered point to point into one (N, S, 2, chunk) tensor on `dst`.  `dst` then
+    reassembles every track from its rows with the weighted overlap-add of benchmark.py:177-202
+    (athd_overlap_add_weighted), computes SDR / SI-SDR per stem against the track's reference stems
+    (benchmark.py:655-688) and, with `output_dir`, writes `evaluation_results.json` (save_results,
+    benchmark.py:853-888).
+
+    overlap=1.5 is benchmark.py's protocol (OurModel's default, the one behind eval_results/*.json); overlap=0
+    separates the dataloader's non-overlapping segments (dataloader.py:67,104-121) and concatenates them.
+    Returns (results, estimates) on dst - estimates {track name: (S, 2, L)} only with keep_estimates - and None
+    elsewhere.  forward_fn / ola_fn(win, L, chunk, ov) / metric_fn(est, ref) -> (sdr, sisdr) default to the native
+    path; tests substitute CPU stand-ins to run the exchange on gloo."""
+    from .benchmark import track_result, log_track, save_results
+    if sorted(stems) != sorted(STEMS):
+        raise ValueError(f"the evaluation needs every stem of {STEMS}, got {list(stems)}")
+    world, rank = _world(group)
+    chunk_len = int(sample_rate * segment_seconds)
+    ov = int(overlap * sample_rate)
+    lengths = tracks.lengths()
+    units = dataset_plan(lengths, chunk_len, ov)
+    N = len(units)
+    lo, hi = shard_range(N, world, rank)
+    block = dataset_windows(tracks, units[lo:hi], chunk_len, ov)
+    if forward_fn is None:
+        block_dev = model.device
+    else:
+        block_dev = block.device
+    out = None
+    if rank == dst:
+        out = torch.empty((N, len(stems), 2, chunk_len), dtype=torch.float32, device=block_dev)
+    out = separate_segments(model, block, stems, dst=dst, group=group, max_batch=max_batch, forward_fn=forward_fn,
+                            n_total=N, out=out)
+    if rank != dst:
+        return None
+    if ola_fn is None:
+        from .benchmark import overlap_add_weighted
+        ola_fn = lambda win, L, c, o: overlap_add_weighted(win, L, c, o)      # noqa: E731
+    results, estimates = [], {}
+    row = 0
+    for ti, L in enumerate(lengths):
+        n = -(-int(L) // (chunk_len - ov))                                     # this track's rows of `out`
+        est = ola_fn(out[row:row + n], int(L), chunk_len, ov)                  # (S, 2, L)
+        row += n
+        name, _, refs = tracks.track(ti)
+        r = track_result(name, model_name, {s: est[i] for i, s in enumerate(stems)}, refs, metric_fn)
+        results.append(r)
+        if keep_estimates:
+            estimates[name] = est
+        if log:
+            log_track(r, log)
+    if output_dir is not None:
+        save_results({model_name: results}, output_dir)
+    return results, estimates
 
 
 @torch.no_grad()
@@ -173,6 +292,7 @@ def separate_track_sharded(model, mixture: torch.Tensor, stems: Sequence[str] = 
         span = torch.empty((S, 2, 0), dtype=torch.float32, device=dev)
         wsum = torch.empty(0, dtype=torch.float32, device=dev)
     # exchange: every non-empty span goes to dst point to point (sizes follow from the plan)
+    _ensure_comm(group, world)
     parts = {rank: (span, wsum)}
     ops = []
     for r, (a, b) in enumerate(ranges):

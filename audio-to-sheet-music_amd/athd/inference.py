@@ -154,6 +154,23 @@ def sdr_loss(estimated: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
     return -out[0]
 
 
+def sisdr_loss(estimated: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
+    """`src/loss.py:33-68`: -mean over rows of the clamped SI-SDR of the zero-meaned rows; a device scalar (fp64
+    sums on the device, athd_sisdr)."""
+    if estimated.shape[0] != target.shape[0] or estimated.numel() != target.numel():
+        raise ValueError("estimated and target must have the same rows and size")
+    rows = estimated.shape[0]
+    est = estimated.reshape(rows, -1).float().contiguous()
+    tgt = target.reshape(rows, -1).float().contiguous()
+    scratch = torch.empty(5 * rows, dtype=torch.float64, device=est.device)
+    out = torch.empty(1, dtype=torch.float32, device=est.device)
+    rc = native.lib.athd_sisdr(est.data_ptr(), tgt.data_ptr(), rows, est.shape[1], scratch.data_ptr(),
+                               out.data_ptr(), _stream(est.device))
+    if rc != 0:
+        raise native.AthdError(f"athd_sisdr failed ({rc})")
+    return -out[0]
+
+
 @torch.no_grad()
 def test_inference(model: AudioTextHTDemucs, mixture: torch.Tensor, references: Optional[torch.Tensor] = None,
                    stems: Sequence[str] = STEMS, sample_rate: int = 44100, segment_seconds: float = 6.0,

@@ -74,6 +74,30 @@ def read_wav(path) -> Tuple[np.ndarray, int]:
     return x[:len(x) // ch * ch].reshape(-1, ch), rate
 
 
+def wav_info(path) -> Tuple[int, int, int]:
+    """(frames, channels, sample rate) of a RIFF/WAVE file from its chunk headers only (no sample data read)."""
+    with open(path, "rb") as f:
+        head = f.read(12)
+        if head[:4] != b"RIFF" or head[8:12] != b"WAVE":
+            raise ValueError(f"{path}: not a RIFF/WAVE file")
+        ch = rate = align = None
+        while True:
+            h = f.read(8)
+            if len(h) < 8:
+                raise ValueError(f"{path}: missing fmt or data chunk")
+            cid, size = h[:4], struct.unpack("<I", h[4:8])[0]
+            if cid == b"fmt ":
+                body = f.read(size)
+                _, ch, rate, _, align, _ = struct.unpack("<HHIIHH", body[:16])
+                f.seek(size & 1, 1)
+            elif cid == b"data":
+                if align is None:
+                    raise ValueError(f"{path}: data chunk before fmt chunk")
+                return size // align, ch, rate
+            else:
+                f.seek(size + (size & 1), 1)
+
+
 def write_wav(path, audio: np.ndarray, sample_rate: int = 44100, subtype: str = "PCM_16") -> None:
     """(frames, channels) or (channels, frames) with channels <= 8 -> WAV.  PCM_16 (soundfile's default for WAV,
     as test_inference.py:157-175 writes) scales by 32767 and clips; FLOAT writes the values."""
@@ -184,8 +208,32 @@ class MusDBTracks:
         for i in range(len(self)):
             yield self.track(i)
 
+    def length(self, i: int) -> int:
+        """Samples of track i as load_stems returns it, read from the file headers (HQ: the shortest of the five
+        WAVs; .stem.npy: memory-mapped shape)."""
+        p = self.files[i]
+        if p.is_dir():
+            return min(wav_info(p / f"{f}.wav")[0] for f in HQ_FILES)
+        if p.suffix == ".npy":
+            return int(np.load(p, mmap_mode="r", allow_pickle=False).shape[1])
+        return self.load_stems(i).shape[1]
+
     def lengths(self) -> List[int]:
-        return [self.load_stems(i).shape[1] for i in range(len(self))]
+        return [self.length(i) for i in range(len(self))]
+
+    def mixture(self, i: int) -> torch.Tensor:
+        """(2, T) float32 mixture of track i (the first row of load_stems) without decoding the other stems when
+        the storage allows it."""
+        p = self.files[i]
+        if p.is_dir():
+            x, rate = read_wav(p / "mixture.wav")
+            if rate != self.sample_rate:
+                raise ValueError(f"{p}/mixture.wav: {rate} Hz, expected {self.sample_rate}")
+            x = x[:self.length(i)]
+            if x.shape[1] == 1:
+                x = np.repeat(x, 2, axis=1)
+            return torch.from_numpy(np.ascontiguousarray(x.T, dtype=np.float32))
+        return torch.from_numpy(self.load_stems(i)[0].T.copy())
 
     def mixture_segments(self, segment_samples: int) -> Tuple[torch.Tensor, List[Tuple[int, int]]]:
         """Every (track, segment) mixture of the split as (N, 2, segment) plus its (file_idx, segment_idx) list:

@@ -351,7 +351,7 @@ int athd_finalize(athd_ctx* c) {
                     }
                 }
                 dw.quad = c->up_gemm(q, co4, K3, qb);
-                if (c->mode == 1 && convt4_supported(dw.cin, dw.cout, 1)) {
+                if (c->mode == 1 && convt4_supported(dw.cin, dw.cout, 1, 32, 1)) {
                     // convt4.hip: per row the residue pair's two input rows only (K = 2 cin)
                     const int K2 = 2 * dw.cin;
                     std::vector<uint16_t> q2((size_t)co4 * K2);

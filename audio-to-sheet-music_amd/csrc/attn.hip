@@ -258,6 +258,7 @@ typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
 // defer-max threshold of the bf16 kernel's online softmax (log2 units): P <= 2^8 before the final 1/l
 constexpr float ATTN_RESCALE = 8.0f;
 
+#ifdef ATHD_KBENCH      // round-1 16x16x32 kernel: tools/kbench A/B builds only
 __global__ __launch_bounds__(256, 3) void attn_bf16_kernel(const AttnDesc d) {
     constexpr int LDK = 72;                        // bf16 per LDS row (64 + 8 pad)
     __shared__ __attribute__((aligned(16))) bf16_t Ks[2][64 * LDK];
@@ -450,6 +451,7 @@ __global__ __launch_bounds__(256, 3) void attn_bf16_kernel(const AttnDesc d) {
         }
     }
 }
+#endif
 #undef ATHD_FETCH
 #undef ATHD_STASH
 
@@ -746,8 +748,8 @@ __global__ __launch_bounds__(256, MINW) void attn32_kernel(const AttnDesc d) {
 
 #undef ATHD_A32_QK
 
-// kernel choice for the bf16 path: 0 = attn32_kernel<3, 2, true> (default: 3 waves per SIMD, 64-key tiles, LDS-DMA
-// staging), 1 = attn_bf16_kernel (16x16x32, ATHD_ATTN_V1=1), 2 = attn32_kernel<2, 2>, 3 = attn32_kernel<2, 4> (128-key
+// kernel choice for the bf16 path (tools/kbench builds, -DATHD_KBENCH; the product always takes 0): 0 =
+// attn32_kernel<3, 2, true> (3 waves per SIMD, 64-key tiles, LDS-DMA staging), 1 = attn_bf16_kernel (16x16x32), 2 = attn32_kernel<2, 2>, 3 = attn32_kernel<2, 4> (128-key
 // tiles), 4 = attn32_kernel<3, 2, false> (register staging), 5 / 6 = attn32_kernel<2, 4> / <4, 2> with LDS-DMA staging;
 // set by tools/kbench.hip for A/B timing.  kbench (B=64, N=2072 / 1034, same box): register staging 722 / 730 TFLOP/s,
 // LDS-DMA staging 849 / 777.  Tried and dropped: a software-pipelined form (QK^T of tile t+1 issued before the
@@ -755,14 +757,12 @@ __global__ __launch_bounds__(256, MINW) void attn32_kernel(const AttnDesc d) {
 // spills: 757) and on LDS-DMA staging (two 32-query blocks sharing every K / V fragment read, 2 waves per workgroup,
 // 2 waves per SIMD at 255 VGPRs: 765 / 648 vs 845 / 776), and 192-query workgroups (6 waves; 2 % tail waste at
 // N = 2072 instead of 5 %, DMA pieces shared by 6 waves): 729-739 / 614-630 vs 853 / 781 on one box.
-int g_attn_variant = -1;
-static int attn_variant() {
-    if (g_attn_variant < 0) {
-        const char* e = std::getenv("ATHD_ATTN_V1");
-        g_attn_variant = e && *e && *e != '0' ? 1 : 0;
-    }
-    return g_attn_variant;
-}
+#ifdef ATHD_KBENCH
+int g_attn_variant = 0;       // set by tools/kbench.hip
+static int attn_variant() { return g_attn_variant; }
+#else
+static constexpr int attn_variant() { return 0; }
+#endif
 
 static bool attn32_ok(const AttnDesc& d, int mode) {
     return attn_variant() != 1 && mode == 1 && d.q_bf16 && d.k_bf16 && d.v_bf16 && d.o_bf16 &&
@@ -786,6 +786,7 @@ int attn_launch(const AttnDesc& d, int mode, hipStream_t s) {
         ks.begin(a32 ? std::string("attn32_kernel") : v2 ? std::string("attn_bf16_kernel") : klabel("attn_kernel<%d>", mode),
                  fl, by);
     }
+#ifdef ATHD_KBENCH
     if (a32 && attn_variant() == 4) hipLaunchKernelGGL((attn32_kernel<3, 2, false>), grid, dim3(256), 0, s, d);
     else if (a32 && attn_variant() == 5) hipLaunchKernelGGL((attn32_kernel<2, 4, true>), grid, dim3(256), 0, s, d);
     else if (a32 && attn_variant() == 6) hipLaunchKernelGGL((attn32_kernel<4, 2, true>), grid, dim3(256), 0, s, d);
@@ -795,6 +796,13 @@ int attn_launch(const AttnDesc& d, int mode, hipStream_t s) {
     else if (mode == 1 && d.q_bf16 && d.k_bf16 && d.v_bf16) hipLaunchKernelGGL(attn_bf16_kernel, grid, dim3(256), 0, s, d);
     else if (mode == 1) hipLaunchKernelGGL(attn_kernel<1>, grid, dim3(256), 0, s, d);
     else hipLaunchKernelGGL(attn_kernel<0>, grid, dim3(256), 0, s, d);
+#else
+    // product: bf16 mode -> attn32_kernel (the forward's Q/K/V/O are bf16, 8-element aligned, Q prescaled);
+    // f32 parity mode -> attn_kernel<0> (fp32 MFMA)
+    if (a32) hipLaunchKernelGGL((attn32_kernel<3, 2, true>), grid, dim3(256), 0, s, d);
+    else if (mode == 0) hipLaunchKernelGGL(attn_kernel<0>, grid, dim3(256), 0, s, d);
+    else return -3;                                // bf16 mode operands attn32_kernel does not take
+#endif
     return (int)hipGetLastError();
 }
 

@@ -23,7 +23,6 @@
 #include "gemm.h"
 #include "kernels.h"
 
-#include <cstdlib>
 
 namespace athd {
 
@@ -243,8 +242,12 @@ __global__ __launch_bounds__(NW * 64) void convt4_kernel(const ConvT4Desc d) {
     flush();
 }
 
-bool convt4_supported(int cin, int cout, int64_t M) {
-    return cin == CT_CI && cout == CT_CO && M > 0 && M < (1LL << 31);
+// A 32-row unit covers at most two items (its statistics split at one item boundary: bf / bl in the loop above), which
+// holds when an item has at least 32 rows, H*W >= 32: Tspec >= 6 for the freq branch (H*W = Tspec^2 after the
+// 259 -> Tspec resize), L >= 32 for the time branch.  Shorter inputs take the tiled GEMM (forward.cpp conv_t).
+bool convt4_supported(int cin, int cout, int64_t nb, int64_t H, int64_t W) {
+    const int64_t M = nb * H * W;
+    return cin == CT_CI && cout == CT_CO && H * W >= 32 && M > 0 && M < (1LL << 31);
 }
 
 template <bool KEEP, int RF, int NW>
@@ -264,32 +267,23 @@ static void launch_ct4(const ConvT4Desc& d, int cus, hipStream_t s) {
     hipLaunchKernelGGL((convt4_kernel<KEEP, RF, NW>), dim3((unsigned)blocks), dim3(NW * 64), 0, s, d);
 }
 
-// variant (ATHD_CONVT4_V, measurement): 0 = 2 row fragments per unit, 8 waves (2 per SIMD); 1 = 1 row fragment,
-// 12 waves (3 per SIMD); 2 = 1 row fragment, 16 waves (4 per SIMD)
 int convt4_launch(const ConvT4Desc& d0, hipStream_t s) {
+    if (!convt4_supported(CT_CI, CT_CO, d0.nb, d0.H, d0.W)) return -1;
     ConvT4Desc d = d0;
     d.fd_w = make_fastdiv((uint32_t)d.W);
     d.fd_h = make_fastdiv((uint32_t)d.H);
     d.fd_hw = make_fastdiv((uint32_t)d.H * (uint32_t)d.W);
     d.M = (uint32_t)((int64_t)d.nb * d.H * d.W);
-    static int cus = 0, var = -1;
+    static int cus = 0;
     if (cus == 0) {
         int dev = 0;
         (void)hipGetDevice(&dev);
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
         if (cus <= 0) cus = 256;
-        const char* e = std::getenv("ATHD_CONVT4_V");
-        var = e && *e ? std::atoi(e) : 0;
     }
-    if (d.keep) {
-        if (var == 1) launch_ct4<true, 1, 12>(d, cus, s);
-        else if (var == 2) launch_ct4<true, 1, 16>(d, cus, s);
-        else launch_ct4<true, 2, 8>(d, cus, s);
-    } else {
-        if (var == 1) launch_ct4<false, 1, 12>(d, cus, s);
-        else if (var == 2) launch_ct4<false, 1, 16>(d, cus, s);
-        else launch_ct4<false, 2, 8>(d, cus, s);
-    }
+    // 2 row fragments per unit, 8 waves (2 per SIMD).  (1 fragment at 12 / 16 waves per workgroup measured slower.)
+    if (d.keep) launch_ct4<true, 2, 8>(d, cus, s);
+    else launch_ct4<false, 2, 8>(d, cus, s);
     return (int)hipGetLastError();
 }
 

@@ -11,8 +11,8 @@
 // registers (a row changes every ~Hd/32 steps) and the per-step resize indices read from an LDS table.  Both
 // passes are VALU-bound: the arithmetic runs on packed fp32 pairs (v_pk_fma_f32), the bias and the skip row
 // base are folded into one per-row-change base so a step costs two packed FMAs per tap:
-//   fdec_lr_stats_kernel: GroupNorm(1) {sum, sumsq} over all 4*Hd ConvT rows;
-//   fdec_lr_merge_kernel: rows 4d+1, 4d+2 (the only rows the exact /4 bilinear resize reads) -> GN -> GELU ->
+//   fdec_lr_stats{2,3}_kernel: GroupNorm(1) {sum, sumsq} over all 4*Hd ConvT rows;
+//   fdec_lr_merge{2,3}_kernel: rows 4d+1, 4d+2 (the only rows the exact /4 bilinear resize reads) -> GN -> GELU ->
 //                         lerp -> + 0.1 * resize_H(skip2) -> D1 [item][d][w][Co].
 #include <algorithm>
 #include <cstdlib>
@@ -66,40 +66,6 @@ template <typename ZT, int NT>
 ATHD_DEV void load_rows(const ZT* base, int64_t rowpitch, int Co, int i0, int i1, float scale, f2 (&r0)[NT],
                         f2 (&dr)[NT]);
 
-// Per-step resize indices of lin_index(v, in, Hd), tabulated once per block in LDS for v < LR_TAB.
-constexpr int LR_TAB = 1024;
-struct LrTab {
-    int ij;     // i0 | i1 << 16
-    float l1;
-};
-ATHD_DEV void lr_fill(LrTab* t, int n, int in, int out) {
-    for (int v = threadIdx.x; v < n && v < LR_TAB; v += blockDim.x) {
-        const LinIdx li = lin_index(v, in, out);
-        t[v].ij = li.i0 | (li.i1 << 16);
-        t[v].l1 = li.l1;
-    }
-}
-struct Lerp {
-    int i0, i1;
-    float l1;
-};
-ATHD_DEV Lerp lr_get(const LrTab* t, int v, int in, int out) {
-    Lerp r;
-    if (v < LR_TAB) {
-        const LrTab e = t[v];
-        const int ij = __builtin_amdgcn_readfirstlane(e.ij);
-        r.i0 = ij & 0xFFFF;
-        r.i1 = ij >> 16;
-        r.l1 = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(e.l1)));
-    } else {
-        const LinIdx li = lin_index(v, in, out);
-        r.i0 = li.i0;
-        r.i1 = li.i1;
-        r.l1 = li.l1;
-    }
-    return r;
-}
-
 // tap index of slot t: all 8 taps (stats pass) or {0, 3, 4, 7} (merge pass: rows 4d+1, 4d+2)
 template <int NT>
 ATHD_DEV constexpr int tap_of(int t) { return NT == 8 ? t : (t == 0 ? 0 : t == 1 ? 3 : t == 2 ? 4 : 7); }
@@ -118,30 +84,6 @@ ATHD_DEV void load_rows(const ZT* base, int64_t rowpitch, int Co, int i0, int i1
         dr[t] = (b[t] - a[t]) * splat(scale);
     }
 }
-
-// The two rows (i0, i1) one lerp reads: r0 = scale * row[i0], dr = scale * (row[i1] - row[i0]) per tap slot, so the
-// lerp is fma(l1, dr, r0) (same value as l0 * a + l1 * b up to rounding; l0 = 1 - l1).
-template <typename ZT, int NT>
-struct LerpRows {
-    f2 r0[NT], dr[NT];
-    int c0 = -1, c1 = -1;
-    ATHD_DEV bool update(const ZT* base, int64_t rowpitch, int Co, const Lerp& li, float scale) {
-        if (li.i0 == c0 && li.i1 == c1) return false;
-        c0 = li.i0;
-        c1 = li.i1;
-        f2 a[NT], b[NT];
-#pragma unroll
-        for (int t = 0; t < NT; ++t) a[t] = ld2(base + (int64_t)li.i0 * rowpitch + tap_of<NT>(t) * Co);
-#pragma unroll
-        for (int t = 0; t < NT; ++t) b[t] = ld2(base + (int64_t)li.i1 * rowpitch + tap_of<NT>(t) * Co);
-#pragma unroll
-        for (int t = 0; t < NT; ++t) {
-            r0[t] = a[t] * splat(scale);
-            dr[t] = (b[t] - a[t]) * splat(scale);
-        }
-        return true;
-    }
-};
 
 struct LrThread {
     int item, seg, w, c;
@@ -162,166 +104,12 @@ ATHD_DEV LrThread lr_thread(const LowRankDesc& d) {
 
 }  // namespace
 
-template <typename ZT>
-__global__ __launch_bounds__(256) void fdec_lr_stats_kernel(const LowRankDesc d) {
-    __shared__ LrTab tz[LR_TAB], tk[LR_TAB];
-    lr_fill(tz, d.Hd, d.Hs, d.Hd);
-    lr_fill(tk, d.Hd, d.Hk, d.Hd);
-    __syncthreads();
-    const LrThread th = lr_thread(d);
-    const int N8 = 8 * d.Co;
-    const int64_t rp = (int64_t)d.W * N8;
-    const ZT* zb = (const ZT*)d.Z + (int64_t)th.item * d.Hs * rp + (int64_t)th.w * N8 + th.c;
-    const ZT* sb = (const ZT*)d.Zs + (int64_t)th.seg * d.Hk * rp + (int64_t)th.w * N8 + th.c;
-    const f2 bias = ld2(d.bias + th.c);
-    LerpRows<ZT, 8> zr, sr;
-    f2 base[8];                // r0(Z) + r0(Zs) (+ bias on taps 2..5: every output row has exactly one of those)
-    f2 prev[4] = {};           // T_{v-1}[4..7]
-    double s1 = 0.0, s2 = 0.0;
-    if (th.active) {
-        for (int v0 = 0; v0 <= d.Hd; v0 += 16) {
-            f2 a1 = {}, a2 = {};
-            const int v1 = min(v0 + 16, d.Hd + 1);
-            for (int v = v0; v < v1; ++v) {
-                f2 T[8];
-                if (v < d.Hd) {
-                    const Lerp a = lr_get(tz, v, d.Hs, d.Hd);
-                    const Lerp k = lr_get(tk, v, d.Hk, d.Hd);
-                    const bool cz = zr.update(zb, rp, d.Co, a, 1.0f);
-                    const bool cs = sr.update(sb, rp, d.Co, k, 0.1f);
-                    if (cz || cs) {
-#pragma unroll
-                        for (int t = 0; t < 8; ++t) base[t] = zr.r0[t] + sr.r0[t] + ((t >= 2 && t <= 5) ? bias : f2{});
-                    }
-#pragma unroll
-                    for (int t = 0; t < 8; ++t) T[t] = pfma(splat(a.l1), zr.dr[t], pfma(splat(k.l1), sr.dr[t], base[t]));
-                } else {
-#pragma unroll
-                    for (int t = 0; t < 8; ++t) T[t] = f2{};
-                }
-                if (v >= 1) {          // rows 4(v-1)+2, 4(v-1)+3
-                    const f2 y2 = prev[0] + T[0];
-                    const f2 y3 = prev[1] + T[1];
-                    a1 += y2 + y3;
-                    a2 = pfma(y2, y2, pfma(y3, y3, a2));
-                }
-                if (v < d.Hd) {        // rows 4v, 4v+1
-                    const f2 y0 = T[2] + prev[2];
-                    const f2 y1 = T[3] + prev[3];
-                    a1 += y0 + y1;
-                    a2 = pfma(y0, y0, pfma(y1, y1, a2));
-                }
-#pragma unroll
-                for (int t = 0; t < 4; ++t) prev[t] = T[4 + t];
-            }
-            s1 += (double)a1.x + (double)a1.y;
-            s2 += (double)a2.x + (double)a2.y;
-        }
-    }
-    s1 = wave_sum_d(s1);
-    s2 = wave_sum_d(s2);
-    __shared__ double sh[2][4];
-    const int wv = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0) { sh[0][wv] = s1; sh[1][wv] = s2; }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        atomicAdd(&d.stats[2 * th.item], sh[0][0] + sh[0][1] + sh[0][2] + sh[0][3]);
-        atomicAdd(&d.stats[2 * th.item + 1], sh[1][0] + sh[1][1] + sh[1][2] + sh[1][3]);
-    }
-}
-
-template <typename ZT, bool FAST>
-__global__ __launch_bounds__(256) void fdec_lr_merge_kernel(const LowRankDesc d) {
-    __shared__ LrTab tz[LR_TAB], tk[LR_TAB], tj[LR_TAB];
-    lr_fill(tz, d.Hd, d.Hs, d.Hd);
-    lr_fill(tk, d.Hd, d.Hk, d.Hd);
-    lr_fill(tj, d.Hd, d.H_skip, d.Hd);
-    __syncthreads();
-    const LrThread th = lr_thread(d);
-    if (!th.active) return;
-    const int N8 = 8 * d.Co;
-    const int64_t rp = (int64_t)d.W * N8;
-    const ZT* zb = (const ZT*)d.Z + (int64_t)th.item * d.Hs * rp + (int64_t)th.w * N8 + th.c;
-    const ZT* sb = (const ZT*)d.Zs + (int64_t)th.seg * d.Hk * rp + (int64_t)th.w * N8 + th.c;
-    float mean, rstd;
-    gn_params(d.stats, th.item, 4LL * d.Hd * d.W * d.Co, mean, rstd);
-    const f2 bias = ld2(d.bias + th.c);
-    const f2 gsc = ld2(d.gn_w + th.c) * splat(rstd);     // (y - mean) * rstd * w + b  as  (y - mean) * gsc + b
-    const f2 gb = ld2(d.gn_b + th.c);
-    // skip2 [seg][H_skip][W][C_skip], channels [0, Co): 0.1 * lerp, rows cached like the Z rows
-    const int64_t kp = (int64_t)d.W * d.C_skip;
-    const int64_t kb = (int64_t)th.seg * d.H_skip * kp + (int64_t)th.w * d.C_skip + th.c;
-    int k0c = -1, k1c = -1;
-    f2 ka = {}, kd = {};
-    const int64_t ob = (int64_t)th.item * d.Hd * d.W * d.Co + (int64_t)th.w * d.Co + th.c;
-    const int64_t op = (int64_t)d.W * d.Co;
-
-    LerpRows<ZT, 4> zr, sr;       // slots: taps 0, 3, 4, 7
-    f2 base[4];
-    f2 cur3 = {}, cur4 = {}, cur7 = {}, prev7 = {};
-    for (int v = 0; v <= d.Hd; ++v) {
-        f2 T[4];
-        if (v < d.Hd) {
-            const Lerp a = lr_get(tz, v, d.Hs, d.Hd);
-            const Lerp k = lr_get(tk, v, d.Hk, d.Hd);
-            const bool cz = zr.update(zb, rp, d.Co, a, 1.0f);
-            const bool cs = sr.update(sb, rp, d.Co, k, 0.1f);
-            if (cz || cs) {
-#pragma unroll
-                for (int t = 0; t < 4; ++t) base[t] = zr.r0[t] + sr.r0[t] + ((t == 1 || t == 2) ? bias : f2{});
-            }
-#pragma unroll
-            for (int t = 0; t < 4; ++t) T[t] = pfma(splat(a.l1), zr.dr[t], pfma(splat(k.l1), sr.dr[t], base[t]));
-        } else {
-#pragma unroll
-            for (int t = 0; t < 4; ++t) T[t] = f2{};
-        }
-        if (v >= 1) {
-            // output row dd: the exact /4 bilinear resize of the 4*Hd ConvT rows reads rows 4dd+1 and 4dd+2 with
-            // weights 0.5 / 0.5 (src = 4dd + 1.5, exact in fp32)
-            const int dd = v - 1;
-            const Lerp lj = lr_get(tj, dd, d.H_skip, d.Hd);
-            if (lj.i0 != k0c || lj.i1 != k1c) {
-                k0c = lj.i0;
-                k1c = lj.i1;
-                f2 a, b;
-                if (d.skip_bf16) {
-                    a = ld2((const bf16_t*)d.skip + kb + (int64_t)lj.i0 * kp);
-                    b = ld2((const bf16_t*)d.skip + kb + (int64_t)lj.i1 * kp);
-                } else {
-                    a = ld2((const float*)d.skip + kb + (int64_t)lj.i0 * kp);
-                    b = ld2((const float*)d.skip + kb + (int64_t)lj.i1 * kp);
-                }
-                ka = a * splat(0.1f);
-                kd = (b - a) * splat(0.1f);
-            }
-            const f2 y1 = cur3 + prev7;
-            const f2 y2 = cur4 + T[0];
-            const f2 g1 = gelu2<FAST>(pfma(y1 - splat(mean), gsc, gb));
-            const f2 g2 = gelu2<FAST>(pfma(y2 - splat(mean), gsc, gb));
-            const f2 o = pfma(g1 + g2, splat(0.5f), pfma(splat(lj.l1), kd, ka));
-            const int64_t oi = ob + (int64_t)dd * op;
-            if (d.out_bf16) {
-                const bf2_t h = __builtin_convertvector(o, bf2_t);
-                *reinterpret_cast<bf2_t*>((bf16_t*)d.out + oi) = h;
-            } else {
-                *reinterpret_cast<f2*>((float*)d.out + oi) = o;
-            }
-        }
-        prev7 = cur7;
-        cur3 = T[1];
-        cur4 = T[2];
-        cur7 = T[3];
-    }
-}
-
-
 // ---------------------------------------------------------------------------------------------------------
-// v2 passes: the same arithmetic as fdec_lr_stats_kernel / fdec_lr_merge_kernel, with the per-step resize lerps and
-// row-change flags read from a step table in global memory (fdec_lr_steps_kernel, once per forward): the step index
-// is wave-uniform, so the entry arrives through scalar loads and the lerp weights feed the packed FMAs as SGPR
-// operands.  This removes the per-step LDS lookups, readfirstlanes and row-index compares (about half the VALU
-// instructions of a step in v1, where both passes are VALU-bound), and the GELU pair runs packed.
+// v2 passes (f32 mode, and bf16 without strict upsampling, i.e. Tspec <= 32): the per-step resize lerps and
+// row-change flags are read from a step table in global memory (fdec_lr_steps_kernel, once per forward): the step
+// index is wave-uniform, so the entry arrives through scalar loads and the lerp weights feed the packed FMAs as SGPR
+// operands (round 1's per-block LDS index tables cost about half the VALU instructions of a step; that version is
+// gone), and the GELU pair runs packed.
 // step entry v through the constant address space: the index is wave-uniform, so this is a scalar load (through a
 // generic pointer the compiler may use a vector load, which the step then waits on)
 typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
@@ -771,25 +559,6 @@ __global__ __launch_bounds__(256) void fdec_lr_merge2_kernel(const LowRankDesc d
     }
 }
 
-static bool lr_v1() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = std::getenv("ATHD_LR_V1");
-        v = e && *e && *e != '0' ? 1 : 0;
-    }
-    return v == 1;
-}
-
-// ATHD_LR_V3=0: the v2 statistics pass in the bf16 mode too (A/B measurement)
-static bool lr_v3() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = std::getenv("ATHD_LR_V3");
-        v = e && *e == '0' ? 0 : 1;
-    }
-    return v == 1;
-}
-
 int fdec_lr_steps_launch(LrStep* steps, int Hd, int Hs, int Hk, int H_skip, hipStream_t s) {
     if (!steps || Hd <= 0 || Hs <= 0 || Hs > 256 || Hk <= 0 || Hk > 256 || H_skip <= 0 || H_skip > 65536) return -1;
     KScope ks(s);
@@ -799,7 +568,7 @@ int fdec_lr_steps_launch(LrStep* steps, int Hd, int Hs, int Hk, int H_skip, hipS
 }
 
 static bool lr_ok(const LowRankDesc& d) {
-    return d.Z && d.Zs && d.bias && d.stats && d.Co % 2 == 0 && d.Hd > 0 && d.Hd < 65536 && d.W > 0 && d.P > 0 &&
+    return d.Z && d.Zs && d.bias && d.stats && d.steps && d.Co % 2 == 0 && d.Hd > 0 && d.Hd < 65536 && d.W > 0 && d.P > 0 &&
            d.NI % d.P == 0 && d.Hs > 0 && d.Hk > 0;
 }
 
@@ -811,16 +580,21 @@ int fdec_lr_stats_launch(const LowRankDesc& d, hipStream_t s) {
         // unique bytes: Z of every item + Zs of every segment, read once
         const double ze = d.z_bf16 ? 2.0 : 4.0;
         const double by = ze * 8.0 * d.Co * d.W * ((double)d.NI * d.Hs + (double)(d.NI / d.P) * d.Hk);
-        ks.begin(d.z_bf16 ? "fdec_lr_stats_kernel<unsignedshort>" : "fdec_lr_stats_kernel<float>", 0.0, by);
+        ks.begin(d.z_bf16 && d.Hd > d.Hs && d.Hd > d.Hk ? "fdec_lr_stats3_kernel"
+                 : d.z_bf16 ? "fdec_lr_stats2_kernel<unsignedshort>" : "fdec_lr_stats2_kernel<float>", 0.0, by);
     }
-    if (d.steps && !lr_v1() && d.z_bf16 && d.Hd > d.Hs && d.Hd > d.Hk && lr_v3()) {
+    if (d.z_bf16 && d.Hd > d.Hs && d.Hd > d.Hk)
         hipLaunchKernelGGL(fdec_lr_stats3_kernel, grid, dim3(256), 0, s, d);
-    } else if (d.steps && !lr_v1()) {
-        if (d.z_bf16) hipLaunchKernelGGL(fdec_lr_stats2_kernel<bf16_t>, grid, dim3(256), 0, s, d);
-        else hipLaunchKernelGGL(fdec_lr_stats2_kernel<float>, grid, dim3(256), 0, s, d);
-    } else if (d.z_bf16) hipLaunchKernelGGL(fdec_lr_stats_kernel<bf16_t>, grid, dim3(256), 0, s, d);
-    else hipLaunchKernelGGL(fdec_lr_stats_kernel<float>, grid, dim3(256), 0, s, d);
+    else if (d.z_bf16)
+        hipLaunchKernelGGL(fdec_lr_stats2_kernel<bf16_t>, grid, dim3(256), 0, s, d);
+    else
+        hipLaunchKernelGGL(fdec_lr_stats2_kernel<float>, grid, dim3(256), 0, s, d);
     return (int)hipGetLastError();
+}
+
+// v3 merge: bf16 mode with strict upsampling of all three lerps (every row change advances by one row)
+static bool merge3(const LowRankDesc& d) {
+    return d.z_bf16 && d.skip_bf16 && d.out_bf16 && d.fast_gelu && d.Hd > d.Hs && d.Hd > d.Hk && d.Hd > d.H_skip;
 }
 
 int fdec_lr_merge_launch(const LowRankDesc& d, hipStream_t s) {
@@ -836,26 +610,18 @@ int fdec_lr_merge_launch(const LowRankDesc& d, hipStream_t s) {
         const double by = ze * 4.0 * d.Co * d.W * ((double)d.NI * d.Hs + (double)(d.NI / d.P) * d.Hk) +
                           (double)(d.NI / d.P) * skip_rows * d.W * d.Co * (d.skip_bf16 ? 2 : 4) +
                           (double)d.NI * d.Hd * d.W * d.Co * (d.out_bf16 ? 2 : 4);
-        ks.begin(klabel("fdec_lr_merge_kernel<%s,%s>", d.z_bf16 ? "unsignedshort" : "float",
-                        d.fast_gelu ? "true" : "false"), 0.0, by);
+        ks.begin(merge3(d) ? std::string("fdec_lr_merge3_kernel")
+                            : klabel("fdec_lr_merge2_kernel<%s,%s>", d.z_bf16 ? "unsignedshort" : "float",
+                                     d.fast_gelu ? "true" : "false"), 0.0, by);
     }
-    if (d.steps && !lr_v1() && d.z_bf16 && d.skip_bf16 && d.out_bf16 && d.fast_gelu && d.Hd > d.Hs && d.Hd > d.Hk &&
-        d.Hd > d.H_skip && lr_v3()) {
+    if (merge3(d)) {
         hipLaunchKernelGGL(fdec_lr_merge3_kernel, grid, dim3(256), 0, s, d);
-    } else if (d.steps && !lr_v1()) {
-        if (d.z_bf16) {
-            if (d.fast_gelu) hipLaunchKernelGGL((fdec_lr_merge2_kernel<bf16_t, true>), grid, dim3(256), 0, s, d);
-            else hipLaunchKernelGGL((fdec_lr_merge2_kernel<bf16_t, false>), grid, dim3(256), 0, s, d);
-        } else {
-            if (d.fast_gelu) hipLaunchKernelGGL((fdec_lr_merge2_kernel<float, true>), grid, dim3(256), 0, s, d);
-            else hipLaunchKernelGGL((fdec_lr_merge2_kernel<float, false>), grid, dim3(256), 0, s, d);
-        }
     } else if (d.z_bf16) {
-        if (d.fast_gelu) hipLaunchKernelGGL((fdec_lr_merge_kernel<bf16_t, true>), grid, dim3(256), 0, s, d);
-        else hipLaunchKernelGGL((fdec_lr_merge_kernel<bf16_t, false>), grid, dim3(256), 0, s, d);
+        if (d.fast_gelu) hipLaunchKernelGGL((fdec_lr_merge2_kernel<bf16_t, true>), grid, dim3(256), 0, s, d);
+        else hipLaunchKernelGGL((fdec_lr_merge2_kernel<bf16_t, false>), grid, dim3(256), 0, s, d);
     } else {
-        if (d.fast_gelu) hipLaunchKernelGGL((fdec_lr_merge_kernel<float, true>), grid, dim3(256), 0, s, d);
-        else hipLaunchKernelGGL((fdec_lr_merge_kernel<float, false>), grid, dim3(256), 0, s, d);
+        if (d.fast_gelu) hipLaunchKernelGGL((fdec_lr_merge2_kernel<float, true>), grid, dim3(256), 0, s, d);
+        else hipLaunchKernelGGL((fdec_lr_merge2_kernel<float, false>), grid, dim3(256), 0, s, d);
     }
     return (int)hipGetLastError();
 }

@@ -498,7 +498,7 @@ __global__ __launch_bounds__(FR_NT, 4) void fenc_row0_kernel(const FencRowDesc d
     for (int i = 0; i < 3; ++i) {
         const int c = tid + FR_NT * i, m = c >> 2, q = c & 3;
         const int fi = 4 * f - 2 + 2 * q;
-        if (m < T && fi >= 0 && fi + 1 < d.Fin && !(d.probe & 1)) {
+        if (m < T && fi >= 0 && fi + 1 < d.Fin) {
             const float* p = (const float*)d.in + (((int64_t)b * T + m) * d.Fin + fi) * 4;
             u[i][0] = ld4f(p);
             u[i][1] = ld4f(p + 4);
@@ -555,14 +555,14 @@ __global__ __launch_bounds__(FR_NT, 4) void fenc_row0_kernel(const FencRowDesc d
 
     // ---- DConv: x += LayerScale(GLU(GN(1x1(GELU(GN(conv3(x)))))))
 #pragma unroll 1
-    for (int dd = 0; dd < ((d.probe & 2) ? 0 : 2); ++dd) {
+    for (int dd = 0; dd < 2; ++dd) {
         const int dil = 1 << dd;
         const int l15 = opaque_lane() & 15;
         f32x4_t ha[3];
 #pragma unroll
         for (int i = 0; i < 3; ++i) ha[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int ks = 0; ks < ((d.probe & 8) ? 0 : 5); ++ks) {
+        for (int ks = 0; ks < 5; ++ks) {
             const int k0 = ks * 32 + 8 * l4;
             const int tap = k0 / C, c0 = k0 - tap * C;
             const bool kok = k0 < 3 * C;
@@ -598,7 +598,7 @@ __global__ __launch_bounds__(FR_NT, 4) void fenc_row0_kernel(const FencRowDesc d
             g1w[q] = d.g1w[dd][min(4 * l4 + q, H - 1)];
             g1b[q] = d.g1b[dd][min(4 * l4 + q, H - 1)];
         }
-        if (!(d.probe & 32)) block_sum2_dpp(s1, s2, red[2 * dd]);
+        block_sum2_dpp(s1, s2, red[2 * dd]);
         float hm, hr;
         gn_from_sums(s1, s2, (float)(H * T), hm, hr);
         // GELU(GN(h)) -> hs (bf16); then the 1x1 output's GroupNorm statistics from the moments of the 1x1 conv
@@ -652,8 +652,7 @@ __global__ __launch_bounds__(FR_NT, 4) void fenc_row0_kernel(const FencRowDesc d
         const float4 gwa = ld4f(d.g2w[dd] + pa), gba = ld4f(d.g2b[dd] + pa);
         const float4 gwg = ld4f(d.g2w[dd] + pa + 16), gbg = ld4f(d.g2b[dd] + pa + 16);
         const float4 sc4 = ld4f(d.scale[dd] + cb);
-        if (!(d.probe & 32)) block_sum2_dpp(s1, s2, red[2 * dd + 1]);
-        else __syncthreads();
+        block_sum2_dpp(s1, s2, red[2 * dd + 1]);
         float ym, yr;
         gn_from_sums(s1, s2, (float)(2 * C * T), ym, yr);
         // (y + b - mean) * rstd * w + beta  as  y * wa + ca  (wa = rstd w, ca = (b - mean) wa + beta)
@@ -667,7 +666,7 @@ __global__ __launch_bounds__(FR_NT, 4) void fenc_row0_kernel(const FencRowDesc d
         // pass 2: GroupNorm -> GLU -> LayerScale -> residual
         const int l15c = opaque_lane() & 15;
 #pragma unroll
-        for (int i = 0; i < ((d.probe & 16) ? 0 : MTW); ++i) {
+        for (int i = 0; i < MTW; ++i) {
             const int mt = mg + 2 * i;
             const int m = mt * 16 + l15c;
             FR_SCHED();
@@ -731,9 +730,8 @@ __global__ __launch_bounds__(FR_NT, 4) void fenc_row0_kernel(const FencRowDesc d
         }
         __syncthreads();
         bf16_t* dst = d.out + ((int64_t)b * d.Fout + f) * (int64_t)T * C;
-        if (!(d.probe & 4))
-            for (int i = tid; i < T * C / 8; i += FR_NT)
-                reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(ob)[i];
+        for (int i = tid; i < T * C / 8; i += FR_NT)
+            reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(ob)[i];
     }
 }
 
@@ -742,7 +740,8 @@ bool fenc_row_supported(int cin, int c, int T) {
 }
 
 int fenc_row_launch(const FencRowDesc& d, int cin, int c, hipStream_t s) {
-    if (!fenc_row_supported(cin, c, d.T) || d.Fout * 4 != d.Fin) return -1;
+    // (the 1x1 convs' GroupNorm statistics come from their moments, d.gram)
+    if (!fenc_row_supported(cin, c, d.T) || d.Fout * 4 != d.Fin || !d.gram[0] || !d.gram[1]) return -1;
     const int R = d.B * d.Fout;
     const dim3 grid((unsigned)(8 * ((R + 7) / 8)));
     KScope ks(s);
@@ -754,21 +753,7 @@ int fenc_row_launch(const FencRowDesc& d, int cin, int c, hipStream_t s) {
         const double in_b = cin == 4 ? (double)d.B * d.Fin * T * 4 * 4 : (double)d.B * d.Fin * T * cin * 2;
         ks.begin(cin == 4 ? "fenc_row0_kernel" : klabel("fenc_row_kernel<%d,%d>", cin, c), 2.0 * macs, in_b + rows * T * c * 2);
     }
-    static int v1 = -1;
-    if (v1 < 0) {
-        const char* e = std::getenv("ATHD_FENC_V1");
-        v1 = e && *e && *e != '0' ? 1 : 0;
-    }
-    static int probe = -1;
-    if (probe < 0) {
-        const char* e = std::getenv("ATHD_FR_PROBE");
-        probe = e && *e ? std::atoi(e) : 0;
-    }
-    FencRowDesc dp = d;
-    dp.probe = probe;
-    if (cin == 4 && !v1 && d.T <= F0_TP && d.gram[0] && d.gram[1]) hipLaunchKernelGGL(fenc_row0_kernel, grid, dim3(FR_NT), 0, s, dp);
-    else if (cin == 4) hipLaunchKernelGGL((fenc_row_kernel<4, 48, 6, false>), grid, dim3(6 * 64), 0, s, d);
-    else if (v1 || !d.gram[0] || !d.gram[1]) hipLaunchKernelGGL((fenc_row_kernel<48, 96, 6, false>), grid, dim3(6 * 64), 0, s, d);
+    if (cin == 4) hipLaunchKernelGGL(fenc_row0_kernel, grid, dim3(FR_NT), 0, s, d);
     else hipLaunchKernelGGL((fenc_row_kernel<48, 96, 12, true>), grid, dim3(12 * 64), 0, s, d);
     return (int)hipGetLastError();
 }

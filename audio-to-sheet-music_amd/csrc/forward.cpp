@@ -539,20 +539,10 @@ void encode(Run& r, const Dims& d, const Bufs& b, const float* wav) {
 // u-1, u; rows 4u+{2,3} read u, u+1.  Each GEMM has N = 2*cout (columns >= cout belong to the odd residue).
 // keep < 0: store all rows (4*H_in rows).  keep > 0: store only rows 4u+1, 4u+2 as slots 2u, 2u+1 (the only
 // rows the following exact /4 bilinear resize reads); statistics (if st) still cover all four residues.
-// ATHD_CONVT4=0: the four-residue ConvT on the tiled GEMM (gemm3) instead of convt4.hip (A/B measurement)
-static bool conv_t4_off() {
-    static int off = -1;
-    if (off < 0) {
-        const char* e = std::getenv("ATHD_CONVT4");
-        off = e && *e == '0' ? 1 : 0;
-    }
-    return off == 1;
-}
-
 void conv_t(Run& r, const DecW& w, const void* A, int a_bf16, int nb, int H_in, int W, void* out, int out_bf16,
             double* st, int keep, const char* stage) {
     KStage kst(stage);
-    if (w.ct4w && a_bf16 && out_bf16 && convt4_supported(w.cin, w.cout, (int64_t)nb * H_in * W) && !conv_t4_off()) {
+    if (w.ct4w && a_bf16 && out_bf16 && convt4_supported(w.cin, w.cout, nb, H_in, W)) {
         // dedicated pass (convt4.hip): weights resident in LDS, barrier-free waves over 32-row units
         ConvT4Desc q;
         q.x = (const uint16_t*)A; q.w = w.ct4w; q.bias = w.ct4b; q.out = (uint16_t*)out; q.stats = st;
@@ -593,16 +583,6 @@ void conv_t(Run& r, const DecW& w, const void* A, int a_bf16, int nb, int H_in, 
     }
 }
 
-// ATHD_TEXT_LN=0: the text cross-attention's norm_out as a separate LayerNorm pass in the bf16 mode too (A/B)
-static bool text_ln_off() {
-    static int off = -1;
-    if (off < 0) {
-        const char* e = std::getenv("ATHD_TEXT_LN");
-        off = e && *e == '0' ? 1 : 0;
-    }
-    return off == 1;
-}
-
 void decode_chunk(Run& r, const Dims& d, const Bufs& b, int64_t s0, int64_t Bc, const float* text, bool text_per_item,
                   float* out) {
     athd_ctx* c = r.c;
@@ -627,7 +607,7 @@ void decode_chunk(Run& r, const Dims& d, const Bufs& b, int64_t s0, int64_t Bc, 
         GemmDesc g2 = r.lin(c->mlp2, Hm, ab, NI, ntok, 384);
         g2.bias = nullptr; g2.pbias = b.tc2;
         g2.C = Yb; g2.res = enc; g2.res_div = P; g2.res_bs = ntok * 384;
-        if (r.actbf && !text_ln_off()) {
+        if (r.actbf) {
             // bf16 mode: norm_out in the GEMM's epilogue (gemm3 row-LayerNorm variant: 128 x 384 tiles hold whole
             // rows), x_cond written directly; Yb is not used
             g2.C = cond; g2.c_bf16 = 1; g2.ln_w = c->ta_nw; g2.ln_b = c->ta_nb;

@@ -297,13 +297,7 @@ int gemm_launch(const GemmDesc& d0, int mode, hipStream_t s) {
     // (K >= 384: 192x192 tiles with a 3-stage ring, two K-tiles in flight across each barrier; measured per call
     // site 2-20 % faster there.  Shorter K, e.g. the K=288 four-residue ConvT, keeps 256x192 x 2 stages.)
     if (mode == 1 && gemm3_supported(d) && d.N >= 192) {
-        int v = d.K >= 384 ? 7 : 3;
-        static int quad_v = -2;
-        if (quad_v == -2) {
-            const char* e = std::getenv("ATHD_G3_QUAD");
-            quad_v = e && *e ? std::atoi(e) : -1;
-        }
-        if (d.k_blk > 0 && quad_v >= 0) v = quad_v;       // (measurement override for the four-residue ConvT)
+        const int v = d.K >= 384 ? 7 : 3;
         return gemm3_launch(d, s, 100 + v);               // persistent grid
     }
     if (mode == 1 && gemm2_supported(d)) return gemm2_launch(d, s);

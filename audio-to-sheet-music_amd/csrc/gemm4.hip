@@ -315,16 +315,6 @@ bool gemm4_supported(const GemmDesc& d) {
            d.col_split % 4 == 0 && (d.act != ACT_GLU || d.N % 32 == 0);
 }
 
-// ATHD_G4_PERSIST=0: one tile per block for every epilogue (A/B measurement)
-int g_g4_persist = -1;
-static bool g4_persist() {
-    if (g_g4_persist < 0) {
-        const char* e = std::getenv("ATHD_G4_PERSIST");
-        g_g4_persist = e && *e == '0' ? 0 : 1;
-    }
-    return g_g4_persist == 1;
-}
-
 template <unsigned F>
 static void launch4f(const GemmDesc& d, hipStream_t s) {
     const int64_t M = (int64_t)d.nb * d.H_out * d.W;
@@ -339,7 +329,7 @@ static void launch4f(const GemmDesc& d, hipStream_t s) {
             (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, gemm4_kernel<F>, 512, 0);
             resident = per_cu > 0 && cus > 0 ? per_cu * cus / 8 * 8 : -1;
         }
-        if (g4_persist() && resident >= 8 && resident < tiles) grid = resident;
+        if (resident >= 8 && resident < tiles) grid = resident;
     }
     KScope ks(s);
     if (ks.on()) {

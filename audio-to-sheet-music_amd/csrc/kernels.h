@@ -127,9 +127,6 @@ struct FencRowDesc {
     const uint16_t* wr = nullptr; int wr_ld = 0; const float* br = nullptr;      // rewrite [2C][C] GLU-interleaved
     const float* row_add = nullptr;    // level 0: freq embedding [Fout][C]
     uint16_t* out = nullptr;           // [B][Fout][T][C] bf16
-    int probe = 0;                     // measurement probe (ATHD_FR_PROBE, fenc_row0_kernel): bit 0 no input loads,
-                                       // bit 1 no DConv, bit 2 no output stores, bit 3 no conv3 MFMAs, bit 4 no
-                                       // apply pass, bit 5 no workgroup reductions (results are garbage)
 };
 bool fenc_row_supported(int cin, int c, int T);
 int fenc_row_launch(const FencRowDesc& d, int cin, int c, hipStream_t s);
@@ -173,7 +170,7 @@ struct ConvT4Desc {
     uint32_t M = 0;                       // filled by convt4_launch
     FastDivU fd_w, fd_h, fd_hw;           // filled by convt4_launch
 };
-bool convt4_supported(int cin, int cout, int64_t M);
+bool convt4_supported(int cin, int cout, int64_t nb, int64_t H, int64_t W);
 int convt4_launch(const ConvT4Desc& d, hipStream_t s);
 // dconv.hip: one DConv layer (conv3 -> GN -> GELU -> 1x1 -> GN -> GLU -> LayerScale -> residual) for C in {48, 96}
 // x: [nb][L][C] f32 or bf16 (x_bf16), updated in place; h: [nb][L][C/8] f32 scratch

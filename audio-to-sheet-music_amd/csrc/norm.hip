@@ -621,6 +621,8 @@ int dec_merge_launch(const MergeDesc& d, hipStream_t s) {
     const int64_t n = (int64_t)d.H_out * d.W * (d.proj_w ? 1 : d.C / V);
     int blocks = (int)((n + 255) / 256);
     if (blocks > 4096) blocks = 4096;
+    // time-branch levels (W = 1, all rows stored, 4 prompts): runs of DM_RUN output rows per thread (dec_merge_w1)
+    const bool w1 = !d.proj_w && V == 8 && d.W == 1 && !d.kept && d.P == 4 && d.C_skip >= d.C;
     KScope ks(s);
     if (ks.on()) {
         // unique bytes: the source rows the H-resize touches (<= 2 per output row), the skip rows likewise (once per
@@ -630,29 +632,15 @@ int dec_merge_launch(const MergeDesc& d, hipStream_t s) {
         const double by = (double)d.NI * src_rows * d.W * d.C * (d.src_bf16 ? 2 : 4) +
                           (double)(d.NI / d.P) * skip_rows * d.W * d.C_skip * (d.skip_bf16 ? 2 : 4) +
                           (double)d.NI * d.H_out * d.W * (d.proj_w ? 2 * 4 : d.C * (d.out_bf16 ? 2 : 4));
-        ks.begin(d.proj_w ? "dec_merge_proj_kernel" : (V == 8 ? "dec_merge_kernel<8>" : "dec_merge_kernel<4>"), 0.0, by);
+        ks.begin(w1 ? (d.fast_gelu ? "dec_merge_w1_kernel<4,2,true>" : "dec_merge_w1_kernel<4,2,false>")
+                 : d.proj_w ? "dec_merge_proj_kernel" : (V == 8 ? "dec_merge_kernel<8>" : "dec_merge_kernel<4>"), 0.0, by);
     }
     const dim3 grid(blocks, d.NI / d.P);
-    static int v1 = -1;
-    if (v1 < 0) {
-        const char* e = std::getenv("ATHD_MERGE_V1");
-        v1 = e && *e && *e != '0' ? 1 : 0;
-    }
-    if (!v1 && !d.proj_w && V == 8 && d.W == 1 && !d.kept && d.P == 4 && d.C_skip >= d.C) {
+    if (w1) {
         const int64_t threads = (int64_t)((d.H_out + DM_RUN - 1) / DM_RUN) * (d.C / 8);
         const dim3 g1((unsigned)((threads + 255) / 256), d.NI / d.P);
-        static int pp = -1;
-        if (pp < 0) {
-            const char* e = std::getenv("ATHD_MERGE_PP");
-            pp = e && *e == '4' ? 4 : e && *e == '1' ? 1 : 2;
-        }
-        if (d.fast_gelu) {
-            if (pp == 4) hipLaunchKernelGGL((dec_merge_w1_kernel<4, 4, true>), g1, dim3(256), 0, s, d);
-            else if (pp == 1) hipLaunchKernelGGL((dec_merge_w1_kernel<4, 1, true>), g1, dim3(256), 0, s, d);
-            else hipLaunchKernelGGL((dec_merge_w1_kernel<4, 2, true>), g1, dim3(256), 0, s, d);
-        } else {
-            hipLaunchKernelGGL((dec_merge_w1_kernel<4, 2, false>), g1, dim3(256), 0, s, d);
-        }
+        if (d.fast_gelu) hipLaunchKernelGGL((dec_merge_w1_kernel<4, 2, true>), g1, dim3(256), 0, s, d);
+        else hipLaunchKernelGGL((dec_merge_w1_kernel<4, 2, false>), g1, dim3(256), 0, s, d);
         return (int)hipGetLastError();
     }
     if (d.proj_w) hipLaunchKernelGGL(dec_merge_proj_kernel, grid, dim3(256), 0, s, d);

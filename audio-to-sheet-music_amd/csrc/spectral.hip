@@ -517,26 +517,12 @@ void istft_ola_launch(const float* fo, int NI, int Tspec, int P, int64_t T, cons
             ks.begin("istft_ola_kernel", 0.0,
                      (double)NI * Tspec * Tspec * 2 * 4 + (double)(NI / P) * 2048 * Tspec * 4 * 4 + (double)NI * T * 2 * 4 +
                          (double)NI * 2 * T * 4);
-        static int var = -1;
-        if (var < 0) {
-            const char* e = std::getenv("ATHD_ISTFT_VAR");     // measurement override: 0 = <2, prefetch>,
-            var = e && *e ? std::atoi(e) : 2;                 // 1 = <3, prefetch>, 2 = <3, no prefetch> (default:
-                                                              // 1512 vs 1781 us for 0), 3 = <2, no pf>
-        }
+        // <3 waves per SIMD, no prefetch>: 1512 vs 1781 us for <2, prefetch> (round 2 measurement)
         if (tw64)
             hipLaunchKernelGGL((istft_ola_kernel<double, double2, 3>), grid, dim3(256), 0, s, fo, Tspec, P, (int)T, spec,
                                tw64, win, win2, xt2, tnorm, out, part, nwg, units);
-        else if (var == 1)
-            hipLaunchKernelGGL((istft_ola_kernel<float, float2, 3, true>), grid, dim3(256), 0, s, fo, Tspec, P, (int)T,
-                               spec, tw, win, win2, xt2, tnorm, out, part, nwg, units);
-        else if (var == 2)
-            hipLaunchKernelGGL((istft_ola_kernel<float, float2, 3, false>), grid, dim3(256), 0, s, fo, Tspec, P, (int)T,
-                               spec, tw, win, win2, xt2, tnorm, out, part, nwg, units);
-        else if (var == 3)
-            hipLaunchKernelGGL((istft_ola_kernel<float, float2, 2, false>), grid, dim3(256), 0, s, fo, Tspec, P, (int)T,
-                               spec, tw, win, win2, xt2, tnorm, out, part, nwg, units);
         else
-            hipLaunchKernelGGL((istft_ola_kernel<float, float2, 2, true>), grid, dim3(256), 0, s, fo, Tspec, P, (int)T,
+            hipLaunchKernelGGL((istft_ola_kernel<float, float2, 3, false>), grid, dim3(256), 0, s, fo, Tspec, P, (int)T,
                                spec, tw, win, win2, xt2, tnorm, out, part, nwg, units);
     }
     if (nwg > 1) {

@@ -144,6 +144,45 @@ def f32_line(sd, table, wav, steps=3):
     return out
 
 
+def dataset_pass(model, wav, n, batch, world, rank, dev):
+    """BASELINE configs[3]: n segments sharded over the ranks in contiguous blocks (each rank's block resident in
+    HBM: distinct segments derived from its bench batch by a per-segment roll and gain), each separated into 4 stems
+    in batches of `batch` by athd.dist.separate_segments, every result gathered point to point into one
+    preallocated (n, 4, 2, T) tensor on rank 0.  Timed: barrier + sync on both sides of the whole pass, max over
+    ranks (one pass after one untimed warm-up pass)."""
+    from athd.dist import separate_segments, shard_range
+    lo, hi = shard_range(n, world, rank)
+    blk = torch.empty((hi - lo, 2, SEG), dtype=torch.float32, device=dev)
+    for j, i in enumerate(range(lo, hi)):
+        blk[j] = torch.roll(wav[i % wav.shape[0]], shifts=(i * 7919) % SEG, dims=-1) * (0.5 + (i % 17) / 16.0)
+    out = torch.empty((n, len(STEMS), 2, SEG), dtype=torch.float32, device=dev) if rank == 0 else None
+
+    def run():
+        separate_segments(model, blk, STEMS, max_batch=batch, n_total=n, out=out)
+
+    run()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    run()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], device=dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        el = float(t.item())
+    return {"metric": "dataset pass: 6s-segments/sec (each separated into 4 stems), gather to rank 0 included",
+            "value": round(n / el, 3), "unit": "segments/s", "n_gpus": world, "segments": n,
+            "segments_per_rank": -(-n // world), "seconds": round(el, 4), "higher_is_better": True,
+            "dtype": model.dtype, "data": "synthetic (rolled / scaled bench segments)",
+            "config": {"workload": "BASELINE configs[3]: dataset of N segments batch-sharded over the GPUs, RCCL "
+                                   "point-to-point gather of every separated waveform to rank 0",
+                       "batch": batch, "prompts": 4, "parallelism": f"segment-sharded dp{world}"}}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -155,6 +194,9 @@ def main():
     ap.add_argument("--no-extras", action="store_true", help="skip the SDR, f32 and section measurements")
     ap.add_argument("--dump-kernels", default=None, help="write the warmup step's per-kernel profile (JSON)")
     ap.add_argument("--kernel", default=None, help="roofline kernel (default: largest summed time in warmup)")
+    ap.add_argument("--segments", type=int, default=0,
+                    help="also time one dataset pass of N segments over all ranks (BASELINE configs[3]: ~6k MUSDB18 "
+                         "test-set segments) through athd.dist.separate_segments; printed as a second JSON line")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -183,7 +225,7 @@ def main():
     wav = torch.as_tensor(synthetic_batch(B, SEG, seed0=1000 + B * rank)).to(dev)
     N = B * world
     out = torch.empty((N, len(STEMS), 2, SEG), dtype=torch.float32, device=dev) if rank == 0 else None
-    pending = PendingSends(limit=None)
+    pending = PendingSends(limit=2)          # at most two batches in flight per rank (bounded send buffers)
 
     def step():
         if world == 1:
@@ -325,6 +367,10 @@ def main():
         rec["cpu_baseline"] = cpu_baseline(sd, table)
     if rank == 0:
         print(json.dumps(rec), flush=True)
+    if args.segments > 0:
+        rec2 = dataset_pass(model, wav, args.segments, B, world, rank, dev)
+        if rank == 0:
+            print(json.dumps(rec2), flush=True)
     if world > 1:
         torch.distributed.barrier()
         torch.distributed.destroy_process_group()

@@ -82,7 +82,76 @@ def _bench_partial(win, k0, k1, L):
     return out, wsum
 
 
-def _worker(rank, world, port, q):
+def _fake_forward(wav, o, n_stems=4):
+    """(b, 2, T) windows -> (b, S, 2, T) stand-in stems; returns a NEW tensor (never fills `o`), the forward_fn
+    contract separate_segments must also accept on dst."""
+    return torch.stack([_fake_stem(wav, si) for si in range(n_stems)], dim=1)
+
+
+def _write_split(root, lengths, sr):
+    """A synthetic MUSDB18-HQ split: one directory per track with mixture/drums/bass/other/vocals.wav (float)."""
+    from athd.musdb import HQ_FILES, write_wav
+    g = torch.Generator().manual_seed(5)
+    for i, L in enumerate(lengths):
+        d = os.path.join(root, f"track {i:02d}")
+        os.makedirs(d, exist_ok=True)
+        for f in HQ_FILES:
+            write_wav(os.path.join(d, f + ".wav"), (0.3 * torch.randn(2, L, generator=g)).numpy(), sr, "FLOAT")
+
+
+def _dataset_checks(rank, world, split_dir, out_dir):
+    """separate_dataset over a 3-track split (benchmark protocol and the dataloader's non-overlapping segments)
+    == per-track benchmark_chunked_inference + oracle metrics, and save_results' layout."""
+    import json
+    from athd.dist import separate_dataset
+    from athd.musdb import MusDBTracks
+    from athd.weights import STEMS
+    from oracle.athtdemucs_ref import sdr_db, sisdr_db
+    tracks = MusDBTracks(split_dir, sample_rate=SR)
+    metric = lambda e, r: (sdr_db(e[None], r[None]), sisdr_db(e[None], r[None]))          # noqa: E731
+
+    def ola(win, L, chunk, ov):
+        hop = chunk - ov
+        out, wsum = torch.zeros((win.shape[1], 2, L)), torch.zeros(L)
+        for k in range(win.shape[0]):
+            s, e = k * hop, min(k * hop + chunk, L)
+            a = e - s
+            fl = min(ov, a // 2)
+            w = torch.ones(a)
+            if s > 0 and fl > 0:
+                w[:fl] = torch.linspace(0, 1, fl)
+            if e < L and fl > 0:
+                w[-fl:] = torch.linspace(1, 0, fl)
+            out[:, :, s:e] += win[k, :, :, :a] * w
+            wsum[s:e] += w
+        return out / wsum.clamp(min=1e-8)
+
+    for ovs in (1.5, 0.0):
+        res = separate_dataset(None, tracks, STEMS, segment_seconds=SEG, overlap=ovs, sample_rate=SR, max_batch=2,
+                               forward_fn=_fake_forward, ola_fn=ola, metric_fn=metric, keep_estimates=True,
+                               output_dir=out_dir if (rank == 0 and ovs) else None, log=None)
+        if rank != 0:
+            assert res is None
+            continue
+        results, est = res
+        assert [r.track_name for r in results] == [tracks.name(i) for i in range(len(tracks))]
+        for i, r in enumerate(results):
+            name, mix, refs = tracks.track(i)
+            for si, s in enumerate(STEMS):
+                want = benchmark_chunked_inference(lambda c: _fake_stem(c, si), mix, SR, SEG, ovs)
+                assert torch.equal(est[name][si], want), (ovs, name, s)
+                sd, ss = metric(want, refs[s])
+                assert getattr(r, f"sdr_{s}") == sd and getattr(r, f"sisdr_{s}") == ss, (ovs, name, s)
+    if rank == 0:
+        saved = json.load(open(os.path.join(out_dir, "evaluation_results.json")))
+        (mname, body), = saved.items()
+        assert mname == "AudioTextHTDemucs (Ours)" and set(body) == {"per_track", "aggregate"}
+        assert [p["track"] for p in body["per_track"]] == [tracks.name(i) for i in range(len(tracks))]
+        assert set(body["per_track"][0]["sdr"]) == set(STEMS) | {"average"}
+        assert set(body["aggregate"]) == {"sdr", "sisdr"}
+
+
+def _worker(rank, world, port, q, split_dir=None, out_dir=None):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         import torch.distributed as dist
@@ -119,6 +188,25 @@ def _worker(rank, world, port, q):
         out = separate_segments(None, segs[:1], ["a", "b", "c"], forward_fn=fwd, max_batch=2)
         if rank == 0:
             assert torch.equal(out, ref[:1]), "segments N=1"
+        # bench.py's N>1 call pattern: block-local input, `out` slices on rank 0, transfers left pending across
+        # 3 steps of >= 3 batches per rank with at most 2 in flight (PendingSends(limit=2)); forward_fn returns a
+        # new tensor (copied into `out` on rank 0)
+        lo, hi = shard_range(14, world, rank)
+        segs14 = torch.randn(14, 2, 300, generator=torch.Generator().manual_seed(14))
+        ref14 = torch.stack([_fake_stem(segs14, si) for si in range(4)], dim=1)
+        pend = PendingSends(limit=2)
+        res = torch.full((14, 4, 2, 300), float("nan")) if rank == 0 else None
+        peak = 0
+        for _ in range(3):
+            out = separate_segments(None, segs14[lo:hi], ["a", "b", "c", "d"], forward_fn=_fake_forward,
+                                    max_batch=2, n_total=14, out=res, pending=pend)
+            peak = max(peak, len(pend.works))
+        pend.wait()
+        assert peak <= 2, peak
+        if rank == 0:
+            assert out is res and torch.equal(out, ref14), "bench pattern"
+        if split_dir is not None:
+            _dataset_checks(rank, world, split_dir, out_dir)
         # --- one track, windows sharded over ranks
         L = 25000
         mix = torch.randn(2, L)
@@ -162,12 +250,15 @@ def test_shard_range():
             assert sum(b - a for a, b in blocks) == n and all(blocks[i][1] == blocks[i + 1][0] for i in range(w - 1))
 
 
-def test_world2_gloo():
+def test_world2_gloo(tmp_path):
+    split = tmp_path / "test"
+    _write_split(str(split), [25000, 6000 * 2 + 17, 4000], SR)
     # spawn, not fork: a child forked after the parent used torch's CPU thread pool can deadlock
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    ps = [ctx.Process(target=_worker, args=(r, 2, port, q, str(split), str(tmp_path / "results")))
+          for r in range(2)]
     for p in ps:
         p.start()
     res = {}

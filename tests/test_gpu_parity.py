@@ -141,6 +141,33 @@ def test_ragged_length(models, oracle_model, text_table, T):
             assert s >= BF16_SDR_DB, s
 
 
+@pytest.mark.parametrize("T,B", [(300000, 1), (4096, 2)])
+def test_prompts_long_and_short(models, oracle_model, text_table, T, B):
+    """forward_prompts (4 prompts) at the two ends of the supported lengths, both dtypes, against the oracle:
+      * T = 300000 (Tspec = 293 > 272): the frequency levels 0-1 take the unfused implicit-GEMM path (fenc_row.hip
+        holds at most 272 frames per row), the main.py:277-290 "variable lengths" case beyond one 6 s window;
+      * T = 4096 (Tspec = 4), B = 2: 8 decode items whose level-2 ConvT rows per item (Tspec^2 = 16 freq, L = 16
+        time) are fewer than a convt4 unit's 32, so a unit would straddle 3+ items: the tiled four-residue GEMM
+        runs instead (convt4_supported)."""
+    from athd.synth import synthetic_batch
+    wav = torch.as_tensor(synthetic_batch(B, T, seed0=T % 1000 + 11))
+    cap = {}
+    oracle_model.forward(wav[:1], torch.as_tensor(text_table[:1]), capture=cap)
+    cond = _phase_cond(cap["z"])
+    ref = oracle_model.forward_prompts(wav, torch.as_tensor(text_table)).numpy()
+    for dt in ("f32", "bf16"):
+        out = models[dt].forward_prompts(wav.cuda(), ["drums", "bass", "other", "vocals"]).cpu().numpy()
+        assert out.shape == ref.shape and np.isfinite(out).all()
+        s = min(sdr_db(ref[b, p], out[b, p]) for b in range(B) for p in range(4))
+        _report(f"prompts_T{T}_B{B}/{dt}", {"sdr_db_min_vs_oracle": s, "phase_cond": cond})
+        if dt == "bf16":
+            assert s >= BF16_SDR_DB, s
+        elif cond >= PHASE_COND_MIN:
+            assert s >= F32_SDR_DB, s
+        else:
+            assert s >= F32_FIXTURE_DB["b1_t44100_vocals"], (s, cond)
+
+
 def test_forward_prompts_matches_forward(models):
     """Encode-once/decode-P path == P separate forwards.  f32 model: equal to fp32 rounding (GroupNorm statistics
     are fp64 atomics whose order varies); bf16 model: the two paths agree to >= 40 dB (order-dependent statistics

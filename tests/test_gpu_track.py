@@ -70,6 +70,40 @@ def test_sdr_loss_matches_reference_formula():
     assert abs(-sdr_loss(est.cuda(), t4.cuda()).item() - sdr_db(est, t4)) < 1e-4
 
 
+def test_loss_known_answers_main_py():
+    """The reference's own known-answer loss checks, `main.py:65-140` (test_losses), on athd_sdr / athd_sisdr with
+    (4, 2, 44100) batches: perfect reconstruction clamps both at +30 dB; a random estimate is negative; a 2x gain
+    gives SDR 10 log10(|s|^2 / |s|^2) = 0 dB and SI-SDR +30 (clamp); target + noise at SNR 20 / 10 / 5 / 0 / -5 dB
+    gives SDR ~ SNR (decreasing); 0.8 target + 0.2 interference gives 10 log10(1 / 0.08) = 10.97 dB (the comment
+    at main.py:136 says "~13-14 dB"; the arithmetic says 11.0).  Every value also equals the oracle's fp64 restatement
+    of src/loss.py to 1e-4 dB (1e-3 for SI-SDR, computed in fp32 torch ops by the reference)."""
+    from athd.inference import sdr_loss, sisdr_loss
+    from oracle.athtdemucs_ref import sisdr_db
+    g = torch.Generator().manual_seed(65)
+
+    def both(est, tgt):
+        s = -sdr_loss(est.cuda(), tgt.cuda()).item()
+        si = -sisdr_loss(est.cuda(), tgt.cuda()).item()
+        assert abs(s - sdr_db(est, tgt)) < 1e-4 and abs(si - sisdr_db(est, tgt)) < 1e-3, (s, si)
+        return s, si
+
+    tgt = torch.randn(4, 2, 44100, generator=g)
+    assert both(tgt.clone(), tgt) == (30.0, 30.0)                                   # Test 1
+    s, si = both(torch.randn(4, 2, 44100, generator=g), torch.randn(4, 2, 44100, generator=g))
+    assert s < 0 and si < 0                                                          # Test 2
+    s, si = both(2.0 * tgt, tgt)                                                     # Test 3
+    assert abs(s) < 1e-5 and si == 30.0
+    prev = None
+    for snr_db in (20, 10, 5, 0, -5):                                                # Test 4
+        noise = torch.randn(4, 2, 44100, generator=g) * torch.sqrt((tgt ** 2).mean() / 10 ** (snr_db / 10))
+        s, _ = both(tgt + noise, tgt)
+        assert abs(s - snr_db) < 0.2, (snr_db, s)
+        assert prev is None or s < prev
+        prev = s
+    s, _ = both(0.8 * tgt + 0.2 * torch.randn(4, 2, 44100, generator=g), tgt)     # Test 5
+    assert abs(s - 10 * np.log10(1 / 0.08)) < 0.2, s
+
+
 def test_separate_track_matches_oracle_loop(state_dict, text_table, oracle_model):
     """12.1 s track, 3 windows (2 full + a 10k-sample tail), 2 stems, f32 model vs the oracle running the
     reference loop window by window (B=1, one stem at a time)."""
