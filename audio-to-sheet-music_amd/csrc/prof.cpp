@@ -21,16 +21,25 @@ static bool sites_on() {
 void KScope::begin(const std::string& label0, double flops, double bytes) {
     KProf* p = t_kprof;
     if (!p) return;
+    // call-site label "kernel@stage.site" (when the launch has a stage / site tag)
+    std::string site = label0;
+    if (t_kstage || t_ksite) {
+        site += "@";
+        if (t_kstage) site += t_kstage;
+        if (t_kstage && t_ksite) site += ".";
+        if (t_ksite) site += t_ksite;
+    }
     std::string label = label0;
     if (p->only == "@section") {
         label = t_ksection ? t_ksection : "other";
-    } else if (sites_on() && (t_kstage || t_ksite)) {
-        label += "@";
-        if (t_kstage) label += t_kstage;
-        if (t_kstage && t_ksite) label += ".";
-        if (t_ksite) label += t_ksite;
+    } else if (p->only == "@sites" || sites_on()) {
+        label = site;
     }
-    if (!p->only.empty() && p->only != "@section" && p->only != label) return;
+    if (!p->only.empty() && p->only[0] != '@') {
+        // one kernel ("gemm4_kernel<129>") or one call site of it ("gemm4_kernel<129>@transformer.linear1")
+        if (p->only != (p->only.find('@') != std::string::npos ? site : label0)) return;
+        label = p->only;
+    }
     hipEvent_t ev[2];
     for (auto& e : ev) {
         if (!p->pool.empty()) {

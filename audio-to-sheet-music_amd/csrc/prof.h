@@ -15,7 +15,8 @@ namespace athd {
 
 struct KProf {
     std::string only;                      // "" = every kernel, "@section" = every kernel aggregated per forward
-                                           // section (KSection), else one label
+                                           // section (KSection), "@sites" = every kernel per call site
+                                           // ("kernel@stage.site"), else one kernel label or one call-site label
     struct Rec { std::string label; hipEvent_t a, b; double flops, bytes; };
     struct Agg { std::string label; long long n; double ms, flops, bytes; };
     std::vector<Rec> recs;

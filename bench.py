@@ -236,25 +236,36 @@ def main():
     def fwd_only():
         return model.forward_prompts(wav, STEMS)
 
-    # warmup; the last warmup step times every kernel (HIP events) to find the dominant one
+    # warmup; the last warmup step times every kernel per call site (HIP events) to find the dominant call site
     for i in range(args.warmup):
         if i == args.warmup - 1:
-            model.profile_start(None)
+            model.profile_start("@sites")
         step()
     pending.wait()
     torch.cuda.synchronize()
     dominant = args.kernel
+    sites = []
     if args.warmup > 0:
-        allk = model.profile_stop()
+        sites = model.profile_stop()
         if args.dump_kernels and rank == 0:
-            for r in allk:
+            per_kernel = {}
+            for r in sites:
+                a = per_kernel.setdefault(r["kernel"].split("@", 1)[0],
+                                          {"kernel": r["kernel"].split("@", 1)[0], "launches": 0, "ms": 0.0,
+                                           "flops": 0.0, "bytes": 0.0})
+                for f in ("launches", "ms", "flops", "bytes"):
+                    a[f] += r[f]
+            allk = list(per_kernel.values())
+            for r in allk + sites:
                 r["tflops"] = r["flops"] / (r["ms"] * 1e-3) / 1e12 if r["ms"] else 0.0
                 r["gbs"] = r["bytes"] / (r["ms"] * 1e-3) / 1e9 if r["ms"] else 0.0
             json.dump(sorted(allk, key=lambda r: -r["ms"]), open(args.dump_kernels, "w"), indent=1)
+            json.dump(sorted(sites, key=lambda r: -r["ms"]), open(args.dump_kernels.replace(".json", "_sites.json"),
+                                                                   "w"), indent=1)
         if dominant is None:
-            dominant = max(allk, key=lambda r: r["ms"])["kernel"]
+            dominant = max(sites, key=lambda r: r["ms"])["kernel"]
     if dominant is None:
-        dominant = "attn_bf16_kernel"
+        dominant = "attn32_kernel@transformer"
 
     def barrier():
         if world > 1:
@@ -296,9 +307,10 @@ def main():
     if kp is None or kp["launches"] == 0:
         raise RuntimeError(f"roofline kernel {dominant!r} was not launched in the timed region")
     per_launch_ms = kp["ms"] / kp["launches"]
-    # the kernel's bound is the larger of its two floors: algorithmic flops at the MFMA peak, algorithmic bytes at
+    kernel_sym = dominant.split("@", 1)[0]
+    # the call site's bound is the larger of its two floors: algorithmic flops at the MFMA peak, algorithmic bytes at
     # the HBM peak (e.g. the decoder's K = 288 ConvT GEMM moves 6.2 GB for 1.2 TFLOP: HBM-bound)
-    t_mfma = kp["flops"] / (peak_mfma * 1e12) if dominant.startswith(MFMA_KERNELS) else 0.0
+    t_mfma = kp["flops"] / (peak_mfma * 1e12) if kernel_sym.startswith(MFMA_KERNELS) else 0.0
     t_hbm = kp["bytes"] / (HBM_PEAK_GBS * 1e9)
     if t_mfma >= t_hbm:
         peak = peak_mfma
@@ -307,17 +319,29 @@ def main():
     else:
         peak, bound, unit = HBM_PEAK_GBS, "hbm", "GB/s"
         ach = kp["bytes"] / (kp["ms"] * 1e-3) / 1e9
-    traffic, traffic_src = pmc_traffic(dominant, B, args.dtype)
+    traffic, traffic_src = pmc_traffic(kernel_sym, B, args.dtype)
+    # the same kernel over ALL its call sites (warm-up profile): what rocprofv3's per-symbol average reports
+    same = [r for r in sites if r["kernel"].split("@", 1)[0] == kernel_sym]
+    all_sites = None
+    if same:
+        n_all = sum(r["launches"] for r in same)
+        all_sites = {"kernel": kernel_sym, "launches_per_step": n_all, "sites": len(same),
+                     "avg_launch_us": round(sum(r["ms"] for r in same) / n_all * 1e3, 2),
+                     "timing": "warm-up step, every launch evented, branches serialised"}
     roofline = {"bound": bound, "achieved": round(ach, 2), "peak": peak, "unit": unit, "frac": round(ach / peak, 4),
-                "traffic": traffic, "kernel": dominant, "launches_per_step": kp["launches"] / ROOF_STEPS,
+                "traffic": traffic, "kernel": kernel_sym, "call_site": dominant,
+                "kernel_all_sites": all_sites,
+                "traffic_note": "PMC bytes per launch of the kernel symbol (all call sites; rocprofv3 cannot split "
+                                "them)" if all_sites and all_sites["sites"] > 1 else "PMC bytes per launch",
+                "launches_per_step": kp["launches"] / ROOF_STEPS,
                 "avg_launch_us": round(per_launch_ms * 1e3, 2),
                 "share_of_step": round(kp["ms"] / ROOF_STEPS / ms, 4),
                 "algorithmic_per_launch": {"flops": kp["flops"] / kp["launches"],
                                            "bytes": kp["bytes"] / kp["launches"]},
                 "floors_ms_per_launch": {"mfma": round(t_mfma * 1e3 / kp["launches"], 4),
                                          "hbm": round(t_hbm * 1e3 / kp["launches"], 4)},
-                "timing": f"HIP events on the launch stream around every launch of the kernel, {ROOF_STEPS} forwards "
-                          "after the timed region (branches serialised on one stream)",
+                "timing": f"HIP events on the launch stream around every launch of the call site, {ROOF_STEPS} "
+                          "forwards after the timed region (branches serialised on one stream)",
                 "step": {"achieved_tflops": round(step_tf, 2), "peak": peak_mfma, "frac": round(step_tf / peak_mfma, 4),
                          "basis": "essential FLOPs per step (SURVEY.md §8(d): 256.5 GFLOP per segment x 4 stems) / "
                                   "timed ms per step"}}

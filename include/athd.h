@@ -129,6 +129,8 @@ int athd_sisdr(const float* est, const float* target, int64_t rows, int64_t n, d
  * by this context's forwards is bracketed by HIP events on the launch stream.  athd_profile_stop synchronises
  * those events and aggregates per kernel: launches, summed event time, summed ALGORITHMIC flops and bytes.
  * kernel = "@section": every kernel, aggregated per forward section ("encoder", "transformer", "decoder").
+ * kernel = "@sites": every kernel per call site, labelled "kernel@stage.site" (e.g.
+ * "gemm4_kernel<129>@transformer.linear1"); kernel = "<kernel>@<stage.site>": every launch of that one call site.
  * While a profile is open the time branch runs on the caller's stream, so each event pair times one kernel. */
 int athd_profile_start(athd_ctx* ctx, const char* kernel);
 int athd_profile_stop(athd_ctx* ctx);

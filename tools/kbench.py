@@ -250,6 +250,16 @@ if __name__ == "__main__":
         gemm_case(256 * 32 * 259, 768, 192)
         gemm_case(M, 1536, 512)
         sys.exit(0)
+    if "g5" in sys.argv[1:]:
+        VARIANTS = (40, 50)
+        for _ in range(2):
+            gemm_case(M, 1536, 512)
+            gemm_case(M, 2048, 512, act=1)
+            gemm_case(M, 512, 2048)
+            gemm_case(M, 512, 512)
+            gemm_case(4096, 4096, 4096)
+            gemm_case(256 * 32 * 259, 768, 192)
+        sys.exit(0)
     if "g4" in sys.argv[1:]:
         gemm_case(M, 1536, 512)
         gemm_case(M, 2048, 512, act=1)
