@@ -284,6 +284,7 @@ int gemm3_launch(const GemmDesc& d, hipStream_t s, int variant);
 int gemm3_ln_launch(const GemmDesc& d, hipStream_t s);
 bool gemm4_supported(const GemmDesc& d);
 int gemm4_launch(const GemmDesc& d, hipStream_t s);
+int gemm5_launch(const GemmDesc& d, hipStream_t s);
 
 int gemm_launch(const GemmDesc& d0, int mode, hipStream_t s) {
     if (d0.Kp % BK != 0 || d0.Kp < d0.K || d0.C_in <= 0 || d0.N <= 0) return -2;
@@ -292,7 +293,13 @@ int gemm_launch(const GemmDesc& d0, int mode, hipStream_t s) {
     if (d.ln_w) return mode == 1 ? gemm3_ln_launch(d, s) : -2;      // row-LayerNorm epilogue: gemm3 only
     // bf16 activations, N a multiple of 256: 256x256 tile, half-tile staged pipeline (gemm4.hip).  (Measured on
     // N = 192 / 384: slower than gemm3's 256x192 tiles, which waste no columns.)
+    // (gemm5: the same tile and epilogues with a staggered two-group K-loop, gemm5.hip; -DATHD_GEMM5 builds that
+    // dispatch for A/B measurement)
+#ifdef ATHD_GEMM5
+    if (mode == 1 && gemm4_supported(d) && d.N % 256 == 0) return gemm5_launch(d, s);
+#else
     if (mode == 1 && gemm4_supported(d) && d.N % 256 == 0) return gemm4_launch(d, s);
+#endif
     // other N >= 192: 256x192 or 192x192 tile, 8 waves (gemm3.hip)
     // (K >= 384: 192x192 tiles with a 3-stage ring, two K-tiles in flight across each barrier; measured per call
     // site 2-20 % faster there.  Shorter K, e.g. the K=288 four-residue ConvT, keeps 256x192 x 2 stages.)

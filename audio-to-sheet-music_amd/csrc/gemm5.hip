@@ -4,21 +4,25 @@
 // The 8 waves are two groups of 4, G0 = waves 0-3 (tile rows 0-127) and G1 = waves 4-7 (rows 128-255): a SIMD holds
 // one wave of each.  A K-tile is 4 phases, one 64 x 32 accumulator quadrant each (16 v_mfma_f32_16x16x32_bf16):
 //   p0 (A0, B0)   p1 (A0, B1)   p2 (A1, B1)   p3 (A1, B0)        fragment reads: p0 A0 + B0, p1 B1, p2 A1, p3 none
-// and a group spends a phase in two SECTIONS separated by workgroup barriers: a load section (its fragment reads, one
-// half-tile of LDS-DMA staging) and an MFMA section (s_waitcnt lgkmcnt(0), s_setprio 1, the 16 MFMAs).  G1 runs one
-// section behind G0 (one extra barrier before its first section), so in every section one group's MFMAs share each
-// SIMD with the other group's LDS reads and DMA issue: matrix beside memory.  gemm4 (both waves of a SIMD read, then
-// both multiply) issues MFMAs ~53 % of its K-loop cycles.
+// and a group spends a phase in two SECTIONS separated by workgroup barriers: a load section (its fragment reads and
+// its share of the LDS-DMA staging) and an MFMA section (s_waitcnt lgkmcnt(0), s_setprio 1, the 16 MFMAs).  G1 runs
+// one section behind G0 (one extra barrier before its first section), so in every section one group's MFMAs share
+// each SIMD with the other group's LDS reads and DMA issue: matrix beside memory.
 //
-// Sections s = 0..7 of K-tile u (G0 loads in even s, G1 in odd s); the half-tile each group stages (2 pieces of 1 KB
-// per wave, gemm4's piece -> wave map, so a half-tile is complete after one G0 and one G1 section):
-//   s0 G0: B1(u+1)  s1 G1: A1(u+1)  s2 G0: A1(u+1)  s3 G1: A0(u+2)  s4 G0: A0(u+2)  s5 G1: B0(u+2)  s6 G0: B0(u+2)
-//   s7 G1: B1(u+2)
-// WAR: each slot is restaged >= 2 sections after its last fragment read (those reads retire at the reader's next
-// lgkmcnt(0), one section later, before a barrier).  RAW: at each load section a wave waits until only the pieces of
-// its previous 3 load sections are in flight (counted vmcnt), so a piece issued in section x is retired in section
-// x + 8 and published by that section's closing barrier; every slot is first read >= 10 sections after its pieces
-// were issued.
+// Staging: every half-tile slot of K-tile u + 2 is restaged in the first section its WAR allows (a slot's last
+// fragment reads retire at the reader's next lgkmcnt(0), one section later, before that section's barrier), each
+// wave issuing gemm4's 2 pieces of 1 KB per half-tile.  Sections s = 0..7 of K-tile u, G0 loading in even s, G1 in
+// odd s:
+//   s0 G0: A1(u+1)   s1 G1: -   s2 G0: -   s3 G1: A0 B0(u+2)   s4 G0: A0 B0(u+2)   s5 G1: B1(u+2)   s6 G0: B1(u+2)
+//   s7 G1: A1(u+2)
+// RAW: at each load section a wave waits (counted vmcnt) until only the pieces of its previous 4 load sections are in
+// flight: a piece issued in section x is retired by section x + 10 and published by that section's barrier; every
+// slot is first read >= 12 sections after its pieces were issued.  That keeps ~1 K-tile (64 KB) per CU in flight.
+// kbench (one box, random operands; tools/kbench.py g5var): M = 132608, N = 1536 / 512, K = 512: +5 / +14 % over
+// gemm4; K = 2048: equal.  The start-up sleep gemm4 uses to desynchronise epilogue store bursts cost 4096^3 a third
+// of its time in isolation, so gemm5 has none.
+// Persistent grid (epilogues without residual or statistics, as gemm4): the resident blocks walk their tiles and
+// issue the next tile's first K-tiles before the current tile's epilogue.
 #include "common.h"
 #include "prof.h"
 #include "gemm.h"
@@ -36,8 +40,9 @@ typedef __attribute__((address_space(1))) void gbl_void;
 
 constexpr int G5_SLOT = 16384;     // one half-tile slot: 128 rows x 64 bf16
 
-ATHD_DEV void vm_wait_n(int n) {   // n = 0, 2, 4, 6 (wave-uniform)
-    if (n >= 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+ATHD_DEV void vm_wait_n(int n) {   // n = 0, 2, 4, 6, 8 (wave-uniform)
+    if (n >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (n >= 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
     else if (n >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     else if (n >= 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -58,12 +63,18 @@ ATHD_DEV int xcd_remap5(int i, int n) {
 
 __device__ __attribute__((aligned(64))) uint4 g_zero_page5[4];
 
-template <unsigned F>
+// PROBE (tools/kbench ablations only; the product instantiates 0): 1 = no LDS-DMA staging in the K-loop, 2 = no
+// fragment reads in the K-loop, 3 = no MFMAs, 4 = no section barriers in the K-loop (results are garbage).
+template <unsigned F, int PROBE = 0>
 __global__ __launch_bounds__(512) void gemm5_kernel(const GemmDesc d) {
+    constexpr bool PERSIST = (F & (F_RES | F_STATS)) == 0;
     constexpr int TM = 8, TN = 4;
     constexpr int NW = 8;
-    __shared__ __attribute__((aligned(16))) char smem[8 * G5_SLOT + 2 * EPI_MAXG * 8];
+    // one LDS array (cdna_hip_programming.md §5 item 4(a)): 8 staging slots | GroupNorm statistics | bias of the
+    // current and the next tile (the bias stays out of the K-loop's registers)
+    __shared__ __attribute__((aligned(16))) char smem[8 * G5_SLOT + 2 * EPI_MAXG * 8 + 2 * 256 * 4];
     double* st_lds = reinterpret_cast<double*>(smem + 8 * G5_SLOT);
+    float* bias_lds = reinterpret_cast<float*>(smem + 8 * G5_SLOT + 2 * EPI_MAXG * 8);
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -78,34 +89,40 @@ __global__ __launch_bounds__(512) void gemm5_kernel(const GemmDesc d) {
     const int chunk = (lane & 7) ^ lrow;       // global 16-B chunk this lane fetches (LDS slot = chunk ^ row&7)
     const char* zero = reinterpret_cast<const char*>(g_zero_page5);
 
-    const int id = xcd_remap5(blockIdx.x, ntiles);
-    const int64_t m0 = (int64_t)(id / ntn) * 256;
-    const int n0 = (id % ntn) * 256;
+    int tile = blockIdx.x;
+    int64_t m0 = 0;
+    int n0 = 0;
     // this lane's slot rows: sr = 8 (wave + 8 q) + lrow, q = 0, 1 (gemm4's piece map)
     uint32_t a_base[2][2];
     int a_h0[2][2];
     uint32_t b_off[2];
+    auto setup = [&](int t) {
+        const int id = xcd_remap5(t, ntiles);
+        m0 = (int64_t)(id / ntn) * 256;
+        n0 = (id % ntn) * 256;
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
+        for (int h = 0; h < 2; ++h)
 #pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            const int sr = 8 * (wave + NW * q) + lrow;
-            const int r = (sr >> 6) * 128 + 64 * h + (sr & 63);
-            const uint32_t m = (uint32_t)(m0 + r);
-            const bool ok = m < (uint32_t)M;
-            const uint32_t mm = ok ? m : 0u;
-            const uint32_t t2 = fdiv(mm, d.fd_w);
-            const uint32_t w = mm - t2 * (uint32_t)d.W;
-            const uint32_t b = fdiv(t2, d.fd_h);
-            const uint32_t ho = t2 - b * (uint32_t)d.H_out;
-            a_base[h][q] = (uint32_t)(b * a_bs + (int64_t)w * d.a_ld);
-            a_h0[h][q] = ok ? (int)ho * d.in_stride + d.in_off : (INT_MIN / 2);
-            if (h == 0) b_off[q] = (uint32_t)(((int64_t)(n0 + (sr >> 5) * 64 + (sr & 31)) * d.Kp + 8 * chunk) * 2);
-        }
+            for (int q = 0; q < 2; ++q) {
+                const int sr = 8 * (wave + NW * q) + lrow;
+                const int r = (sr >> 6) * 128 + 64 * h + (sr & 63);
+                const uint32_t m = (uint32_t)(m0 + r);
+                const bool ok = m < (uint32_t)M;
+                const uint32_t mm = ok ? m : 0u;
+                const uint32_t t2 = fdiv(mm, d.fd_w);
+                const uint32_t w = mm - t2 * (uint32_t)d.W;
+                const uint32_t b = fdiv(t2, d.fd_h);
+                const uint32_t ho = t2 - b * (uint32_t)d.H_out;
+                a_base[h][q] = (uint32_t)(b * a_bs + (int64_t)w * d.a_ld);
+                a_h0[h][q] = ok ? (int)ho * d.in_stride + d.in_off : (INT_MIN / 2);
+                if (h == 0) b_off[q] = (uint32_t)(((int64_t)(n0 + (sr >> 5) * 64 + (sr & 31)) * d.Kp + 8 * chunk) * 2);
+            }
+    };
     const uint32_t b_h1 = (uint32_t)(32 * d.Kp * 2);     // slot B1 rows are 32 columns further
     const int nk = d.Kp / 64;
 
     auto issueA = [&](int kt, int h) {
+        if (PROBE == 1 && kt > 1) return;
         char* dst = smem + ((kt & 1) * 4 + h) * G5_SLOT;
         const int k = kt * 64 + 8 * chunk;
         const bool kok = k < d.K;
@@ -119,6 +136,7 @@ __global__ __launch_bounds__(512) void gemm5_kernel(const GemmDesc d) {
         }
     };
     auto issueB = [&](int kt, int h) {
+        if (PROBE == 1 && kt > 1) return;
         char* dst = smem + ((kt & 1) * 4 + 2 + h) * G5_SLOT;
         const char* wb = (const char*)d.Wp + (int64_t)kt * 128 + (h ? b_h1 : 0u);
 #pragma unroll
@@ -128,6 +146,7 @@ __global__ __launch_bounds__(512) void gemm5_kernel(const GemmDesc d) {
 
     const int fr = lane & 15, g = lane >> 4;
     auto readA = [&](int buf, int mh, bf16v8 (&af)[4][2]) {
+        if (PROBE == 2) return;
         const char* base = smem + (buf * 4 + mh) * G5_SLOT + (wr * 64 + fr) * 128;
 #pragma unroll
         for (int i = 0; i < 4; ++i)
@@ -136,6 +155,7 @@ __global__ __launch_bounds__(512) void gemm5_kernel(const GemmDesc d) {
                 af[i][ks] = *reinterpret_cast<const bf16v8*>(base + i * 16 * 128 + ((4 * ks + g) ^ (fr & 7)) * 16);
     };
     auto readB = [&](int buf, int nh, bf16v8 (&bf)[2][2]) {
+        if (PROBE == 2) return;
         const char* base = smem + (buf * 4 + 2 + nh) * G5_SLOT + (wc * 32 + fr) * 128;
 #pragma unroll
         for (int j = 0; j < 2; ++j)
@@ -145,14 +165,18 @@ __global__ __launch_bounds__(512) void gemm5_kernel(const GemmDesc d) {
     };
 
     f32x4_t acc[TM][TN];
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
     auto quad = [&](int mh, int nh, const bf16v8 (&af)[4][2], const bf16v8 (&bf)[2][2]) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_setprio(1);
+        if (PROBE == 3) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) asm volatile("" ::"v"(af[i][0]), "v"(af[i][1]));
+#pragma unroll
+            for (int j = 0; j < 2; ++j) asm volatile("" ::"v"(bf[j][0]), "v"(bf[j][1]));
+            __builtin_amdgcn_s_setprio(0);
+            return;
+        }
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
@@ -163,127 +187,177 @@ __global__ __launch_bounds__(512) void gemm5_kernel(const GemmDesc d) {
                         __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][ks], af[i][ks], acc[4 * mh + i][2 * nh + j], 0, 0, 0);
         __builtin_amdgcn_s_setprio(0);
     };
-    if (d.stats && tid < 2 * EPI_MAXG) st_lds[tid] = 0.0;
-    float4 bias4[TN];                             // loaded now: retired long before the epilogue needs it
-    load_bias4<TN>(d, n0, wn0, lane, bias4);
-    // Desynchronise the first wave of workgroups (one per CU) as gemm4 does: their epilogue store bursts then
-    // overlap other CUs' K-loops
-    if (blockIdx.x < 256) {
-        const int q = (int)(blockIdx.x >> 3) & 3;
-        const int n = q * (nk + 5) / 8;
-        for (int i = 0; i < n; ++i) __builtin_amdgcn_s_sleep(127);
-    }
-
-    // prologue: K-tile 0 whole, then what the steady state would have staged in the sections of K-tile -1:
-    // A0(1), B0(1) (both groups), B1(1) (G1 only; G0 stages its pieces in section 0)
-    issueA(0, 0);
-    issueB(0, 0);
-    issueB(0, 1);
-    issueA(0, 1);
-    const bool two = nk > 1;
-    if (two) {
-        issueA(1, 0);
-        issueB(1, 0);
-        if (wr == 1) issueB(1, 1);
-    }
-    // retire K-tile 0 (this wave's pieces of tile 1 stay in flight) and publish it
-    if (!two) vm_wait_n(0);
-    else if (wr == 0) vm_wait_n(4);
-    else vm_wait_n(6);
-    section_barrier();
-    // issue history of this wave's previous three load sections (for the counted waits); the prologue's tile-1
-    // pieces stand for the K-tile -1 sections that would have issued them
-    bool h1 = two, h2 = two, h3 = two && wr == 1;
-    auto load_wait = [&]() { vm_wait_n(2 * ((int)h1 + (int)h2 + (int)h3)); };
-    auto push = [&](bool issued) {
-        h3 = h2;
-        h2 = h1;
-        h1 = issued;
+    // pieces this wave issued in each of its previous load sections (hist[0] = most recent), for the counted waits
+    int hist[4] = {0, 0, 0, 0};
+    auto load_wait = [&]() { vm_wait_n(hist[0] + hist[1] + hist[2] + hist[3]); };
+    auto push = [&](int pieces) {
+        hist[3] = hist[2];
+        hist[2] = hist[1];
+        hist[1] = hist[0];
+        hist[0] = pieces;
     };
-    if (wr == 1) section_barrier();               // the stagger: G1 runs one section behind G0
+    // prologue of a tile: K-tile 0 whole, then what the sections of K-tile -1 would have staged: A0(1), B0(1), B1(1)
+    // (both groups) and A1(1) (G1; G0 stages its pieces in section 0); afterwards the pieces of K-tile 1 are the
+    // in-flight history
+    const bool two = nk > 1;
+    auto prologue = [&]() {
+        issueA(0, 0);
+        issueB(0, 0);
+        issueB(0, 1);
+        issueA(0, 1);
+        hist[0] = hist[1] = hist[2] = hist[3] = 0;
+        if (two) {
+            issueA(1, 0);
+            issueB(1, 0);
+            issueB(1, 1);
+            if (wr == 1) issueA(1, 1);
+            if (wr == 0) { hist[0] = 2; hist[1] = 4; }                 // u=-1: p3 B1, p2 A0 + B0
+            else { hist[0] = 2; hist[1] = 2; hist[2] = 4; }            // u=-1: p3 A1, p2 B1, p1 A0 + B0
+        }
+    };
+    if (d.stats && tid < 2 * EPI_MAXG) st_lds[tid] = 0.0;
+    setup(tile);
+    // the tile's 256 bias values, one per thread of waves 0-3 (0 past N or without bias)
+    auto bias_load = [&]() -> float {
+        return (tid < 256 && d.bias && n0 + tid < d.N) ? d.bias[n0 + tid] : 0.f;
+    };
+    int bsel = 0;
+    {
+        const float bv = bias_load();
+        if (tid < 256) bias_lds[tid] = bv;
+    }
+    prologue();
+    load_wait();                                  // K-tile 0 retired (K-tile 1's pieces stay in flight) ...
+    section_barrier();                            // ... and published (the bias too)
 
     bf16v8 af[4][2], bf0[2][2], bf1[2][2];
-    for (int u = 0; u < nk; ++u) {
-        const int buf = u & 1;
-        const bool n1 = u + 1 < nk, n2 = u + 2 < nk;
-        // ---- phase 0: (A0, B0)
-        load_wait();
-        if (wr == 0) {
-            if (n1) issueB(u + 1, 1);
-            push(n1);
-        } else {
-            if (n1) issueA(u + 1, 1);
-            push(n1);
-        }
-        readB(buf, 0, bf0);
-        readA(buf, 0, af);
-        section_barrier();
-        quad(0, 0, af, bf0);
-        section_barrier();
-        // ---- phase 1: (A0, B1)
-        load_wait();
-        if (wr == 0) {
-            if (n1) issueA(u + 1, 1);
-            push(n1);
-        } else {
-            if (n2) issueA(u + 2, 0);
-            push(n2);
-        }
-        readB(buf, 1, bf1);
-        section_barrier();
-        quad(0, 1, af, bf1);
-        section_barrier();
-        // ---- phase 2: (A1, B1)
-        load_wait();
-        if (wr == 0) {
-            if (n2) issueA(u + 2, 0);
-        } else {
-            if (n2) issueB(u + 2, 0);
-        }
-        push(n2);
-        readA(buf, 1, af);
-        section_barrier();
-        quad(1, 1, af, bf1);
-        section_barrier();
-        // ---- phase 3: (A1, B0)
-        load_wait();
-        if (wr == 0) {
-            if (n2) issueB(u + 2, 0);
-        } else {
-            if (n2) issueB(u + 2, 1);
-        }
-        push(n2);
-        section_barrier();
-        quad(1, 0, af, bf0);
-        section_barrier();
-    }
-    if (wr == 0) section_barrier();               // G0 waits out G1's last MFMA section: equal barrier counts
-    vm_wait_n(0);
-
-    // consume the bias registers once, unconditionally (gemm4)
+    if (PROBE == 2) {
+        const bf16v8 z = {};
 #pragma unroll
-    for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(bias4[j].x), "v"(bias4[j].y), "v"(bias4[j].z), "v"(bias4[j].w));
-    bool fast = false;
-    if constexpr ((F & F_RES) != 0 && (F & ~(F_RES | F_STATS)) == 0) {
-        if (epi_res_fast_ok(d)) {
-            gemm_epilogue_res<TM, TN, F>(d, acc, m0, n0, wm0, wn0, lane, st_lds, 256, bias4);
-            fast = true;
-        }
+        for (int i = 0; i < 4; ++i) af[i][0] = af[i][1] = z;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) bf0[j][0] = bf0[j][1] = bf1[j][0] = bf1[j][1] = z;
     }
-    if (!fast) gemm_epilogue<TM, TN, F, true>(d, acc, m0, n0, wm0, wn0, lane, st_lds, 256, bias4);
+    auto sbar = [&]() {
+        if (PROBE != 4) section_barrier();
+    };
+    for (;;) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+        if (wr == 1) section_barrier();           // the stagger: G1 runs one section behind G0
+        for (int u = 0; u < nk; ++u) {
+            const int buf = u & 1;
+            const bool n1 = u + 1 < nk, n2 = u + 2 < nk;
+            // ---- phase 0: (A0, B0)
+            load_wait();
+            if (wr == 0 && n1) issueA(u + 1, 1);
+            push(wr == 0 && n1 ? 2 : 0);
+            readB(buf, 0, bf0);
+            readA(buf, 0, af);
+            sbar();
+            quad(0, 0, af, bf0);
+            sbar();
+            // ---- phase 1: (A0, B1)
+            load_wait();
+            if (wr == 1 && n2) {
+                issueA(u + 2, 0);
+                issueB(u + 2, 0);
+            }
+            push(wr == 1 && n2 ? 4 : 0);
+            readB(buf, 1, bf1);
+            sbar();
+            quad(0, 1, af, bf1);
+            sbar();
+            // ---- phase 2: (A1, B1)
+            load_wait();
+            if (n2) {
+                if (wr == 0) {
+                    issueA(u + 2, 0);
+                    issueB(u + 2, 0);
+                } else {
+                    issueB(u + 2, 1);
+                }
+            }
+            push(n2 ? (wr == 0 ? 4 : 2) : 0);
+            readA(buf, 1, af);
+            sbar();
+            quad(1, 1, af, bf1);
+            sbar();
+            // ---- phase 3: (A1, B0)
+            load_wait();
+            if (n2) {
+                if (wr == 0) issueB(u + 2, 1);
+                else issueA(u + 2, 1);
+            }
+            push(n2 ? 2 : 0);
+            sbar();
+            quad(1, 0, af, bf0);
+            sbar();
+        }
+        if (wr == 0) section_barrier();           // G0 waits out G1's last MFMA section: equal barrier counts
+        // every slot's last fragment reads have retired (lgkmcnt(0) before the barriers above)
+        const int next = tile + (int)gridDim.x;
+        const int64_t m0_done = m0;
+        const int n0_done = n0;
+        float bnext = 0.f;
+        if (PERSIST && next < ntiles) {
+            setup(next);
+            bnext = bias_load();                  // (before the DMA: its wait then needs no glds retired)
+            prologue();                           // the next tile's loads overlap this tile's epilogue
+        } else {
+            vm_wait_n(0);
+        }
+        float4 bias4[TN];
+        {
+            const float* bl = bias_lds + 256 * bsel + wn0 + 4 * (lane >> 4);
+#pragma unroll
+            for (int j = 0; j < TN; ++j) bias4[j] = *reinterpret_cast<const float4*>(bl + 16 * j);
+        }
+        bool fast = false;
+        if constexpr ((F & F_RES) != 0 && (F & ~(F_RES | F_STATS)) == 0) {
+            if (epi_res_fast_ok(d)) {
+                gemm_epilogue_res<TM, TN, F>(d, acc, m0_done, n0_done, wm0, wn0, lane, st_lds, 256, bias4);
+                fast = true;
+            }
+        }
+        if (!fast) gemm_epilogue<TM, TN, F, true>(d, acc, m0_done, n0_done, wm0, wn0, lane, st_lds, 256, bias4);
+        if (!PERSIST || next >= ntiles) break;
+        tile = next;
+        // the epilogue's stores sit behind the staged K-tiles on the VM counter: drain all (K-tile 1 included);
+        // stage the next bias; publish K-tile 0 and the bias
+        vm_wait_n(0);
+        hist[0] = hist[1] = hist[2] = hist[3] = 0;
+        bsel ^= 1;
+        if (tid < 256) bias_lds[256 * bsel + tid] = bnext;
+        section_barrier();
+    }
 }
 
-template <unsigned F>
+template <unsigned F, int PROBE = 0>
 static void launch5f(const GemmDesc& d, hipStream_t s) {
     const int64_t M = (int64_t)d.nb * d.H_out * d.W;
     const int64_t tiles = ((M + 255) / 256) * ((d.N + 255) / 256);
+    int64_t grid = tiles;
+    if constexpr ((F & (F_RES | F_STATS)) == 0) {   // persistent: the resident blocks (one per CU), a multiple of 8
+        static int resident = 0;
+        if (resident == 0) {
+            int per_cu = 0, cus = 0, dev = 0;
+            (void)hipGetDevice(&dev);
+            (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+            (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, gemm5_kernel<F, PROBE>, 512, 0);
+            resident = per_cu > 0 && cus > 0 ? per_cu * cus / 8 * 8 : -1;
+        }
+        if (resident >= 8 && resident < tiles) grid = resident;
+    }
     KScope ks(s);
     if (ks.on()) {
         double fl, by;
         gemm_work(d, 1, fl, by);
         ks.begin(klabel("gemm5_kernel<%u>", F), fl, by);
     }
-    hipLaunchKernelGGL((gemm5_kernel<F>), dim3((unsigned)tiles), dim3(512), 0, s, with_fastdiv(d));
+    hipLaunchKernelGGL((gemm5_kernel<F, PROBE>), dim3((unsigned)grid), dim3(512), 0, s, with_fastdiv(d));
 }
 
 int gemm5_launch(const GemmDesc& d, hipStream_t s) {
@@ -296,5 +370,17 @@ int gemm5_launch(const GemmDesc& d, hipStream_t s) {
     }
     return (int)hipGetLastError();
 }
+
+#ifdef ATHD_KBENCH
+int gemm5_probe_launch(const GemmDesc& d, hipStream_t s, int probe) {
+    if (epi_flags(d) != F_CBF16) return -1;
+    if (probe == 1) launch5f<F_CBF16, 1>(d, s);
+    else if (probe == 2) launch5f<F_CBF16, 2>(d, s);
+    else if (probe == 3) launch5f<F_CBF16, 3>(d, s);
+    else if (probe == 4) launch5f<F_CBF16, 4>(d, s);
+    else return -1;
+    return (int)hipGetLastError();
+}
+#endif
 
 }  // namespace athd

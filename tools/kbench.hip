@@ -12,6 +12,7 @@ int gemm2_launch(const GemmDesc& d, hipStream_t s);
 int gemm3_launch(const GemmDesc& d, hipStream_t s, int variant);
 int gemm4_launch(const GemmDesc& d, hipStream_t s);
 int gemm5_launch(const GemmDesc& d, hipStream_t s);
+int gemm5_probe_launch(const GemmDesc& d, hipStream_t s, int probe);
 }
 
 extern "C" {
@@ -25,6 +26,7 @@ int kb_gemm(int variant, const void* A, int a_bf16, const void* W, const float* 
     if (variant >= 40 && N % 256 != 0) return -1;   // gemm4 reads whole 256-row weight tiles; W here has N rows
     if (variant == 40) return gemm4_launch(d, (hipStream_t)stream);
     if (variant == 50) return gemm5_launch(d, (hipStream_t)stream);
+    if (variant > 50 && variant < 58) return gemm5_probe_launch(d, (hipStream_t)stream, variant - 50);
     if (variant == 41) { d.store = 0; return gemm4_launch(d, (hipStream_t)stream); }   // timing probe: no C stores
     if (variant == 42) { d.bias = nullptr; return gemm4_launch(d, (hipStream_t)stream); }   // timing probe: no bias
     if (variant == 2) return gemm2_launch(d, (hipStream_t)stream);

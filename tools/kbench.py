@@ -250,6 +250,21 @@ if __name__ == "__main__":
         gemm_case(256 * 32 * 259, 768, 192)
         gemm_case(M, 1536, 512)
         sys.exit(0)
+    if "g5var" in sys.argv[1:]:               # gemm5 schedule variants: 55 no sleep, 56 early + no sleep, 57 early
+        VARIANTS = (40, 50, 55, 56, 57)
+        for _ in range(2):
+            gemm_case(4096, 4096, 4096)
+            gemm_case(M, 512, 2048)
+            gemm_case(M, 1536, 512)
+            gemm_case(M, 2048, 512, act=1)
+            gemm_case(M, 512, 512)
+        sys.exit(0)
+    if "g5probe" in sys.argv[1:]:             # gemm5 ablations: 51 no staging, 52 no fragment reads, 53 no MFMA, 54 no barriers
+        VARIANTS = (40, 50, 51, 52, 53, 54)
+        gemm_case(4096, 4096, 4096)
+        gemm_case(M, 512, 2048)
+        gemm_case(M, 1536, 512)
+        sys.exit(0)
     if "g5" in sys.argv[1:]:
         VARIANTS = (40, 50)
         for _ in range(2):

@@ -76,11 +76,16 @@ def main():
     if calib and widths:
         rule = ("hbm_bytes = (c * FETCH_SIZE + WRITE_SIZE / w16) * 1024 per launch, c = sum_w share_w / fetch_factor_w "
                 "(load-width shares: " + a.widths + "; factors measured by tools/pmc_calib.hip: " + a.calib + ")")
+    elif calib:
+        rule = ("hbm_bytes = (c * FETCH_SIZE + WRITE_SIZE / w16) * 1024 per launch, c = 1 / the FETCH_SIZE factor "
+                "measured by tools/pmc_calib.hip (" + a.calib + "), the same at every access width")
     else:
         rule = ("hbm_bytes = (c * FETCH_SIZE + WRITE_SIZE) * 1024 per launch; c = 2 for 16-B/lane read streams "
                 "(gfx950 FETCH_SIZE halving, kernels " + ", ".join(WIDE_READS) + "), else 1")
     out = {"batch": a.batch, "dtype": a.dtype, "correction": rule, "calibration": calib and
            {"fetch": calib["fetch"], "write": calib["write"]}, "kernels": {}}
+
+    uniform = calib and len(set(calib["fetch"].values())) == 1
 
     def fetch_corr(k):
         if calib and widths:
@@ -88,6 +93,8 @@ def main():
             wk = widths.get(base) or next((v for n, v in widths.items() if n.split("<", 1)[0] == base), None)
             if wk:
                 return sum(sh / calib["fetch"].get(w, 1.0) for w, sh in wk["byte_share"].items()), "calibrated"
+        if uniform:        # the measured factor is the same at every width: no per-kernel width mix needed
+            return 1.0 / next(iter(calib["fetch"].values())), "calibrated (same factor at 2/4/8/16 B per lane)"
         return (2 if k.startswith(WIDE_READS) else 1), "round-2 rule"
     wf = calib["write"].get("16", 1.0) if calib else 1.0
     for k in sorted(set(fe) | set(wr)):
