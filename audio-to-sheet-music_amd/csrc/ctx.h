@@ -178,7 +178,7 @@ struct athd_ctx {
     }
     float* up_key(const std::string& k) { return up_f32(W(k).v); }
     // Pack a [N][K] fp32 host matrix (row-major, k contiguous) into the compute dtype, Kp = roundup(K, 64).  The
-    // allocation holds roundup(N, 256) rows, the extra ones zero: a 256-column GEMM tile (gemm4.hip) may read
+    // allocation holds roundup(N, 256) rows, the extra ones zero: a 256-column GEMM tile (gemm5.hip) may read
     // whole tiles of rows past N.
     GemmW up_gemm(const std::vector<float>& w, int N, int K, const std::vector<float>& bias) {
         GemmW g;

@@ -265,7 +265,7 @@ void dconv(Run& r, const EncW& e, void* x, int64_t nb, int64_t L, float* hbuf, u
         g.C = hbuf; g.H_out_total = (int)L; g.ldo = Hh; g.stats = st_h;
         r.gemm(g, "dconv.conv3");
         // bf16 mode: GELU(GN(h)) written once as bf16, so both 1x1 passes read half the bytes and run on the bf16
-        // MFMA GEMMs (gemm3 / gemm4) instead of converting fp32 A on load
+        // MFMA GEMMs (gemm3 / gemm5) instead of converting fp32 A on load
         const bool hb = r.actbf && hbuf_b && Hh % 8 == 0;
         {
             KSite site("dconv.gn_gelu");

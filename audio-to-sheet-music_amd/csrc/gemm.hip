@@ -282,8 +282,7 @@ int gemm2_launch(const GemmDesc& d, hipStream_t s);
 bool gemm3_supported(const GemmDesc& d);
 int gemm3_launch(const GemmDesc& d, hipStream_t s, int variant);
 int gemm3_ln_launch(const GemmDesc& d, hipStream_t s);
-bool gemm4_supported(const GemmDesc& d);
-int gemm4_launch(const GemmDesc& d, hipStream_t s);
+bool gemm5_supported(const GemmDesc& d);
 int gemm5_launch(const GemmDesc& d, hipStream_t s);
 
 int gemm_launch(const GemmDesc& d0, int mode, hipStream_t s) {
@@ -291,15 +290,10 @@ int gemm_launch(const GemmDesc& d0, int mode, hipStream_t s) {
     const GemmDesc d = with_fastdiv(d0);
     if (d.act == ACT_GLU && (d.N % 32 != 0)) return -2;
     if (d.ln_w) return mode == 1 ? gemm3_ln_launch(d, s) : -2;      // row-LayerNorm epilogue: gemm3 only
-    // bf16 activations, N a multiple of 256: 256x256 tile, half-tile staged pipeline (gemm4.hip).  (Measured on
-    // N = 192 / 384: slower than gemm3's 256x192 tiles, which waste no columns.)
-    // (gemm5: the same tile and epilogues with a staggered two-group K-loop, gemm5.hip; -DATHD_GEMM5 builds that
-    // dispatch for A/B measurement)
-#ifdef ATHD_GEMM5
-    if (mode == 1 && gemm4_supported(d) && d.N % 256 == 0) return gemm5_launch(d, s);
-#else
-    if (mode == 1 && gemm4_supported(d) && d.N % 256 == 0) return gemm4_launch(d, s);
-#endif
+    // bf16 activations, N a multiple of 256: 256x256 tile, staggered two-group K-loop (gemm5.hip; it replaced round
+    // 2's gemm4.hip, which tools/kbench still builds as the A/B baseline: kbench +6..16 % on the transformer shapes,
+    // equal at K = 2048).  (Measured on N = 192 / 384: slower than gemm3's 256x192 tiles, which waste no columns.)
+    if (mode == 1 && gemm5_supported(d) && d.N % 256 == 0) return gemm5_launch(d, s);
     // other N >= 192: 256x192 or 192x192 tile, 8 waves (gemm3.hip)
     // (K >= 384: 192x192 tiles with a 3-stage ring, two K-tiles in flight across each barrier; measured per call
     // site 2-20 % faster there.  Shorter K, e.g. the K=288 four-residue ConvT, keeps 256x192 x 2 stages.)

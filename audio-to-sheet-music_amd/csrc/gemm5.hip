@@ -335,6 +335,14 @@ __global__ __launch_bounds__(512) void gemm5_kernel(const GemmDesc d) {
     }
 }
 
+bool gemm5_supported(const GemmDesc& d) {
+    const int64_t a_elems = (d.a_bs >= 0 ? d.a_bs : (int64_t)d.H_in * d.W * d.a_ld) * d.nb;
+    // N % 64 == 0: the packed weights hold roundup(N, 256) rows (ctx.h up_gemm), the epilogue skips columns >= N
+    return d.a_bf16 && !d.a_norm && d.C_in % 8 == 0 && d.a_ld % 8 == 0 && d.a_cs == 1 && d.Kp % 64 == 0 &&
+           d.N % 64 == 0 && (int64_t)(d.N + 255) * d.Kp * 2 < (1LL << 31) && a_elems < (1LL << 31) &&
+           d.col_split % 4 == 0 && (d.act != ACT_GLU || d.N % 32 == 0);
+}
+
 template <unsigned F, int PROBE = 0>
 static void launch5f(const GemmDesc& d, hipStream_t s) {
     const int64_t M = (int64_t)d.nb * d.H_out * d.W;

@@ -36,7 +36,7 @@ void KScope::begin(const std::string& label0, double flops, double bytes) {
         label = site;
     }
     if (!p->only.empty() && p->only[0] != '@') {
-        // one kernel ("gemm4_kernel<129>") or one call site of it ("gemm4_kernel<129>@transformer.linear1")
+        // one kernel ("gemm5_kernel<129>") or one call site of it ("gemm5_kernel<129>@transformer.linear1")
         if (p->only != (p->only.find('@') != std::string::npos ? site : label0)) return;
         label = p->only;
     }
