@@ -783,7 +783,7 @@ int attn_launch(const AttnDesc& d, int mode, hipStream_t s) {
         const double fl = 4.0 * nh * d.Nq * d.Nk * 64;
         const double by = nh * 64 * (d.Nq * (d.q_bf16 ? 2 : 4) + d.Nk * ((d.k_bf16 ? 2 : 4) + (d.v_bf16 ? 2 : 4)) +
                                      d.Nq * (d.o_bf16 ? 2 : 4));
-        ks.begin(a32 ? std::string("attn32_kernel") : v2 ? std::string("attn_bf16_kernel") : klabel("attn_kernel<%d>", mode),
+        ks.begin(a32 ? std::string("attn32_kernel<3,2,true>") : v2 ? std::string("attn_bf16_kernel") : klabel("attn_kernel<%d>", mode),
                  fl, by);
     }
 #ifdef ATHD_KBENCH

@@ -264,7 +264,7 @@ static void dconv_small_t(void* x, float* h, int64_t nb, int64_t L, int dil, con
     const int64_t P = nb * L;
     const double px = (double)P;
     const double xb = (double)sizeof(TS);
-    const char* tn = sizeof(TS) == 2 ? "bf16" : "f32";
+    const char* tn = sizeof(TS) == 2 ? "unsignedshort" : "float";   // (rocprofv3 symbol spelling)
     {
         KScope ks(s);
         if (ks.on()) ks.begin(klabel("dconv_c3_kernel<%d,%s>", C, tn), 2.0 * px * H * 3 * C, px * (C * xb + H * 4));
@@ -273,13 +273,13 @@ static void dconv_small_t(void* x, float* h, int64_t nb, int64_t L, int dil, con
     }
     {
         KScope ks(s);
-        if (ks.on()) ks.begin(klabel("dconv_c1_stats_kernel<%d>", C), 2.0 * px * (H * H + 3 * H), px * H * 4);
+        if (ks.on()) ks.begin(klabel("dconv_c1_stats_kernel<%d,%s>", C, FAST ? "true" : "false"), 2.0 * px * (H * H + 3 * H), px * H * 4);
         hipLaunchKernelGGL((dconv_c1_stats_kernel<C, FAST>), dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, h, nb,
                            L, st_h, g1w, g1b, gram1, st_y);
     }
     {
         KScope ks(s);
-        if (ks.on()) ks.begin(klabel("dconv_c1_apply_kernel<%d,%s>", C, tn), 2.0 * px * 2 * C * H, px * (H * 4 + 2 * C * xb));
+        if (ks.on()) ks.begin(klabel("dconv_c1_apply_kernel<%d,%s,%s>", C, tn, FAST ? "true" : "false"), 2.0 * px * 2 * C * H, px * (H * 4 + 2 * C * xb));
         hipLaunchKernelGGL((dconv_c1_apply_kernel<C, TS, FAST>), dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s,
                            (TS*)x, h, nb, L, st_h, g1w, g1b, w1, b1, st_y, g2w, g2b, scale);
     }

@@ -660,7 +660,7 @@ int fdec_tail_launch(const DecLastDesc& d, hipStream_t s) {
         const double segs = d.NI / d.P;
         const double by = (double)d.NI * 2 * d.H * d.W * DL_C * eg + segs * std::min(d.H_skip2, 2 * d.H) * d.W * DL_C * es2 +
                           segs * 2 * d.H * d.W * 4 * es + (double)d.NI * d.H * d.W * 2 * 4;
-        ks.begin("fdec_tail_kernel", 0.0, by);
+        ks.begin(d.g_bf16 ? "fdec_tail_kernel<true>" : "fdec_tail_kernel<false>", 0.0, by);
     }
     if (d.g_bf16) hipLaunchKernelGGL(fdec_tail_kernel<true>, grid, dim3(256), 0, s, d, nreg);
     else hipLaunchKernelGGL(fdec_tail_kernel<false>, grid, dim3(256), 0, s, d, nreg);
@@ -687,7 +687,7 @@ int tdec_tail_launch(const DecLastDesc& d, hipStream_t s) {
         const double segs = d.NI / d.P;
         const double by = (double)d.NI * d.Hg * DL_C * eg + segs * d.H_skip2 * DL_C * es2 + segs * d.H_skip * 4 * es +
                           (double)d.NI * d.T * 2 * 4;
-        ks.begin("tdec_tail_kernel", 0.0, by);
+        ks.begin(d.g_bf16 ? "tdec_tail_kernel<true>" : "tdec_tail_kernel<false>", 0.0, by);
     }
     const dim3 grid((unsigned)((d.H + TL_IN - 1) / TL_IN), (unsigned)d.NI);
     if (d.g_bf16) hipLaunchKernelGGL(tdec_tail_kernel<true>, grid, dim3(TL_NT), 0, s, d);
@@ -706,7 +706,7 @@ int fdec_last_launch(const DecLastDesc& d, hipStream_t s) {
         const double eb = d.in_bf16 ? 2 : 4;
         const double by = (double)d.NI * d.H * d.W * DL_C * eb + (double)(d.NI / d.P) * 2 * d.H * d.W * 4 * (d.skip_bf16 ? 2 : 4) +
                           (double)d.NI * d.H * d.W * 2 * 4;
-        ks.begin("fdec_last_kernel", 0.0, by);
+        ks.begin(d.in_bf16 ? "fdec_last_kernel<unsignedshort>" : "fdec_last_kernel<float>", 0.0, by);
     }
     if (d.in_bf16) hipLaunchKernelGGL(fdec_last_kernel<bf16_t>, grid, dim3(256), 0, s, d);
     else hipLaunchKernelGGL(fdec_last_kernel<float>, grid, dim3(256), 0, s, d);
@@ -721,7 +721,7 @@ int tdec_last_launch(const DecLastDesc& d, hipStream_t s) {
         const double eb = d.in_bf16 ? 2 : 4;
         const double by = (double)d.NI * d.H * DL_C * eb + (double)(d.NI / d.P) * d.H_skip * 4 * (d.skip_bf16 ? 2 : 4) +
                           (double)d.NI * d.T * 2 * 4;
-        ks.begin(exact ? "tdec_last_kernel" : "tdec_last_generic_kernel", 0.0, by);
+        ks.begin(klabel("%s<%s>", exact ? "tdec_last_kernel" : "tdec_last_generic_kernel", d.in_bf16 ? "unsignedshort" : "float"), 0.0, by);
     }
     if (exact) {
         const dim3 grid((unsigned)((d.H + TL_IN - 1) / TL_IN), (unsigned)d.NI);

@@ -751,7 +751,7 @@ int fenc_row_launch(const FencRowDesc& d, int cin, int c, hipStream_t s) {
         const double H = c / 8.0;
         const double macs = rows * T * (c * 8.0 * cin + 2 * (H * 3 * c + 2.0 * c * H) + 2.0 * c * c);
         const double in_b = cin == 4 ? (double)d.B * d.Fin * T * 4 * 4 : (double)d.B * d.Fin * T * cin * 2;
-        ks.begin(cin == 4 ? "fenc_row0_kernel" : klabel("fenc_row_kernel<%d,%d>", cin, c), 2.0 * macs, in_b + rows * T * c * 2);
+        ks.begin(cin == 4 ? "fenc_row0_kernel" : "fenc_row_kernel<48,96,12,true>", 2.0 * macs, in_b + rows * T * c * 2);
     }
     if (cin == 4) hipLaunchKernelGGL(fenc_row0_kernel, grid, dim3(FR_NT), 0, s, d);
     else hipLaunchKernelGGL((fenc_row_kernel<48, 96, 12, true>), grid, dim3(12 * 64), 0, s, d);

@@ -99,7 +99,7 @@ inline void gemm_work(const GemmDesc& d, int mode, double& flops, double& bytes)
     const double nout = d.act == ACT_GLU ? d.N / 2 : d.N;
     bytes = (double)d.nb * d.H_in * d.W * d.C_in * (d.a_bf16 ? 2 : 4) + (double)d.N * d.K * (mode == 1 ? 2 : 4);
     if (d.store) bytes += M * nout * (d.c_bf16 ? 2 : 4) * (d.pfold > 1 ? d.pfold : 1);
-    if (d.res) bytes += M * nout * 4 / (d.res_div > 1 ? d.res_div : 1);
+    if (d.res) bytes += M * nout * (d.res_bf16 ? 2 : 4) / (d.res_div > 1 ? d.res_div : 1);
     if (d.pbias) bytes += (double)d.nb * (d.pfold > 1 ? d.pfold : 1) * d.N * 4;
 }
 

@@ -363,7 +363,7 @@ static void launch5f(const GemmDesc& d, hipStream_t s) {
     if (ks.on()) {
         double fl, by;
         gemm_work(d, 1, fl, by);
-        ks.begin(klabel("gemm5_kernel<%u>", F), fl, by);
+        ks.begin(klabel("gemm5_kernel<%u,%d>", F, PROBE), fl, by);
     }
     hipLaunchKernelGGL((gemm5_kernel<F, PROBE>), dim3((unsigned)grid), dim3(512), 0, s, with_fastdiv(d));
 }

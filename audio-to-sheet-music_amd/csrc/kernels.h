@@ -24,19 +24,14 @@ void tconv0_launch(const float* wav, int nb, int64_t T, int64_t Lo, const float*
 // tw64 != nullptr (f32 parity mode): the FFT runs in double (spectral.hip)
 void stft_launch(const float* wav, int nb, int64_t T, const PadPlan& pp, int Tspec, const float2* tw,
                  const double2* tw64, const float* win, float* specT, double* stats, hipStream_t s);
-// fo: FO^T [item][t][row][2] (dec_merge_proj_kernel output); specT as above
-void istft_frames_launch(const float* fo, int NI, int Tspec, int P, const float* specT, const float2* tw,
-                         const double2* tw64, const float* win, float* frames, hipStream_t s);
-// fused: mask + inverse FFT + overlap-add + envelope + time branch (replaces istft_frames + combine); part:
+// fo: FO^T [item][t][row][2] (fdec_tail_kernel output); specT as above
+// fused: mask + inverse FFT + overlap-add + envelope + time branch (round 1's frame tensor is gone); part:
 // istft_ola_part_floats(NI, Tspec) floats of boundary partial sums
 void istft_ola_launch(const float* fo, int NI, int Tspec, int P, int64_t T, const float* spec, const float2* tw,
                       const double2* tw64, const float* win, const float* win2, const float* xt2, const float* tnorm,
                       float* out, float* part, hipStream_t s);
 int istft_ola_nwg(int Tspec);
 inline int64_t istft_ola_part_floats(int64_t NI, int Tspec) { return NI * istft_ola_nwg(Tspec) * 2 * 3 * 1024 * 2; }
-// out[item][c][n] = OLA(frames)/env + xt2[item][n][c] * stdt[b] + meant[b]   (xt2: tdec_last_launch output)
-void combine_launch(const float* frames, int NI, int Tspec, int64_t T, const float* win2, const float* xt2,
-                    const float* tnorm, int P, float* out, hipStream_t s);
 
 // norm.hip
 // per-batch {sum, sumsq} (double) of x[b][0..n)

@@ -11,9 +11,9 @@
 // iSTFT: per (item, frame) the decoder's freq map is resized 2048 rows (PyTorch fp32 bilinear index math),
 // passed through sigmoid, and the masking formula of ATHTDemucs_v2.py:303-309 is applied to both channels;
 // the two Hermitian spectra are packed into one complex inverse FFT (x_L = Re, x_R = Im), scaled 1/64 and
-// windowed into a frame buffer.  The combine kernel then gathers the <=4 overlapping frames per output sample,
-// divides by the window envelope of ALL le+4 frames (torch.istft), and adds the denormalised time branch after
-// its 1x1 output conv (ATHTDemucs_v2.py:314-324).
+// windowed; the overlap-add of the <=4 frames per output sample runs in registers, divided by the window envelope
+// of ALL le+4 frames (torch.istft), plus the denormalised time branch after its 1x1 output conv
+// (ATHTDemucs_v2.py:314-324): istft_ola_kernel below, no frame tensor in HBM.
 #include <cstdlib>
 
 #include "common.h"
@@ -195,83 +195,13 @@ __global__ __launch_bounds__(256) void stft_kernel(const float* __restrict__ wav
 void stft_launch(const float* wav, int nb, int64_t T, const PadPlan& pp, int Tspec, const float2* tw,
                  const double2* tw64, const float* win, float* specT, double* stats, hipStream_t s) {
     KScope ks(s);
-    if (ks.on()) ks.begin("stft_kernel", 0.0, (double)nb * 2 * T * 4 + (double)nb * 2048 * Tspec * 4 * 4);
+    if (ks.on()) ks.begin(tw64 ? "stft_kernel<double,HIP_vector_type<double,2>>" : "stft_kernel<float,HIP_vector_type<float,2>>", 0.0, (double)nb * 2 * T * 4 + (double)nb * 2048 * Tspec * 4 * 4);
     if (tw64)
         hipLaunchKernelGGL((stft_kernel<double, double2>), dim3(Tspec, nb), dim3(256), 0, s, wav, T, pp, Tspec, tw64, win,
                            specT, stats);
     else
         hipLaunchKernelGGL((stft_kernel<float, float2>), dim3(Tspec, nb), dim3(256), 0, s, wav, T, pp, Tspec, tw, win,
                            specT, stats);
-}
-
-// ---------------------------------------------------------------------------------------------------------
-template <typename R, typename TW>
-__global__ __launch_bounds__(256) void istft_frames_kernel(const float* __restrict__ fo, int Tspec, int P,
-                                                           const float* __restrict__ specT,
-                                                           const TW* __restrict__ tw,
-                                                           const float* __restrict__ win,
-                                                           float* __restrict__ frames) {
-    __shared__ cpx buf[FPAD];
-    const int t = blockIdx.x;
-    const int64_t item = blockIdx.y;
-    const int64_t b = item / P;
-    const float* F0 = fo + (item * (int64_t)Tspec + t) * Tspec * 2;   // FO^T: [item][t][row][2]
-    const float* S = specT + (b * Tspec + t) * 2048LL * 4;             // [b][t][k][4]
-    for (int k = threadIdx.x; k < 2048; k += 256) {
-        const LinIdx li = lin_index(k, Tspec, 2048);
-        const float* r0 = F0 + (int64_t)li.i0 * 2;
-        const float* r1 = F0 + (int64_t)li.i1 * 2;
-        const float xd0 = li.l0 * r0[0] + li.l1 * r1[0];
-        const float xd1 = li.l0 * r0[1] + li.l1 * r1[1];
-        const float m0 = sigmoidf_(xd0), m1 = sigmoidf_(xd1);
-        const float4 z = *reinterpret_cast<const float4*>(S + (int64_t)k * 4);
-        // masked_z = (mag*mask) * (z / (mag + 1e-8)); ch0: z_L with mag = Re z_L; ch1: z_R with mag = Im z_L
-        const float ms0 = z.x * m0, ms1 = z.y * m1;
-        const float d0 = z.x + 1e-8f, d1 = z.y + 1e-8f;
-        cpx X0 = {ms0 * (z.x / d0), ms0 * (z.y / d0)};
-        cpx X1 = {ms1 * (z.z / d1), ms1 * (z.w / d1)};
-        if (k == 0) { X0.y = 0.f; X1.y = 0.f; }          // c2r ignores the imaginary part of the DC bin
-        // Z = X0 + i X1 (k), and its Hermitian mirror at N-k: conj(X0) + i conj(X1); conj() for the inverse
-        // (ifft(Z) = conj(fft(conj(Z))))
-        cpx Zk = {X0.x - X1.y, X0.y + X1.x};
-        buf[pidx(k)] = {Zk.x, -Zk.y};
-        if (k > 0) {
-            cpx Zm = {X0.x + X1.y, -X0.y + X1.x};
-            buf[pidx(NFFT - k)] = {Zm.x, -Zm.y};
-        }
-    }
-    if (threadIdx.x == 0) buf[pidx(2048)] = {0.f, 0.f};    // Nyquist bin padded with zero (HTDemucs._ispec)
-    __syncthreads();
-    cx<R> v[16];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const cpx z = buf[pidx(threadIdx.x + 256 * r)];
-        v[r] = {(R)z.x, (R)z.y};
-    }
-    __syncthreads();
-    fft4096(v, buf, tw, (int)threadIdx.x);
-    float* o = frames + (item * Tspec + t) * 2LL * NFFT;
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-        const int n = threadIdx.x + 256 * q;
-        const float w = win[n] * (1.f / 64.f);
-        o[n] = (float)v[vq(q)].x * w;             // conj(fft(conj Z)) -> real part unchanged
-        o[NFFT + n] = -(float)v[vq(q)].y * w;     // imag part negated
-    }
-}
-
-void istft_frames_launch(const float* fo, int NI, int Tspec, int P, const float* spec, const float2* tw,
-                         const double2* tw64, const float* win, float* frames, hipStream_t s) {
-    KScope ks(s);
-    if (ks.on())
-        ks.begin("istft_frames_kernel", 0.0, (double)NI * Tspec * Tspec * 2 * 4 + (double)(NI / P) * 2048 * Tspec * 4 * 4 +
-                                                 (double)NI * Tspec * 2 * 4096 * 4);
-    if (tw64)
-        hipLaunchKernelGGL((istft_frames_kernel<double, double2>), dim3(Tspec, NI), dim3(256), 0, s, fo, Tspec, P, spec,
-                           tw64, win, frames);
-    else
-        hipLaunchKernelGGL((istft_frames_kernel<float, float2>), dim3(Tspec, NI), dim3(256), 0, s, fo, Tspec, P, spec, tw,
-                           win, frames);
 }
 
 // ---------------------------------------------------------------------------------------------------------
@@ -283,14 +213,14 @@ void istft_frames_launch(const float* fo, int NI, int Tspec, int P, const float*
 // i.e. offsets o = j + 256 (q' & 3) of the frame's hop h = q' >> 2: every thread owns the same 4 offsets of every hop
 // block, so the overlap-add runs in registers: acc[h] = block f + h, frame f adds its hop h to acc[h] (ascending f,
 // from 0.0f), then block f has all of this workgroup's frames and the ring shifts by one block.
-// Workgroup k of an item runs the IO_G real frames t = IO_G k .. (one inverse FFT per frame, as istft_frames did).
+// Workgroup k of an item runs the IO_G real frames t = IO_G k .. (one inverse FFT per frame).
 // Its blocks whose frames all lie in its range are final: divided by the window envelope, the denormalised time
 // branch added, stored (4 coalesced samples x 2 channels per thread).  The 3 blocks at each end of its range also
 // take frames of the neighbouring workgroup: their partial sums go to `part` (head: first 3 blocks, tail: the 3
 // after the last frame) and istft_fix_kernel adds tail(k-1) + head(k) and finishes them.  Workgroup 0's head and
 // the last workgroup's tail only border zero frames and are final in place.
 // Traffic per item: FO + the segment's spectrum (shared by its prompts through L2) + xt2 + out + 48 KB of partials
-// per workgroup, vs a 8.5 MB frame tensor written and read back per item by istft_frames + combine.
+// per workgroup, vs round 1's 8.5 MB frame tensor written and read back per item.
 constexpr int IO_G = 32;
 
 // Finish hop block B: out = y / env + denormalised time branch, for the samples of [0, T).  Every block holding an
@@ -408,7 +338,7 @@ __global__ __launch_bounds__(256, MINW) void istft_ola_kernel(const float* __res
         // slots) is recomputed each frame instead of being hoisted out of the loop and spilled
         int j;
         asm volatile("v_mov_b32 %0, %1" : "=v"(j) : "v"((int)threadIdx.x));
-        // ---- masked, Hermitian-packed spectrum of frame t into LDS (istft_frames_kernel's arithmetic) ----
+        // ---- masked, Hermitian-packed spectrum of frame t into LDS  ----
         const float* F0 = fo + (item * (int64_t)Tspec + t) * Tspec * 2;
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
@@ -514,7 +444,8 @@ void istft_ola_launch(const float* fo, int NI, int Tspec, int P, int64_t T, cons
         const dim3 grid((unsigned)(8 * ((units + 7) / 8) * P));
         KScope ks(s);
         if (ks.on())
-            ks.begin("istft_ola_kernel", 0.0,
+            ks.begin(tw64 ? "istft_ola_kernel<double,HIP_vector_type<double,2>,3,true>"
+                          : "istft_ola_kernel<float,HIP_vector_type<float,2>,3,false>", 0.0,
                      (double)NI * Tspec * Tspec * 2 * 4 + (double)(NI / P) * 2048 * Tspec * 4 * 4 + (double)NI * T * 2 * 4 +
                          (double)NI * 2 * T * 4);
         // <3 waves per SIMD, no prefetch>: 1512 vs 1781 us for <2, prefetch> (round 2 measurement)
@@ -533,47 +464,5 @@ void istft_ola_launch(const float* fo, int NI, int Tspec, int P, int64_t T, cons
     }
 }
 
-// out[item][c][n] = OLA(frames)/env + xt2[item][n][c] * stdt[b] + meant[b]   (ATHTDemucs_v2.py:310-324; xt2 is
-// time_out of the time decoder, dec_last.hip)
-__global__ __launch_bounds__(256) void combine_kernel(const float* __restrict__ frames, int Tspec, int64_t T,
-                                                      const float* __restrict__ win2, const float* __restrict__ xt2,
-                                                      const float* __restrict__ tnorm, int P,
-                                                      float* __restrict__ out) {
-    const int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    const int64_t item = blockIdx.y;
-    if (n >= T) return;
-    const int64_t b = item / P;
-    const int64_t q = n + 3584;                      // OLA index: 1536 (_ispec slice) + 2048 (istft centre)
-    const int nfr = Tspec + 4;
-    int f_lo;                                        // first frame f' with 1024 f' + 4096 > q
-    if (q - NFFT + 1 <= 0) f_lo = 0;
-    else f_lo = (int)((q - NFFT + 1 + HOP - 1) / HOP);
-    int f_hi = (int)(q / HOP);
-    if (f_hi > nfr - 1) f_hi = nfr - 1;
-    float env = 0.f, y0 = 0.f, y1 = 0.f;
-    for (int f = f_lo; f <= f_hi; ++f) {
-        const int j = (int)(q - (int64_t)f * HOP);
-        env += win2[j];
-        const int t = f - 2;
-        if (t >= 0 && t < Tspec) {
-            const float* fr = frames + (item * Tspec + t) * 2LL * NFFT;
-            y0 += fr[j];
-            y1 += fr[NFFT + j];
-        }
-    }
-    const float2 x2 = *reinterpret_cast<const float2*>(xt2 + (item * T + n) * 2);
-    const float mean = tnorm[2 * b], stdv = tnorm[2 * b + 1];
-    out[(item * 2 + 0) * T + n] = y0 / env + (x2.x * stdv + mean);
-    out[(item * 2 + 1) * T + n] = y1 / env + (x2.y * stdv + mean);
-}
-
-void combine_launch(const float* frames, int NI, int Tspec, int64_t T, const float* win2, const float* xt2,
-                    const float* tnorm, int P, float* out, hipStream_t s) {
-    dim3 grid((unsigned)((T + 255) / 256), NI);
-    KScope ks(s);
-    if (ks.on())
-        ks.begin("combine_kernel", 0.0, (double)NI * Tspec * 2 * 4096 * 4 + (double)NI * T * 2 * 4 + (double)NI * 2 * T * 4);
-    hipLaunchKernelGGL(combine_kernel, grid, dim3(256), 0, s, frames, Tspec, T, win2, xt2, tnorm, P, out);
-}
 
 }  // namespace athd
