@@ -536,14 +536,22 @@ __global__ __launch_bounds__(TL_NT) void tdec_tail_kernel(const DecLastDesc d) {
     constexpr int GS_BYTES = TtRow<BF>::BYTES > TL_NT * TZ_LD * 4 ? TtRow<BF>::BYTES : TL_NT * TZ_LD * 4;
     __shared__ __attribute__((aligned(16))) char gsm[GS_BYTES];
     float* zb = reinterpret_cast<float*>(gsm);
-    const int64_t item = blockIdx.y;
-    const int64_t seg = item / d.P;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    // 1-D block index -> (segment region g = (seg, bx), prompt), as fdec_tail: XCD x runs regions g = x, x + 8, ...
+    // with the P prompts of each back to back, so the skip rows of a region are read once into that XCD's L2 and
+    // served to the other P - 1 prompts from it
     const int Lin = d.H;
+    const int nbx = (Lin + TL_IN - 1) / TL_IN;
+    const int L8 = blockIdx.x, x8 = L8 & 7, jj = L8 >> 3;
+    const int g = 8 * (jj / d.P) + x8, pr = jj % d.P;
+    if (g >= nbx * (d.NI / d.P)) return;                   // block-uniform
+    const int64_t seg = g / nbx;
+    const int bxi = g % nbx;
+    const int64_t item = seg * d.P + pr;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     float mean, rstd;
     gn_params(d.stats, item, d.gn_count, mean, rstd);
     int r0;
-    const int nr = tt_span(blockIdx.x, Lin, d.Hg, r0);
+    const int nr = tt_span(bxi, Lin, d.Hg, r0);
     const int64_t gb = (item * d.Hg + r0) * (int64_t)DL_C;
     for (int i = tid; i < nr * (DL_C / 8); i += TL_NT) {
         const int rr = i / (DL_C / 8), q = i % (DL_C / 8);
@@ -573,7 +581,7 @@ __global__ __launch_bounds__(TL_NT) void tdec_tail_kernel(const DecLastDesc d) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const int r = 64 * k + 16 * wave + p;
-        const int u = blockIdx.x * TL_IN - 1 + r;
+        const int u = bxi * TL_IN - 1 + r;
         float x[12];
 #pragma unroll
         for (int s = 0; s < 12; ++s) x[s] = 0.f;      // x = 0 outside [0, Lin): zero taps
@@ -602,7 +610,7 @@ __global__ __launch_bounds__(TL_NT) void tdec_tail_kernel(const DecLastDesc d) {
     for (int k = 0; k < 4; ++k)
         *reinterpret_cast<float4*>(zb + (64 * k + 16 * wave + p) * TZ_LD + 4 * cg) = make_float4(z[k][0], z[k][1], z[k][2], z[k][3]);
     __syncthreads();
-    const int u = blockIdx.x * TL_IN - 1 + tid;
+    const int u = bxi * TL_IN - 1 + tid;
     if (!(tid > 0 && tid < TL_NT - 1 && u < Lin)) return;
     const float* F = d.fold;
     const float* cb = F + 16 * DL_C;             // P b (2), then tb (2), then 0.1 P (8)
@@ -689,7 +697,9 @@ int tdec_tail_launch(const DecLastDesc& d, hipStream_t s) {
                           (double)d.NI * d.T * 2 * 4;
         ks.begin(d.g_bf16 ? "tdec_tail_kernel<true>" : "tdec_tail_kernel<false>", 0.0, by);
     }
-    const dim3 grid((unsigned)((d.H + TL_IN - 1) / TL_IN), (unsigned)d.NI);
+    // 8 XCD lanes x ceil(regions / 8) x P prompts (tdec_tail_kernel's block order); spare blocks return at once
+    const int64_t regions = (int64_t)((d.H + TL_IN - 1) / TL_IN) * (d.NI / d.P);
+    const dim3 grid((unsigned)(8 * ((regions + 7) / 8) * d.P));
     if (d.g_bf16) hipLaunchKernelGGL(tdec_tail_kernel<true>, grid, dim3(TL_NT), 0, s, d);
     else hipLaunchKernelGGL(tdec_tail_kernel<false>, grid, dim3(TL_NT), 0, s, d);
     return (int)hipGetLastError();

@@ -732,6 +732,10 @@ __global__ __launch_bounds__(FR_NT, 4) void fenc_row0_kernel(const FencRowDesc d
         bf16_t* dst = d.out + ((int64_t)b * d.Fout + f) * (int64_t)T * C;
         for (int i = tid; i < T * C / 8; i += FR_NT)
             reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(ob)[i];
+        if (d.out4) {            // the decoder's level-3 skip reads channels 0..3 only: a compact copy
+            uint2* d4 = reinterpret_cast<uint2*>(d.out4 + ((int64_t)b * d.Fout + f) * (int64_t)T * 4);
+            for (int m = tid; m < T; m += FR_NT) d4[m] = *reinterpret_cast<const uint2*>(&ob[m * C]);
+        }
     }
 }
 

@@ -61,6 +61,8 @@ struct Bufs {
     // encoder activations: f32 in parity mode, bf16 in throughput mode (Bufs::ea bytes per element)
     void* saved[4];
     void* saved_t[4];
+    void* sk4;                        // channels 0..3 of saved[0] / saved_t[0] ([rows][4]): the decoders' level-3 skip
+    void* sk4t;
     void* ybuf;
     void* ybuf_t;                     // the time encoder's level buffers (it runs on the second stream)
     float* hbuf_t;
@@ -113,6 +115,8 @@ size_t plan(Arena& ar, const Dims& d, Bufs& b, bool actbf) {
         ymax_t = std::max(ymax_t, rows_t * C);
         hmax_t = std::max(hmax_t, rows_t * (C / 8));
     }
+    b.sk4 = act(B * d.F[1] * Ts * 4);
+    b.sk4t = act(B * d.L[1] * 4);
     b.ybuf_t = act(ymax_t);
     b.hbuf_t = ar.take<float>(hmax_t);
     b.hbuf_b_t = ab == 2 ? ar.take<uint16_t>(hmax_t) : nullptr;
@@ -349,6 +353,7 @@ void encode(Run& r, const Dims& d, const Bufs& b, const float* wav) {
             fr.wr = (const uint16_t*)e.rewrite.w; fr.wr_ld = e.rewrite.Kp; fr.br = e.rewrite.bias;
             fr.row_add = i == 0 ? c->femb : nullptr;
             fr.out = (uint16_t*)b.saved[i];
+            fr.out4 = i == 0 ? (uint16_t*)b.sk4 : nullptr;
             KSite site("fenc_row");
             r.check(fenc_row_launch(fr, e.cin, C, r.s), "fenc_row");
         } else {
@@ -370,6 +375,7 @@ void encode(Run& r, const Dims& d, const Bufs& b, const float* wav) {
         gr.Wp = e.rewrite.w; gr.N = 2 * C; gr.K = C; gr.Kp = e.rewrite.Kp; gr.bias = e.rewrite.bias;
         gr.C = b.saved[i]; gr.c_bf16 = eab; gr.H_out_total = Fo; gr.ldo = C; gr.act = ACT_GLU;
         gr.row_add = i == 0 ? c->femb : nullptr;    // + freq_emb_scale * freq_emb(frs) (ATHTDemucs_v2.py:212-215)
+        gr.c4 = i == 0 ? b.sk4 : nullptr;
         r.gemm(gr, "fenc.rewrite");
         }
 
@@ -395,6 +401,7 @@ void encode(Run& r, const Dims& d, const Bufs& b, const float* wav) {
         grt.A = b.ybuf_t; grt.a_bf16 = eab; grt.nb = (int)B; grt.H_in = (int)Lo; grt.W = 1; grt.C_in = C; grt.a_ld = C; grt.H_out = (int)Lo;
         grt.Wp = et.rewrite.w; grt.N = 2 * C; grt.K = C; grt.Kp = et.rewrite.Kp; grt.bias = et.rewrite.bias;
         grt.C = b.saved_t[i]; grt.c_bf16 = eab; grt.H_out_total = (int)Lo; grt.ldo = C; grt.act = ACT_GLU;
+        grt.c4 = i == 0 ? b.sk4t : nullptr;
         r.gemm(grt, "tenc.rewrite");
         r.s = s_enc;
     }
@@ -682,7 +689,9 @@ void decode_chunk(Run& r, const Dims& d, const Bufs& b, int64_t s0, int64_t Bc, 
             dl.g = b.G; dl.g_bf16 = ab; dl.stats = sti; dl.gn_count = 4 * Ts * Ts * w.cout; dl.gn_w = w.gnw; dl.gn_b = w.gnb;
             dl.fast_gelu = ab; dl.skip2 = sv[1]; dl.skip2_bf16 = ab; dl.H_skip2 = skH[1]; dl.C_skip2 = skC[1];
             dl.NI = NI; dl.P = P; dl.H = (int)Ts; dl.W = (int)Ts;
-            dl.fold = c->flast; dl.skip = sv[0]; dl.skip_bf16 = ab; dl.H_skip = skH[2]; dl.C_skip = skC[2];
+            // level-3 skip = saved[0][:, :4]: the compact copy the encoder wrote (4 channels per row)
+            dl.fold = c->flast; dl.skip = eoff(b.sk4, s0 * 512 * Ts * 4, ea); dl.skip_bf16 = ab; dl.H_skip = skH[2];
+            dl.C_skip = 4;
             dl.out = b.FO;
             r.check(fdec_tail_launch(dl, r.s), "fdec_tail");
         }
@@ -717,7 +726,8 @@ void decode_chunk(Run& r, const Dims& d, const Bufs& b, int64_t s0, int64_t Bc, 
                 dl.gn_w = w.gnw; dl.gn_b = w.gnb; dl.fast_gelu = ab;
                 dl.skip2 = svt[1]; dl.skip2_bf16 = ab; dl.H_skip2 = (int)d.L[2]; dl.C_skip2 = ENC_CH[1];
                 dl.NI = NI; dl.P = P; dl.H = (int)target; dl.T = d.T;
-                dl.fold = c->tlast; dl.skip = svt[0]; dl.skip_bf16 = ab; dl.H_skip = (int)d.L[1]; dl.C_skip = ENC_CH[0];
+                dl.fold = c->tlast; dl.skip = eoff(b.sk4t, s0 * d.L[1] * 4, ea); dl.skip_bf16 = ab; dl.H_skip = (int)d.L[1];
+                dl.C_skip = 4;
                 dl.out = b.Dt;
                 if (tdec_tail_supported(dl)) {
                     KStage kst3("tdec3");
@@ -735,7 +745,8 @@ void decode_chunk(Run& r, const Dims& d, const Bufs& b, int64_t s0, int64_t Bc, 
             KStage kst("tdec3");
             DecLastDesc dl;
             dl.in = b.Dt; dl.in_bf16 = ab; dl.NI = NI; dl.P = P; dl.H = (int)Lin; dl.T = d.T;
-            dl.fold = c->tlast; dl.skip = svt[0]; dl.skip_bf16 = ab; dl.H_skip = (int)d.L[1]; dl.C_skip = ENC_CH[0];
+            dl.fold = c->tlast; dl.skip = eoff(b.sk4t, s0 * d.L[1] * 4, ea); dl.skip_bf16 = ab; dl.H_skip = (int)d.L[1];
+            dl.C_skip = 4;
             dl.out = b.Gt;
             r.check(tdec_last_launch(dl, r.s), "tdec_last");
             xt2 = b.Gt;

@@ -61,6 +61,9 @@ struct GemmDesc {
     int col_off = 0;
     int64_t c_bs = -1;        // elements between output batches (-1: H_out_total*W*ldo)
     int store = 1;            // 0: compute statistics only
+    // GLU epilogue only: the first 4 output channels of every row also go to c4 [rows][4] (C's dtype), the compact
+    // copy the decoders' last level reads as its skip (saved[0][:, :4], ATHTDemucs_v2.py:96-103 / :130-137)
+    void* c4 = nullptr;
     int col_split = 0;        // >0: column group g = n / col_split goes to output row + g * hi_row_off, column
     int hi_row_off = 1;       //     n - g * col_split (ConvTranspose residue classes computed by one GEMM)
     int store_mask = 3;       //     bit g: store column group g

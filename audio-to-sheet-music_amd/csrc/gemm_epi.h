@@ -194,6 +194,11 @@ ATHD_DEV void gemm_epilogue(const GemmDesc& d, const f32x4_t (&acc)[TM][TN], int
                         } else {
                             *reinterpret_cast<float4*>((float*)d.C + obase + oc) = make_float4(o[0], o[1], o[2], o[3]);
                         }
+                        if (d.c4 && oc == 0) {        // compact copy of channels 0..3 (row index of the dense C)
+                            const int64_t ri = (obase - d.col_off) / d.ldo;
+                            if (f_cbf) *reinterpret_cast<uint2*>((bf16_t*)d.c4 + 4 * ri) = make_uint2(pack2bf(o[0], o[1]), pack2bf(o[2], o[3]));
+                            else *reinterpret_cast<float4*>((float*)d.c4 + 4 * ri) = make_float4(o[0], o[1], o[2], o[3]);
+                        }
                     }
                 }
             } else {

@@ -122,6 +122,7 @@ struct FencRowDesc {
     const uint16_t* wr = nullptr; int wr_ld = 0; const float* br = nullptr;      // rewrite [2C][C] GLU-interleaved
     const float* row_add = nullptr;    // level 0: freq embedding [Fout][C]
     uint16_t* out = nullptr;           // [B][Fout][T][C] bf16
+    uint16_t* out4 = nullptr;          // level 0 (optional): channels 0..3 of out, [B][Fout][T][4] (decoder skip copy)
 };
 bool fenc_row_supported(int cin, int c, int T);
 int fenc_row_launch(const FencRowDesc& d, int cin, int c, hipStream_t s);
