@@ -621,11 +621,10 @@ __global__ __launch_bounds__(FR_NT, 4) void fenc_row0_kernel(const FencRowDesc d
                 make_uint2(pack2bf(g[0], g[1]), pack2bf(g[2], g[3]));
         }
         // (the hidden rows of this wave's positions were written by this wave: LDS order within a wave suffices)
-        if (l4 == 0) {
-#pragma unroll
-            for (int i = 0; i < 3; ++i) {
-                const int mt = wave + FR_NW * i;
-                if (mt * 16 + l15 >= T) continue;
+        // lane group l4 < 3 takes the positions of m-tile wave + FR_NW l4: the wave's 48 positions in one pass
+        {
+            const int mt = wave + FR_NW * l4;
+            if (l4 < 3 && mt * 16 + l15 < T) {
                 const uint4 hq = *reinterpret_cast<const uint4*>(&hs[(mt * 16 + l15) * F0_HS_P]);
                 const float x[6] = {__uint_as_float(hq.x << 16), __uint_as_float(hq.x & 0xFFFF0000u),
                                     __uint_as_float(hq.y << 16), __uint_as_float(hq.y & 0xFFFF0000u),

@@ -251,17 +251,96 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const LnDesc d) {
     }
 }
 
+// C = 512 with RW rows per wave: every load of the wave's rows (and the affine rows) is issued before the first
+// reduction, RW x 32 B in flight per lane instead of 32 B (one short row per wave left each wave mostly waiting on
+// its single load).  Per row the arithmetic is layernorm_kernel<8>'s.
+template <int RW>
+__global__ __launch_bounds__(256) void layernorm_rows_kernel(const LnDesc d) {
+    constexpr int C = 512;
+    const int lane = threadIdx.x & 63;
+    const int64_t row0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * RW;
+    const int64_t rows = (int64_t)d.nb * d.N;
+    if (row0 >= rows) return;
+    float v[RW][8];
+#pragma unroll
+    for (int r = 0; r < RW; ++r) {
+        const int64_t row = row0 + r < rows ? row0 + r : rows - 1;
+        ld8(d.x + row * C + 8 * lane, v[r]);
+    }
+    float wv[8], bv[8];
+    ld8(d.w + 8 * lane, wv);
+    ld8(d.b + 8 * lane, bv);
+    if (d.gn_stats) {
+        float gw[8], gb[8];
+        ld8(d.gn_w + 8 * lane, gw);
+        ld8(d.gn_b + 8 * lane, gb);
+#pragma unroll
+        for (int r = 0; r < RW; ++r) {
+            const int64_t row = row0 + r;
+            if (row >= rows) break;
+            float gm, gr;
+            gn_params(d.gn_stats, row / d.N, d.N * (int64_t)C, gm, gr);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[r][j] = (v[r][j] - gm) * gr * gw[j] + gb[j];
+            float4* xo = reinterpret_cast<float4*>(d.x + row * C + 8 * lane);
+            xo[0] = make_float4(v[r][0], v[r][1], v[r][2], v[r][3]);
+            xo[1] = make_float4(v[r][4], v[r][5], v[r][6], v[r][7]);
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < RW; ++r) {
+        const int64_t row = row0 + r;
+        if (row >= rows) break;
+        float s = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s += v[r][j];
+        const float mean = wave_sum(s) * (1.f / C);
+        float q = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { const float t = v[r][j] - mean; q += t * t; }
+        const float rstd = 1.f / sqrtf(wave_sum(q) * (1.f / C) + 1e-5f);
+        float pv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};     // (positional rows: the input LayerNorms only)
+        if (d.pos) ld8(d.pos + (row % d.N) * C + 8 * lane, pv);
+        float y[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) y[j] = (v[r][j] - mean) * rstd * wv[j] + bv[j] + pv[j];
+        if (d.out_bf16) {
+            reinterpret_cast<uint4*>((bf16_t*)d.out + row * C)[lane] =
+                make_uint4(pack2bf(y[0], y[1]), pack2bf(y[2], y[3]), pack2bf(y[4], y[5]), pack2bf(y[6], y[7]));
+        } else {
+            float4* o = reinterpret_cast<float4*>((float*)d.out + row * C);
+            o[2 * lane] = make_float4(y[0], y[1], y[2], y[3]);
+            o[2 * lane + 1] = make_float4(y[4], y[5], y[6], y[7]);
+        }
+    }
+}
+
+#ifndef ATHD_LN_RW
+#define ATHD_LN_RW 4
+#endif
+constexpr int LN_RW = ATHD_LN_RW;
+
 void layernorm_launch(const LnDesc& d, hipStream_t s) {
     const int64_t rows = (int64_t)d.nb * d.N;
+    if (d.C == 512) {
+        const dim3 grid((unsigned)((rows + 4 * LN_RW - 1) / (4 * LN_RW)));
+        KScope ks(s);
+        if (ks.on()) {
+            double by = (double)rows * d.C * (4 + (d.out_bf16 ? 2 : 4)) + (d.gn_stats ? (double)rows * d.C * 4 : 0.0);
+            if (d.pos) by += (double)d.N * d.C * 4;
+            ks.begin(klabel("layernorm_rows_kernel<%d>", LN_RW), 0.0, by);
+        }
+        hipLaunchKernelGGL(layernorm_rows_kernel<LN_RW>, grid, dim3(256), 0, s, d);
+        return;
+    }
     dim3 grid((unsigned)((rows + 3) / 4));
     KScope ks(s);
     if (ks.on()) {
         double by = (double)rows * d.C * (4 + (d.out_bf16 ? 2 : 4)) + (d.gn_stats ? (double)rows * d.C * 4 : 0.0);
         if (d.pos) by += (double)d.N * d.C * 4;
-        ks.begin(d.C == 512 ? "layernorm_kernel<8>" : "layernorm_kernel<6>", 0.0, by);
+        ks.begin("layernorm_kernel<6>", 0.0, by);
     }
-    if (d.C == 512) hipLaunchKernelGGL(layernorm_kernel<8>, grid, dim3(256), 0, s, d);
-    else hipLaunchKernelGGL(layernorm_kernel<6>, grid, dim3(256), 0, s, d);
+    hipLaunchKernelGGL(layernorm_kernel<6>, grid, dim3(256), 0, s, d);
 }
 
 // --------------------------------------------------------------------------------------------- text conditioning

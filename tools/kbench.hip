@@ -33,6 +33,18 @@ int kb_gemm(int variant, const void* A, int a_bf16, const void* W, const float* 
     if (variant >= 30) return gemm3_launch(d, (hipStream_t)stream, variant - 30);
     return gemm_launch(d, 1, (hipStream_t)stream);
 }
+// residual-stream GEMM as the transformer's out_proj / linear2 run it: C (f32, in place) = C + scale * (A @ W^T + bias),
+// with stats != NULL also {sum, sumsq} of the result (one group: nb = 1)
+int kb_gemm_res(int variant, const void* A, const void* W, const float* bias, float* C, const float* scale,
+                double* stats, int M, int N, int K, int Kp, void* stream) {
+    GemmDesc d;
+    d.A = A; d.a_bf16 = 1; d.nb = 1; d.H_in = M; d.W = 1; d.C_in = K; d.a_ld = K; d.H_out = M;
+    d.Wp = W; d.N = N; d.K = K; d.Kp = Kp; d.bias = bias; d.C = C; d.c_bf16 = 0; d.H_out_total = M; d.ldo = N;
+    d.res = C; d.res_scale = scale; d.stats = stats;
+    if (variant == 50) return N % 256 == 0 ? gemm5_launch(d, (hipStream_t)stream) : -1;
+    if (variant >= 30) return gemm3_launch(d, (hipStream_t)stream, variant - 30);
+    return gemm_launch(d, 1, (hipStream_t)stream);
+}
 // ConvT residue-pair GEMM as the decoder runs it (kept mode, pair 0): A (nb, H, W, Cin) bf16, 2 taps (rows u-1, u),
 // N = 2*Cout columns split at Cout, only the high half stored into slot 2u of a (nb, 2H, W, Cout) bf16 output,
 // GroupNorm statistics per nb.

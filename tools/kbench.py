@@ -50,6 +50,39 @@ def gemm_case(M, N, K, act=0):
     print(f"GEMM M={M} N={N} K={K} act={act}: " + "  ".join(f"{k}: {v[0]:8.1f}us {v[1]:7.1f}TF err={v[2]:.1e}" for k, v in res.items()), flush=True)
 
 
+def res_case(M, N, K, stats=False, variants=(50, 31, 131, 32, 132, 37, 137)):
+    """transformer residual GEMM (out_proj: K = 512; linear2: K = 2048 with GroupNorm statistics), C f32 in place"""
+    dev = "cuda"
+    A = (torch.randn(M, K, device=dev) * 0.5).to(torch.bfloat16)
+    Kp = (K + 63) // 64 * 64
+    W = torch.zeros(N, Kp, device=dev, dtype=torch.bfloat16)
+    W[:, :K] = (torch.randn(N, K, device=dev) * 0.05).to(torch.bfloat16)
+    bias = torch.randn(N, device=dev) * 0.1
+    scale = torch.rand(N, device=dev) * 0.2
+    R = torch.randn(M, N, device=dev)
+    C = R.clone()
+    st_buf = torch.zeros(2, device=dev, dtype=torch.float64) if stats else None
+    s = torch.cuda.current_stream().cuda_stream
+    ref = R + scale * (A.float() @ W[:, :K].float().t() + bias)
+    flops = 2.0 * M * N * K
+    hbm = M * K * 2 + 2 * M * N * 4
+    res = {}
+    for v in variants:
+        C.copy_(R)
+        rc = lib.kb_gemm_res(v, vp(A.data_ptr()), vp(W.data_ptr()), vp(bias.data_ptr()), vp(C.data_ptr()),
+                             vp(scale.data_ptr()), vp(st_buf.data_ptr() if stats else 0), M, N, K, Kp, vp(s))
+        if rc != 0:
+            continue
+        torch.cuda.synchronize()
+        err = (C - ref).abs().max().item() / (ref.abs().max().item() + 1e-9)
+        f = lambda: lib.kb_gemm_res(v, vp(A.data_ptr()), vp(W.data_ptr()), vp(bias.data_ptr()), vp(C.data_ptr()),
+                                    vp(scale.data_ptr()), vp(st_buf.data_ptr() if stats else 0), M, N, K, Kp, vp(s))
+        us = timeit(f)
+        res[f"v{v}"] = (us, flops / us / 1e6, hbm / us / 1e3, err)
+    print(f"RES GEMM M={M} N={N} K={K} stats={stats}: " + "  ".join(
+        f"{k}: {v[0]:7.1f}us {v[1]:6.1f}TF {v[2]:6.0f}GB/s err={v[3]:.1e}" for k, v in res.items()), flush=True)
+
+
 def convt_case(nb, H, Wd, Cin, Cout, variants):
     dev = "cuda"
     A = (torch.randn(nb, H, Wd, Cin, device=dev) * 0.5).to(torch.bfloat16)
@@ -264,6 +297,12 @@ if __name__ == "__main__":
         gemm_case(4096, 4096, 4096)
         gemm_case(M, 512, 2048)
         gemm_case(M, 1536, 512)
+        sys.exit(0)
+    if "res" in sys.argv[1:]:                 # residual-epilogue GEMMs: gemm5 vs gemm3 tiles (+100: persistent)
+        for _ in range(2):
+            res_case(M, 512, 512)
+            res_case(M, 512, 2048, stats=True)
+            res_case(64 * 259, 512, 512)
         sys.exit(0)
     if "g5" in sys.argv[1:]:
         VARIANTS = (40, 50)
