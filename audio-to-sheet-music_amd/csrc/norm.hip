@@ -315,10 +315,9 @@ __global__ __launch_bounds__(256) void layernorm_rows_kernel(const LnDesc d) {
     }
 }
 
-#ifndef ATHD_LN_RW
-#define ATHD_LN_RW 4
-#endif
-constexpr int LN_RW = ATHD_LN_RW;
+// rows per wave: 4 measured 1.80 ms per forward vs 1.83 for one row per wave (layernorm_kernel<8>); whole-step A/B of
+// 1, 2 and 4 within noise (tools/gpu_r03f.sh)
+constexpr int LN_RW = 4;
 
 void layernorm_launch(const LnDesc& d, hipStream_t s) {
     const int64_t rows = (int64_t)d.nb * d.N;
