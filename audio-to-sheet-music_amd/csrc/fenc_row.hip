@@ -249,10 +249,11 @@ __global__ __launch_bounds__(NW * 64, CIN == 4 ? 3 : 1) void fenc_row_kernel(con
         s1 = 0.f;
         s2 = 0.f;
         if constexpr (GRAM) {
-            // the 1x1 output's GroupNorm statistics from the moments of the 1x1 conv (see fenc_row0_kernel), one
-            // position per lane (l4 = 0) from the hidden rows this wave wrote (in-wave LDS order)
+            // the 1x1 output's GroupNorm statistics from the moments of the 1x1 conv (see fenc_row0_kernel) from the
+            // hidden rows this wave wrote (in-wave LDS order): lane (l15, l4) takes rows j = l4, l4 + 4, .. of the
+            // quadratic form for position l15 of each of the wave's m-tiles (the workgroup sum adds the parts)
             const float* G = gsh[dd];
-            if (l4 == 0) {
+            {
 #pragma unroll
                 for (int i = 0; i < C3I; ++i) {
                     const int mt = wave + NW * i;
@@ -271,17 +272,20 @@ __global__ __launch_bounds__(NW * 64, CIN == 4 ? 3 : 1) void fenc_row_kernel(con
                         }
                     }
                     float q = 0.f, lv = 0.f, lw = 0.f;
-#pragma unroll 1
-                    for (int j = 0; j < H; ++j) {            // (rolled: G's rows are read from LDS per j)
+#pragma unroll
+                    for (int jj = 0; jj < (H + 3) / 4; ++jj) {
+                        const int j = 4 * jj + l4;
+                        if (j >= H) break;
+                        const float xj = __uint_as_float((uint32_t)hs[(mt * 16 + l15) * HS_P + j] << 16);
                         float t = 0.f;
 #pragma unroll
                         for (int kk = 0; kk < H; ++kk) t += G[j * H + kk] * x[kk];
-                        q += x[j] * t;
-                        lv += G[H * H + j] * x[j];
-                        lw += G[H * H + H + j] * x[j];
+                        q += xj * t;
+                        lv += G[H * H + j] * xj;
+                        lw += G[H * H + H + j] * xj;
                     }
-                    s1 += G[H * H + 2 * H] + lw;
-                    s2 += G[H * H + 2 * H + 1] + (2.f * lv + q);
+                    s1 += (l4 == 0 ? G[H * H + 2 * H] : 0.f) + lw;
+                    s2 += (l4 == 0 ? G[H * H + 2 * H + 1] : 0.f) + (2.f * lv + q);
                 }
             }
         }
@@ -318,14 +322,17 @@ __global__ __launch_bounds__(NW * 64, CIN == 4 ? 3 : 1) void fenc_row_kernel(con
         block_sum2<NW>(s1, s2, red[2 * dd + 1]);      // (its barrier also publishes hs)
         float ym, yr;
         gn_from_sums(s1, s2, (float)(2 * C * T), ym, yr);
-        float gwa[4], gba[4], gwg[4], gbg[4], sc[4];
+        // (y + b - mean) * rstd * w + beta as y * wa + ca, the LayerScale folded into the 'a' half and -log2(e) into
+        // the gate half: x += a' / (1 + 2^g')
+        float wav[4], cav[4], wgv[4], cgv[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            gwa[q] = d.g2w[dd][pa + q];
-            gba[q] = d.g2b[dd][pa + q];
-            gwg[q] = d.g2w[dd][pa + 16 + q];
-            gbg[q] = d.g2b[dd][pa + 16 + q];
-            sc[q] = d.scale[dd][cb + q];
+            const float sc = d.scale[dd][cb + q];
+            const float wa_ = d.g2w[dd][pa + q] * yr, wg_ = d.g2w[dd][pa + 16 + q] * yr;
+            wav[q] = wa_ * sc;
+            cav[q] = ((ba[q] - ym) * wa_ + d.g2b[dd][pa + q]) * sc;
+            wgv[q] = wg_ * -1.4426950408889634f;
+            cgv[q] = ((bg[q] - ym) * wg_ + d.g2b[dd][pa + 16 + q]) * -1.4426950408889634f;
         }
 #pragma unroll
         for (int i = 0; i < MTW; ++i) {
@@ -338,9 +345,9 @@ __global__ __launch_bounds__(NW * 64, CIN == 4 ? 3 : 1) void fenc_row_kernel(con
             if (m >= T) continue;                 // positions >= T stay 0 in xr and xs
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                const float a = (ya[q] + ba[q] - ym) * yr * gwa[q] + gba[q];
-                const float g = (yg[q] + bg[q] - ym) * yr * gwg[q] + gbg[q];
-                xr[i][q] = xr[i][q] + sc[q] * (a * sigmoid_fast(g));
+                const float a = ya[q] * wav[q] + cav[q];
+                const float g = yg[q] * wgv[q] + cgv[q];
+                xr[i][q] = a * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(g)) + xr[i][q];
             }
             st4bf(&xs[(FR_HALO + m) * XS_P + cb], xr[i][0], xr[i][1], xr[i][2], xr[i][3]);
         }
@@ -541,10 +548,14 @@ __global__ __launch_bounds__(FR_NT, 4) void fenc_row0_kernel(const FencRowDesc d
         const int l15 = opaque_lane() & 15;
 #pragma unroll
         for (int i = 0; i < MTW; ++i) {
-            const int m = (mg + 2 * i) * 16 + l15;
-            const bool ok = m < T;
+            const int mt = mg + 2 * i;
+            const int m = mt * 16 + l15;
 #pragma unroll
-            for (int q = 0; q < 4; ++q) xr[i][q] = ok ? gelu_fast(xr[i][q] + bcv[q]) : 0.f;
+            for (int q = 0; q < 4; ++q) xr[i][q] = gelu_fast(xr[i][q] + bcv[q]);
+            if (mt * 16 + 16 > T) {               // (wave-uniform) the tile holding position T: zero the tail
+#pragma unroll
+                for (int q = 0; q < 4; ++q) xr[i][q] = m < T ? xr[i][q] : 0.f;
+            }
             st4bf(&xs[(FR_HALO + m) * F0_XS_P + cb], xr[i][0], xr[i][1], xr[i][2], xr[i][3]);
         }
     }
@@ -654,14 +665,20 @@ __global__ __launch_bounds__(FR_NT, 4) void fenc_row0_kernel(const FencRowDesc d
         block_sum2_dpp(s1, s2, red[2 * dd + 1]);
         float ym, yr;
         gn_from_sums(s1, s2, (float)(2 * C * T), ym, yr);
-        // (y + b - mean) * rstd * w + beta  as  y * wa + ca  (wa = rstd w, ca = (b - mean) wa + beta)
-        const float gwav[4] = {gwa.x * yr, gwa.y * yr, gwa.z * yr, gwa.w * yr};
-        const float gwgv[4] = {gwg.x * yr, gwg.y * yr, gwg.z * yr, gwg.w * yr};
-        const float cav[4] = {(bav[0] - ym) * gwav[0] + gba.x, (bav[1] - ym) * gwav[1] + gba.y,
-                              (bav[2] - ym) * gwav[2] + gba.z, (bav[3] - ym) * gwav[3] + gba.w};
-        const float cgv[4] = {(bgv[0] - ym) * gwgv[0] + gbg.x, (bgv[1] - ym) * gwgv[1] + gbg.y,
-                              (bgv[2] - ym) * gwgv[2] + gbg.z, (bgv[3] - ym) * gwgv[3] + gbg.w};
+        // (y + b - mean) * rstd * w + beta  as  y * wa + ca  (wa = rstd w, ca = (b - mean) wa + beta); the 'a' half
+        // carries the LayerScale, the gate half -log2(e): x += a' / (1 + 2^g')
         const float scv[4] = {sc4.x, sc4.y, sc4.z, sc4.w};
+        const float gwa4[4] = {gwa.x * yr, gwa.y * yr, gwa.z * yr, gwa.w * yr};
+        const float gwg4[4] = {gwg.x * yr, gwg.y * yr, gwg.z * yr, gwg.w * yr};
+        const float gba4[4] = {gba.x, gba.y, gba.z, gba.w}, gbg4[4] = {gbg.x, gbg.y, gbg.z, gbg.w};
+        float gwav[4], cav[4], gwgv[4], cgv[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            gwav[q] = gwa4[q] * scv[q];
+            cav[q] = ((bav[q] - ym) * gwa4[q] + gba4[q]) * scv[q];
+            gwgv[q] = gwg4[q] * -1.4426950408889634f;
+            cgv[q] = ((bgv[q] - ym) * gwg4[q] + gbg4[q]) * -1.4426950408889634f;
+        }
         // pass 2: GroupNorm -> GLU -> LayerScale -> residual
         const int l15c = opaque_lane() & 15;
 #pragma unroll
@@ -672,13 +689,15 @@ __global__ __launch_bounds__(FR_NT, 4) void fenc_row0_kernel(const FencRowDesc d
             const bf16x8_t hf = ldfrag(&hs[m * F0_HS_P + 8 * l4]);
             const f32x4_t z = f32x4_t{0.f, 0.f, 0.f, 0.f};
             const f32x4_t ya = mfma(wa, hf, z), yg = mfma(wg, hf, z);
-            const bool ok = m < T;                // positions >= T stay 0 in xr and xs
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const float a = ya[q] * gwav[q] + cav[q];
                 const float g = yg[q] * gwgv[q] + cgv[q];
-                const float nx = xr[i][q] + scv[q] * (a * sigmoid_fast(g));
-                xr[i][q] = ok ? nx : 0.f;
+                xr[i][q] = a * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(g)) + xr[i][q];
+            }
+            if (mt * 16 + 16 > T) {               // (wave-uniform) positions >= T stay 0 in xr and xs
+#pragma unroll
+                for (int q = 0; q < 4; ++q) xr[i][q] = m < T ? xr[i][q] : 0.f;
             }
             st4bf(&xs[(FR_HALO + m) * F0_XS_P + cb], xr[i][0], xr[i][1], xr[i][2], xr[i][3]);
         }
@@ -698,7 +717,9 @@ __global__ __launch_bounds__(FR_NT, 4) void fenc_row0_kernel(const FencRowDesc d
             wa[ks] = ldfrag(wr + (int64_t)(32 * ct + l15) * d.wr_ld + ks * 32 + 8 * l4);
             wg[ks] = ldfrag(wr + (int64_t)(32 * ct + 16 + l15) * d.wr_ld + ks * 32 + 8 * l4);
         }
-        const float bav[4] = {ba.x, ba.y, ba.z, ba.w}, bgv[4] = {bg.x, bg.y, bg.z, bg.w};
+        const float bav[4] = {ba.x, ba.y, ba.z, ba.w};
+        const float bgv[4] = {bg.x * -1.4426950408889634f, bg.y * -1.4426950408889634f, bg.z * -1.4426950408889634f,
+                              bg.w * -1.4426950408889634f};
         const float rav[4] = {ra.x, ra.y, ra.z, ra.w};
         uint2 ov[MTW];
         const int l15 = opaque_lane() & 15;
@@ -717,7 +738,8 @@ __global__ __launch_bounds__(FR_NT, 4) void fenc_row0_kernel(const FencRowDesc d
             }
             float o[4];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) o[q] = (za[q] + bav[q]) * sigmoid_fast(zg[q] + bgv[q]) + rav[q];
+            for (int q = 0; q < 4; ++q)
+                o[q] = (za[q] + bav[q]) * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(zg[q] * -1.4426950408889634f + bgv[q])) + rav[q];
             ov[i] = make_uint2(pack2bf(o[0], o[1]), pack2bf(o[2], o[3]));
         }
         __syncthreads();         // every wave has read xs: stage the output row [T][C] there
