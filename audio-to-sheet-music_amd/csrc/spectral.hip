@@ -213,7 +213,7 @@ void stft_launch(const float* wav, int nb, int64_t T, const PadPlan& pp, int Tsp
 // i.e. offsets o = j + 256 (q' & 3) of the frame's hop h = q' >> 2: every thread owns the same 4 offsets of every hop
 // block, so the overlap-add runs in registers: acc[h] = block f + h, frame f adds its hop h to acc[h] (ascending f,
 // from 0.0f), then block f has all of this workgroup's frames and the ring shifts by one block.
-// Workgroup k of an item runs the IO_G real frames t = IO_G k .. (one inverse FFT per frame).
+// Workgroup k of an item runs the g real frames t = g k .. (one inverse FFT per frame; istft_ola_split).
 // Its blocks whose frames all lie in its range are final: divided by the window envelope, the denormalised time
 // branch added, stored (4 coalesced samples x 2 channels per thread).  The 3 blocks at each end of its range also
 // take frames of the neighbouring workgroup: their partial sums go to `part` (head: first 3 blocks, tail: the 3
@@ -221,7 +221,22 @@ void stft_launch(const float* wav, int nb, int64_t T, const PadPlan& pp, int Tsp
 // the last workgroup's tail only border zero frames and are final in place.
 // Traffic per item: FO + the segment's spectrum (shared by its prompts through L2) + xt2 + out + 48 KB of partials
 // per workgroup, vs round 1's 8.5 MB frame tensor written and read back per item.
-constexpr int IO_G = 32;
+constexpr int IO_G = 32;            // at most this many frames per workgroup
+
+// Frames per workgroup g and workgroups per item n: n = ceil(Tspec / 32) workgroups of g = ceil(Tspec / n) frames
+// (balanced: at 6 s, Tspec = 259, 9 x 29 | 27 instead of 8 x 32 | 3, so the 2304 workgroups of the bench config fill
+// exactly 3 rounds of 768 resident workgroups instead of leaving a third of the last round idle).  Every workgroup
+// but the first must hold >= 3 frames: its 3 head blocks border the previous workgroup, its 3 tail blocks the next
+// one (a 1- or 2-frame workgroup would hand out head and tail parts of the same blocks), so n grows until the last
+// workgroup has >= 3 frames.
+struct OlaSplit { int n, g; };
+static OlaSplit istft_ola_split(int Tspec) {
+    // (terminates for every Tspec >= 1: checked exhaustively up to 200000 frames, 55 h of audio)
+    for (int n = (Tspec + IO_G - 1) / IO_G;; ++n) {
+        const int g = (Tspec + n - 1) / n;
+        if (n == 1 || (g >= 3 && Tspec - (n - 1) * g >= 3) || g < 3) return {n, g};
+    }
+}
 
 // Finish hop block B: out = y / env + denormalised time branch, for the samples of [0, T).  Every block holding an
 // output sample is interior (q = n + 3584 >= 3 HOP, and B <= (T + 3583) / HOP <= Tspec + 3 = nfr - 1 because
@@ -274,7 +289,7 @@ __global__ __launch_bounds__(256, MINW) void istft_ola_kernel(const float* __res
                                                            const float* __restrict__ win2,
                                                            const float* __restrict__ xt2,
                                                            const float* __restrict__ tnorm, float* __restrict__ out,
-                                                           float* __restrict__ part, int nwg, int units) {
+                                                           float* __restrict__ part, int nwg, int g, int units) {
     constexpr bool FAST = sizeof(R) == 4;
     __shared__ cpx buf[FPAD];
     __shared__ uint2 ltab[2048];       // resize of the Tspec decoder rows to 2048 bins: {i0 | i1 << 16, l1}
@@ -286,7 +301,7 @@ __global__ __launch_bounds__(256, MINW) void istft_ola_kernel(const float* __res
     const int64_t b = u / nwg;
     const int k = u % nwg;
     const int64_t item = b * P + jx % P;
-    const int t0 = k * IO_G, t1 = min(t0 + IO_G, Tspec);
+    const int t0 = k * g, t1 = min(t0 + g, Tspec);
     for (int kb = threadIdx.x; kb < 2048; kb += 256) {
         const LinIdx li = lin_index(kb, Tspec, 2048);
         ltab[kb] = make_uint2((uint32_t)li.i0 | ((uint32_t)li.i1 << 16), __float_as_uint(li.l1));
@@ -409,9 +424,9 @@ __global__ __launch_bounds__(256, MINW) void istft_ola_kernel(const float* __res
     }
 }
 
-// boundary blocks: block 2 + IO_G k + h (k = 1 .. nwg-1, h = 0..2) = tail partial of workgroup k-1 + head of k
+// boundary blocks: block 2 + g k + h (k = 1 .. nwg-1, h = 0..2) = tail partial of workgroup k-1 + head of k
 // (exact division by the envelope: the blocks are few, so the f32 parity arithmetic serves both modes)
-__global__ __launch_bounds__(256) void istft_fix_kernel(int Tspec, int P, int T, int nwg,
+__global__ __launch_bounds__(256) void istft_fix_kernel(int Tspec, int P, int T, int nwg, int g,
                                                         const float* __restrict__ win2, const float* __restrict__ xt2,
                                                         const float* __restrict__ tnorm, float* __restrict__ out,
                                                         const float* __restrict__ part) {
@@ -429,16 +444,17 @@ __global__ __launch_bounds__(256) void istft_fix_kernel(int Tspec, int P, int T,
         y[o][1] = a.y + c.y;
     }
     ola_env_in(j, win2, env_in);
-    ola_finish<false>(2 + IO_G * k + h, j, y, T, env_in, xt2 + item * (int64_t)T * 2, tnorm[2 * b],
+    ola_finish<false>(2 + g * k + h, j, y, T, env_in, xt2 + item * (int64_t)T * 2, tnorm[2 * b],
                       tnorm[2 * b + 1], out + (item * 2 + 0) * T, out + (item * 2 + 1) * T);
 }
 
-int istft_ola_nwg(int Tspec) { return (Tspec + IO_G - 1) / IO_G; }
+int istft_ola_nwg(int Tspec) { return istft_ola_split(Tspec).n; }
 
 void istft_ola_launch(const float* fo, int NI, int Tspec, int P, int64_t T, const float* spec, const float2* tw,
                       const double2* tw64, const float* win, const float* win2, const float* xt2, const float* tnorm,
                       float* out, float* part, hipStream_t s) {
-    const int nwg = istft_ola_nwg(Tspec);
+    const OlaSplit sp = istft_ola_split(Tspec);
+    const int nwg = sp.n;
     {
         const int units = (NI / P) * nwg;
         const dim3 grid((unsigned)(8 * ((units + 7) / 8) * P));
@@ -451,16 +467,16 @@ void istft_ola_launch(const float* fo, int NI, int Tspec, int P, int64_t T, cons
         // <3 waves per SIMD, no prefetch>: 1512 vs 1781 us for <2, prefetch> (round 2 measurement)
         if (tw64)
             hipLaunchKernelGGL((istft_ola_kernel<double, double2, 3>), grid, dim3(256), 0, s, fo, Tspec, P, (int)T, spec,
-                               tw64, win, win2, xt2, tnorm, out, part, nwg, units);
+                               tw64, win, win2, xt2, tnorm, out, part, nwg, sp.g, units);
         else
             hipLaunchKernelGGL((istft_ola_kernel<float, float2, 3, false>), grid, dim3(256), 0, s, fo, Tspec, P, (int)T,
-                               spec, tw, win, win2, xt2, tnorm, out, part, nwg, units);
+                               spec, tw, win, win2, xt2, tnorm, out, part, nwg, sp.g, units);
     }
     if (nwg > 1) {
         const dim3 grid((unsigned)(3 * (nwg - 1)), (unsigned)NI);
         KScope ks(s);
         if (ks.on()) ks.begin("istft_fix_kernel", 0.0, (double)NI * (nwg - 1) * 3 * 1024 * 2 * 4 * 4);
-        hipLaunchKernelGGL(istft_fix_kernel, grid, dim3(256), 0, s, Tspec, P, (int)T, nwg, win2, xt2, tnorm, out, part);
+        hipLaunchKernelGGL(istft_fix_kernel, grid, dim3(256), 0, s, Tspec, P, (int)T, nwg, sp.g, win2, xt2, tnorm, out, part);
     }
 }
 

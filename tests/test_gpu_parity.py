@@ -120,10 +120,12 @@ def _phase_cond(z):
     return float(np.abs(m + 1e-8)[m != 0].min())
 
 
-@pytest.mark.parametrize("T", [30001, 44102, 9999])
+@pytest.mark.parametrize("T", [30001, 44102, 9999, 33297])
 def test_ragged_length(models, oracle_model, text_table, T):
     """T % 4 != 0: the time encoder's right pad and the time decoder's last ConvT output (4 L1 samples) linearly
-    resized to T (ATHTDemucs_v2.py:128-131), the general branch of tdec_last (dec_last.hip)."""
+    resized to T (ATHTDemucs_v2.py:128-131), the general branch of tdec_last (dec_last.hip).  T = 33297 (Tspec = 33):
+    the fused iSTFT splits the frames over 2 workgroups of 17 | 16 (spectral.hip istft_ola_split; a fixed 32-frame
+    split would leave a 1-frame last workgroup whose head and tail blocks coincide)."""
     from athd.synth import synthetic_batch
     wav = torch.as_tensor(synthetic_batch(1, T, seed0=6))
     cap = {}
