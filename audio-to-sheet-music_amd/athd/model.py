@@ -181,3 +181,30 @@ class AudioTextHTDemucs:
         ctx.forward_prompts(wav.data_ptr(), B, T, table.data_ptr(), P, out.data_ptr(), ws.data_ptr(), ws.numel(),
                             stream)
         return out
+
+    @torch.no_grad()
+    def capture_prompts(self, wav: torch.Tensor, prompts: List[str], out: Optional[torch.Tensor] = None):
+        """`forward_prompts` on these exact buffers captured into one HIP graph (torch.cuda.CUDAGraph over the
+        library's launches: both branch streams, their event fork / joins and the statistics memset).  Returns
+        (graph, out): `graph.replay()` re-runs every kernel of the forward on the same device buffers, so the caller
+        refreshes `wav` in place between replays; the prompt rows, the workspace and `out` stay bound to the graph.
+        `wav` must already be a contiguous float32 (B, 2, T) tensor on the model's device (no copy is captured)."""
+        if wav.dtype != torch.float32 or not wav.is_contiguous():
+            raise ValueError("capture_prompts needs a contiguous float32 wav (B, 2, T)")
+        wav = self._check_wav(wav)
+        B, _, T = wav.shape
+        ctx = self._ensure_ctx()
+        table = self.embedder.rows(list(prompts), len(prompts)).to(self.device).contiguous()
+        P = table.shape[0]
+        if out is None:
+            out = torch.empty((B, P, 2, T), dtype=torch.float32, device=self.device)
+        ws = self._workspace(ctx.workspace_bytes(B, T, P))
+        run = lambda: ctx.forward_prompts(wav.data_ptr(), B, T, table.data_ptr(), P, out.data_ptr(), ws.data_ptr(),
+                                          ws.numel(), torch.cuda.current_stream(self.device).cuda_stream)
+        run()                                   # eager once: one-time launch-configuration queries happen outside
+        torch.cuda.synchronize(self.device)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            run()
+        g._athd_keep = (wav, table, out, ws)    # the graph's device pointers stay valid while it lives
+        return g, out

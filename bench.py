@@ -194,6 +194,8 @@ def main():
     ap.add_argument("--no-extras", action="store_true", help="skip the SDR, f32 and section measurements")
     ap.add_argument("--dump-kernels", default=None, help="write the warmup step's per-kernel profile (JSON)")
     ap.add_argument("--kernel", default=None, help="roofline kernel (default: largest summed time in warmup)")
+    ap.add_argument("--eager", action="store_true",
+                    help="launch every step's kernels from the host instead of replaying the captured HIP graph")
     ap.add_argument("--segments", type=int, default=0,
                     help="also time one dataset pass of N segments over all ranks (BASELINE configs[3]: ~6k MUSDB18 "
                          "test-set segments) through athd.dist.separate_segments; printed as a second JSON line")
@@ -227,7 +229,15 @@ def main():
     out = torch.empty((N, len(STEMS), 2, SEG), dtype=torch.float32, device=dev) if rank == 0 else None
     pending = PendingSends(limit=2)          # at most two batches in flight per rank (bounded send buffers)
 
+    # N = 1: one athd_forward_prompts captured into a HIP graph (both branch streams and their event joins), replayed
+    # per step: the same kernels on the same buffers, without the host launch gaps between them
+    graph = None
+    if world == 1 and not args.eager:
+        graph, _ = model.capture_prompts(wav, STEMS, out=out)
+
     def step():
+        if graph is not None:
+            return graph.replay()
         if world == 1:
             return model.forward_prompts(wav, STEMS, out=out)
         # shard + point-to-point gather of the separated waveforms to rank 0, transfers left in flight
@@ -239,8 +249,10 @@ def main():
     # warmup; the last warmup step times every kernel per call site (HIP events) to find the dominant call site
     for i in range(args.warmup):
         if i == args.warmup - 1:
-            model.profile_start("@sites")
-        step()
+            model.profile_start("@sites")        # (events around eager launches: the graph's launches are baked)
+            fwd_only() if graph is not None else step()
+        else:
+            step()
     pending.wait()
     torch.cuda.synchronize()
     dominant = args.kernel
@@ -377,7 +389,8 @@ def main():
                                + ("; configs[3] shape: segments sharded over the GPUs, RCCL gather to rank 0 timed"
                                   if world > 1 else ""),
                    "global_batch": N, "seq_len": SEG, "prompts": 4, "parallelism": f"segment-sharded dp{world}",
-                   "gather_timed": world > 1},
+                   "gather_timed": world > 1,
+                   "launch": "hipGraph replay of one athd_forward_prompts" if graph is not None else "eager"},
         "stems_per_s": round(4 * value, 3),
         "roofline": roofline,
         "step_essential_tflops": round(step_tf, 2),

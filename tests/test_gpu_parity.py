@@ -310,3 +310,25 @@ def test_sharp_attention_encoder(state_dict, text_table):
     _report("sharp_attention", res)
     for key, v in res.items():
         assert v >= (F32_STAGE_DB if key.startswith("f32") else SHARP_BF16_SDR_DB), res
+
+
+@pytest.mark.parametrize("dt", ["f32", "bf16"])
+def test_graph_replay_matches_eager(models, dt):
+    """capture_prompts: one forward_prompts captured into a HIP graph (both branch streams, event fork/joins,
+    statistics memset) and replayed equals the eager call, also after the input is rewritten in place (the graph
+    reads the buffer, not a snapshot).  f32: fp32 rounding (order-dependent fp64 statistics atomics); bf16: >= 40 dB."""
+    from athd.synth import synthetic_batch
+    prompts = ["drums", "bass", "other", "vocals"]
+    m = models[dt]
+    wav = torch.as_tensor(synthetic_batch(2, 50000, seed0=321)).cuda()
+    g, out = m.capture_prompts(wav, prompts)
+    for seed in (321, 555):
+        wav.copy_(torch.as_tensor(synthetic_batch(2, 50000, seed0=seed)))
+        g.replay()
+        torch.cuda.synchronize()
+        ref = m.forward_prompts(wav, prompts)
+        if dt == "f32":
+            assert torch.allclose(out, ref, atol=1e-5, rtol=1e-4), seed
+        else:
+            assert sdr_db(ref.cpu().numpy(), out.cpu().numpy()) >= 40.0, seed
+    del g
