@@ -234,6 +234,8 @@ int athd_finalize(athd_ctx* c) {
                     e.dc.b1f[d] = c->up_key(q + ".3.bias");
                     e.dc.g2wf[d] = c->up_key(q + ".4.weight");
                     e.dc.g2bf[d] = c->up_key(q + ".4.bias");
+                } else if (c->mode == 1) {      // wide levels: the 1x1's statistics from its moments (gn_gelu_mom)
+                    e.dc.gram1b[d] = c->up_f32(conv1x1_moments(c->W(q + ".3.weight").v, c->W(q + ".3.bias").v, 2 * C, C / 8, true));
                 }
             }
         }

@@ -271,18 +271,30 @@ void dconv(Run& r, const EncW& e, void* x, int64_t nb, int64_t L, float* hbuf, u
         // bf16 mode: GELU(GN(h)) written once as bf16, so both 1x1 passes read half the bytes and run on the bf16
         // MFMA GEMMs (gemm3 / gemm5) instead of converting fp32 A on load
         const bool hb = r.actbf && hbuf_b && Hh % 8 == 0;
+        // the 1x1's GroupNorm statistics from its moments, taken by the GN+GELU pass (no statistics GEMM pass)
+        bool mom = false;
         {
             KSite site("dconv.gn_gelu");
-            if (hb) gn_gelu_bf16_launch(hbuf, hbuf_b, (int)nb, L * Hh, Hh, st_h, e.dc.g1w[dd], e.dc.g1b[dd], r.s);
-            else gn_gelu_launch(hbuf, (int)nb, L * Hh, Hh, st_h, e.dc.g1w[dd], e.dc.g1b[dd], r.s, r.actbf);
+            if (hb && e.dc.gram1b[dd])
+                mom = gn_gelu_mom_launch(hbuf, hbuf_b, (int)nb, L, Hh, st_h, e.dc.g1w[dd], e.dc.g1b[dd], e.dc.gram1b[dd],
+                                         st_y, r.s) == 0;
+            if (mom) {
+                // (statistics of the 1x1 already in st_y)
+            } else if (hb) {
+                gn_gelu_bf16_launch(hbuf, hbuf_b, (int)nb, L * Hh, Hh, st_h, e.dc.g1w[dd], e.dc.g1b[dd], r.s);
+            } else {
+                gn_gelu_launch(hbuf, (int)nb, L * Hh, Hh, st_h, e.dc.g1w[dd], e.dc.g1b[dd], r.s, r.actbf);
+            }
         }
         GemmDesc g2;
         g2.A = hb ? (const void*)hbuf_b : (const void*)hbuf; g2.a_bf16 = hb ? 1 : 0; g2.nb = (int)nb; g2.H_in = (int)L; g2.W = 1; g2.C_in = Hh; g2.a_ld = Hh; g2.H_out = (int)L;
         g2.Wp = e.dc.c1[dd].w; g2.N = 2 * C; g2.K = Hh; g2.Kp = e.dc.c1[dd].Kp; g2.bias = e.dc.c1[dd].bias;
         g2.C = x; g2.c_bf16 = ab; g2.H_out_total = (int)L; g2.ldo = C;
-        GemmDesc g1 = g2;
-        g1.stats = st_y; g1.store = 0;
-        r.gemm(g1, "dconv.conv1x1.stats");
+        if (!mom) {
+            GemmDesc g1 = g2;
+            g1.stats = st_y; g1.store = 0;
+            r.gemm(g1, "dconv.conv1x1.stats");
+        }
         g2.act = ACT_GLU; g2.gn_stats = st_y; g2.gn_count = L * 2 * C; g2.gn_w = e.dc.g2w[dd]; g2.gn_b = e.dc.g2b[dd];
         g2.res = x; g2.res_bf16 = ab; g2.res_scale = e.dc.scale[dd];
         r.gemm(g2, "dconv.conv1x1.apply");

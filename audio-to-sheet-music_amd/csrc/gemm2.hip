@@ -198,7 +198,9 @@ __global__ __launch_bounds__(256) void gemm2_kernel(const GemmDesc d) {
 
 bool gemm2_supported(const GemmDesc& d) {
     const bool flat = d.C_in < 8 && 8 % d.C_in == 0 && !d.a_bf16 && d.a_hs == d.C_in && d.dil == 1;
-    if ((d.C_in % 8 != 0 && !flat) || d.a_ld % (flat ? d.C_in : 8) != 0 || d.a_cs != 1 || d.Kp % 64 != 0 || d.N < 48)
+    const bool narrow = d.N <= 32 && d.N % 4 == 0 && d.a_bf16 && epi_flags(d) == F_STATS;   // launch2f<256, 32>
+    if ((d.C_in % 8 != 0 && !flat) || d.a_ld % (flat ? d.C_in : 8) != 0 || d.a_cs != 1 || d.Kp % 64 != 0 ||
+        (d.N < 48 && !narrow))
         return false;
     if (flat && (d.a_bs % 4 != 0 || d.a_ld % 4 != 0)) return false;      // 16-B aligned chunk starts
     if (d.a_bf16 && d.a_norm) return false;
@@ -233,7 +235,10 @@ static void launch2(const GemmDesc& d, hipStream_t s) {
 }
 
 int gemm2_launch(const GemmDesc& d, hipStream_t s) {
-    if (d.N <= 64) launch2<128, 64>(d, s);
+    // N <= 32 (the wide DConv levels' conv3, C -> C/8 = 24, with the GroupNorm statistics of h): 256 x 32 tiles,
+    // instantiated for that epilogue only (round 2 ran it on the v1 kernel at 1.4 TB/s)
+    if (d.N <= 32 && d.a_bf16 && epi_flags(d) == F_STATS) launch2f<256, 32, F_STATS>(d, s);
+    else if (d.N <= 64) launch2<128, 64>(d, s);
     else launch2<128, 128>(d, s);
     return (int)hipGetLastError();
 }

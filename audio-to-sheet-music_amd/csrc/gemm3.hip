@@ -270,6 +270,9 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm3_kernel(const GemmDesc d) {
             // the last ring stage is free here (the next tile's prologue filled stages 0 .. STAGES-2)
             gemm3_epilogue_ln<BM, BN, WM, WN, TM, TN>(d, acc, m0_done, wm0, wn0, lane, wave % WN,
                                                       reinterpret_cast<float*>(smem + (STAGES - 1) * STAGE), bias4);
+        } else if constexpr (F == (F_GN | F_GLU | F_RES | F_CBF16) && TN % 2 == 0) {
+            if (epi_glures_ok(d)) gemm_epilogue_glures<TM, TN>(d, acc, m0_done, n0, wm0, wn0, lane, bias4);
+            else gemm_epilogue<TM, TN, F, true>(d, acc, m0_done, n0, wm0, wn0, lane, st_lds, BM, bias4);
         } else {
             gemm_epilogue<TM, TN, F, true>(d, acc, m0_done, n0, wm0, wn0, lane, st_lds, BM, bias4);
         }

@@ -322,6 +322,12 @@ __global__ __launch_bounds__(512) void gemm5_kernel(const GemmDesc d) {
                 fast = true;
             }
         }
+        if constexpr (F == (F_GN | F_GLU | F_RES | F_CBF16) && TN % 2 == 0) {
+            if (epi_glures_ok(d)) {
+                gemm_epilogue_glures<TM, TN>(d, acc, m0_done, n0_done, wm0, wn0, lane, bias4);
+                fast = true;
+            }
+        }
         if (!fast) gemm_epilogue<TM, TN, F, true>(d, acc, m0_done, n0_done, wm0, wn0, lane, st_lds, 256, bias4);
         if (!PERSIST || next >= ntiles) break;
         tile = next;

@@ -316,6 +316,83 @@ ATHD_DEV void gemm_epilogue(const GemmDesc& d, const f32x4_t (&acc)[TM][TN], int
     }
 }
 
+// DConv 1x1 apply epilogue (F_GN | F_GLU | F_RES | F_CBF16 with a bf16 residual, dense rows: row m at m*ldo; the
+// wide encoder levels, forward.cpp dconv): out = res + scale * GLU(GN(acc + bias)).  Branch-free: every residual
+// value of the wave's rows is loaded before the first store (rows past M read the last row and store into a sink),
+// so the tile pays one load latency, not one per row fragment behind the previous fragment's stores as in
+// gemm_epilogue's guarded form.
+__device__ __attribute__((weak)) uint2 g_epi_sink2[64];
+
+ATHD_HD bool epi_glures_ok(const GemmDesc& d) {
+    return d.act == ACT_GLU && d.res && d.res_bf16 && d.c_bf16 && d.store && d.gn_stats && !d.row_add && !d.pbias &&
+           !d.col_split && !d.stats && !d.c4 && d.o_stride == 1 && d.o_off == 0 && d.H_out_total == d.H_out &&
+           d.c_bs < 0 && d.col_off == 0 && d.N % 32 == 0;
+}
+
+template <int TM, int TN>
+ATHD_DEV void gemm_epilogue_glures(const GemmDesc& d, f32x4_t (&acc)[TM][TN], int64_t m0, int n0, int wm0, int wn0,
+                                   int lane, const float4 (&bj)[TN]) {
+    static_assert(TN % 2 == 0, "GLU column pairs");
+    constexpr int TP = TN / 2;
+    const int fr = lane & 15, fg = lane >> 4;
+    const uint32_t M = (uint32_t)d.nb * d.H_out * d.W;
+    const int Nout = d.N / 2;
+    const bf16_t* X = (const bf16_t*)d.res;
+    uint2 rr[TM][TP];
+    int64_t ro[TM];
+    bool ok[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+        const uint32_t m = (uint32_t)m0 + wm0 + 16 * i + fr;
+        ok[i] = m < M;
+        ro[i] = (int64_t)(ok[i] ? m : M - 1) * d.ldo;
+#pragma unroll
+        for (int p = 0; p < TP; ++p) {
+            const int oc = (n0 + wn0 + 32 * p) / 2 + 4 * fg;
+            rr[i][p] = *reinterpret_cast<const uint2*>(X + ro[i] + (oc < Nout ? oc : 0));
+        }
+    }
+    float gm[TM], gr[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+        const uint32_t b = fdiv((uint32_t)(ro[i] / d.ldo), d.fd_hw);
+        const double mm = d.gn_stats[2 * b] / (double)d.gn_count;
+        double var = d.gn_stats[2 * b + 1] / (double)d.gn_count - mm * mm;
+        if (var < 0) var = 0;
+        gm[i] = (float)mm;
+        gr[i] = (float)(1.0 / sqrt(var + 1e-5));
+    }
+#pragma unroll
+    for (int p = 0; p < TP; ++p) {
+        const int na = n0 + wn0 + 32 * p + 4 * fg;            // packed columns of the 'a' half (gate: na + 16)
+        const int oc = (n0 + wn0 + 32 * p) / 2 + 4 * fg;      // output channels oc .. oc + 3
+        if (oc >= Nout) continue;
+        const float4 wa = *reinterpret_cast<const float4*>(d.gn_w + na), ba = *reinterpret_cast<const float4*>(d.gn_b + na);
+        const float4 wg = *reinterpret_cast<const float4*>(d.gn_w + na + 16), bg = *reinterpret_cast<const float4*>(d.gn_b + na + 16);
+        const float4 sc = d.res_scale ? *reinterpret_cast<const float4*>(d.res_scale + oc) : make_float4(1.f, 1.f, 1.f, 1.f);
+        const float wav[4] = {wa.x, wa.y, wa.z, wa.w}, bav[4] = {ba.x, ba.y, ba.z, ba.w};
+        const float wgv[4] = {wg.x, wg.y, wg.z, wg.w}, bgv[4] = {bg.x, bg.y, bg.z, bg.w};
+        const float scv[4] = {sc.x, sc.y, sc.z, sc.w};
+        const float b0[4] = {bj[2 * p].x, bj[2 * p].y, bj[2 * p].z, bj[2 * p].w};
+        const float b1[4] = {bj[2 * p + 1].x, bj[2 * p + 1].y, bj[2 * p + 1].z, bj[2 * p + 1].w};
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+            const uint2 q = rr[i][p];
+            const float r4[4] = {__uint_as_float(q.x << 16), __uint_as_float(q.x & 0xFFFF0000u),
+                                 __uint_as_float(q.y << 16), __uint_as_float(q.y & 0xFFFF0000u)};
+            float o[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const float a = (acc[i][2 * p][e] + b0[e] - gm[i]) * gr[i] * wav[e] + bav[e];
+                const float g = (acc[i][2 * p + 1][e] + b1[e] - gm[i]) * gr[i] * wgv[e] + bgv[e];
+                o[e] = r4[e] + scv[e] * (a * sigmoid_fast(g));
+            }
+            uint2* dst = ok[i] ? reinterpret_cast<uint2*>((bf16_t*)d.C + ro[i] + oc) : g_epi_sink2 + lane;
+            *dst = make_uint2(pack2bf(o[0], o[1]), pack2bf(o[2], o[3]));
+        }
+    }
+}
+
 // Residual-stream epilogue (F_RES [+ F_STATS], f32 output and residual, dense rows: row m at m*ldo): out = res +
 // res_scale * (acc + bias), GroupNorm statistics of out.  Written branch-free - rows past M read a clamped row and
 // store into a sink line - with the residual loads of row tile i+1 issued before the stores of tile i.  The compiler

@@ -45,6 +45,10 @@ void gn_gelu_launch(float* h, int nb, int64_t per_batch, int H, const double* st
 // out[nb][per_batch] (bf16) = GELU_fast(GN(h)); per_batch % 8 == 0, H % 8 == 0
 void gn_gelu_bf16_launch(const float* h, uint16_t* out, int nb, int64_t per_batch, int H, const double* stats,
                          const float* w, const float* b, hipStream_t s);
+// gn_gelu_bf16 on [nb][L][H] (H = 24 / 48, L >= 64) plus the following 1x1 conv's GroupNorm {sum, sumsq} per nb
+// into st_y from its moments `gram` (ctx.h conv1x1_moments, bf16-rounded weights); -1 if the shape is not covered
+int gn_gelu_mom_launch(const float* h, uint16_t* out, int nb, int64_t L, int H, const double* stats, const float* w,
+                       const float* b, const float* gram, double* st_y, hipStream_t s);
 void gn_gelu_bf16in_launch(const uint16_t* h, uint16_t* out, int nb, int64_t per_batch, int H, const double* stats,
                            const float* w, const float* b, hipStream_t s);
 // x[nb][N][C] = GN(x) in place

@@ -118,6 +118,102 @@ void gn_gelu_bf16_launch(const float* h, bf16_t* out, int nb, int64_t per_batch,
     hipLaunchKernelGGL(gn_gelu_bf16_kernel<false>, dim3(blocks, nb), dim3(256), 0, s, h, out, per_batch, H, stats, w, b);
 }
 
+// Wide DConv levels (H = C/8 = 24, 48; bf16 mode): gn_gelu_bf16_kernel's output plus the GroupNorm statistics of the
+// following 1x1 conv's 2C outputs from its moments (ctx.h conv1x1_moments on the bf16-rounded weights: G = W^T W,
+// v = W^T b, u = W^T 1, sum b, sum b^2), so no separate statistics GEMM pass over the 1x1 (forward.cpp dconv):
+//   sum_n y_n = sum b + u.x,   sum_n y_n^2 = sum b^2 + 2 v.x + x^T G x,   x = the bf16 GELU(GN(h)) row the GEMM reads.
+// One lane per position (row of H channels); groups of L >= 64 positions, so a wave spans at most two groups (its
+// sums go to the first active lane's group and, for lanes past a boundary, to the last lane's group).
+template <int H>
+__global__ __launch_bounds__(256) void gn_gelu_mom_kernel(const float* __restrict__ h, bf16_t* __restrict__ out,
+                                                          int64_t npos, int64_t L, const double* __restrict__ st,
+                                                          const float* __restrict__ w, const float* __restrict__ bb,
+                                                          const float* __restrict__ gram, double* __restrict__ st_y) {
+    __shared__ float wb[2 * H];
+    for (int i = threadIdx.x; i < 2 * H; i += 256) wb[i] = i < H ? w[i] : bb[i - H];
+    __syncthreads();
+    const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const bool act = p < npos;
+    const int64_t pp = act ? p : npos - 1;
+    const int64_t g = pp / L;
+    float mean, rstd;
+    gn_params(st, g, L * H, mean, rstd);
+    float x[H];
+    const float4* hr = reinterpret_cast<const float4*>(h + pp * H);
+#pragma unroll
+    for (int q = 0; q < H / 4; ++q) {
+        const float4 v = hr[q];
+        x[4 * q] = v.x; x[4 * q + 1] = v.y; x[4 * q + 2] = v.z; x[4 * q + 3] = v.w;
+    }
+    uint32_t pk[H / 2];
+#pragma unroll
+    for (int j = 0; j < H; j += 2) {
+        pk[j / 2] = pack2bf(gelu_fast((x[j] - mean) * rstd * wb[j] + wb[H + j]),
+                            gelu_fast((x[j + 1] - mean) * rstd * wb[j + 1] + wb[H + j + 1]));
+        x[j] = __uint_as_float(pk[j / 2] << 16);                 // the bf16 values the 1x1 GEMM multiplies
+        x[j + 1] = __uint_as_float(pk[j / 2] & 0xFFFF0000u);
+    }
+    if (act) {
+        uint4* o = reinterpret_cast<uint4*>(out + pp * H);
+#pragma unroll
+        for (int q = 0; q < H / 8; ++q) o[q] = make_uint4(pk[4 * q], pk[4 * q + 1], pk[4 * q + 2], pk[4 * q + 3]);
+    }
+    // the moments are wave-uniform: scalar loads, one G row per step (the pointer is made opaque per row, so the
+    // compiler cannot hoist all H*H loads to the front, which needed ~2300 registers and spilled)
+    typedef __attribute__((address_space(4))) const float cfloat;    // constant address space: scalar loads
+    float qf = 0.f, lv = 0.f, lw = 0.f;
+#pragma unroll
+    for (int j = 0; j < H; ++j) {
+        cfloat* gr = (cfloat*)(gram + j * H);
+        asm volatile("" : "+s"(gr), "+v"(qf));              // row j's loads after row j-1's products
+        float t = 0.f;
+#pragma unroll
+        for (int k0 = 0; k0 < H; k0 += 24) {               // (at most 24 row values in SGPRs at a time)
+            cfloat* gk = gr + k0;
+            if (k0 > 0) asm volatile("" : "+s"(gk), "+v"(t));
+#pragma unroll
+            for (int k = 0; k < 24; ++k) t = fmaf(gk[k], x[k0 + k], t);
+        }
+        qf = fmaf(x[j], t, qf);
+        lv = fmaf(gr[H * (H - j) + j], x[j], lv);            // gram[H*H + j]      = (W^T b)_j
+        lw = fmaf(gr[H * (H - j) + H + j], x[j], lw);        // gram[H*H + H + j]  = (W^T 1)_j
+    }
+    cfloat* gt = (cfloat*)(gram + H * H + 2 * H);
+    const float sb = gt[0], sb2 = gt[1];
+    const double s1 = act ? (double)(sb + lw) : 0.0;
+    const double s2 = act ? (double)(sb2 + (2.f * lv + qf)) : 0.0;
+    // segmented wave sums: group gA of the first lane, gB of the last active lane (gA <= g <= gB, gB <= gA + 1)
+    const int64_t gA = __builtin_amdgcn_readfirstlane((int)g);
+    const int64_t last = (int64_t)blockIdx.x * 256 + (threadIdx.x & ~63) + 63;
+    const int64_t gB = (last < npos ? last : npos - 1) / L;
+    const bool inA = g == gA;
+    const double a1 = wave_sum_d(inA ? s1 : 0.0), a2 = wave_sum_d(inA ? s2 : 0.0);
+    if ((threadIdx.x & 63) == 0) {
+        atomicAdd(&st_y[2 * gA], a1);
+        atomicAdd(&st_y[2 * gA + 1], a2);
+    }
+    if (gB != gA) {
+        const double b1 = wave_sum_d(inA ? 0.0 : s1), b2 = wave_sum_d(inA ? 0.0 : s2);
+        if ((threadIdx.x & 63) == 0) {
+            atomicAdd(&st_y[2 * gB], b1);
+            atomicAdd(&st_y[2 * gB + 1], b2);
+        }
+    }
+}
+
+int gn_gelu_mom_launch(const float* h, uint16_t* out, int nb, int64_t L, int H, const double* stats, const float* w,
+                       const float* b, const float* gram, double* st_y, hipStream_t s) {
+    if (L < 64 || (H != 24 && H != 48)) return -1;
+    const int64_t npos = (int64_t)nb * L;
+    const dim3 grid((unsigned)((npos + 255) / 256));
+    KScope ks(s);
+    if (ks.on())
+        ks.begin(klabel("gn_gelu_mom_kernel<%d>", H), 2.0 * npos * (H * H + 2 * H), (double)npos * H * (4 + 2));
+    if (H == 24) hipLaunchKernelGGL(gn_gelu_mom_kernel<24>, grid, dim3(256), 0, s, h, out, npos, L, stats, w, b, gram, st_y);
+    else hipLaunchKernelGGL(gn_gelu_mom_kernel<48>, grid, dim3(256), 0, s, h, out, npos, L, stats, w, b, gram, st_y);
+    return (int)hipGetLastError();
+}
+
 void gn_gelu_bf16in_launch(const uint16_t* h, uint16_t* out, int nb, int64_t per_batch, int H, const double* stats,
                            const float* w, const float* b, hipStream_t s) {
     int blocks = (int)((per_batch / 8 + 255) / 256);
