@@ -44,17 +44,16 @@ ATHD_DEV float erf_fast(float x) {
 // bf16-mode GELU: the tanh form x * sigmoid(sqrt(8/pi) (x + 0.044715 x^3)) on v_exp_f32 + v_rcp_f32, 7 VALU ops.
 // |gelu_fast - gelu_erf| <= 4.8e-4 absolute (at x ~ 2.7, value 2.69: 1.8e-4 relative, below half a bf16 ulp).
 ATHD_DEV float gelu_fast(float x) {
-    const float u = x * fmaf(0.044715f * 1.5957691216057308f, x * x, 1.5957691216057308f);
-    return x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(u * -1.4426950408889634f));
+    constexpr float K0 = -1.5957691216057308f * 1.4426950408889634f, K1 = K0 * 0.044715f;   // (-log2(e) folded in)
+    return x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(x * fmaf(K1, x * x, K0)));
 }
 template <bool FAST>
 ATHD_DEV float gelu(float x) { if constexpr (FAST) return gelu_fast(x); else return gelu_erf(x); }
 // gelu_fast on a pair: the polynomial and scaling on packed f32 ops (v_pk_mul / v_pk_fma), exp2 / rcp per lane
+// (the -log2(e) of the exp2 folded into the polynomial's constants: 4 packed ops + 2 x (exp, rcp) per pair)
 ATHD_DEV athd_f2v gelu_fast_pk(athd_f2v x) {
-    const athd_f2v c1 = {0.044715f * 1.5957691216057308f, 0.044715f * 1.5957691216057308f};
-    const athd_f2v c0 = {1.5957691216057308f, 1.5957691216057308f};
-    const athd_f2v u = x * __builtin_elementwise_fma(c1, x * x, c0);
-    const athd_f2v t = u * (athd_f2v){-1.4426950408889634f, -1.4426950408889634f};
+    constexpr float K0 = -1.5957691216057308f * 1.4426950408889634f, K1 = K0 * 0.044715f;
+    const athd_f2v t = x * __builtin_elementwise_fma((athd_f2v){K1, K1}, x * x, (athd_f2v){K0, K0});
     const athd_f2v den = (athd_f2v){__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)} + (athd_f2v){1.0f, 1.0f};
     return x * (athd_f2v){__builtin_amdgcn_rcpf(den.x), __builtin_amdgcn_rcpf(den.y)};
 }

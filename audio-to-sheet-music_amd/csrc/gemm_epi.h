@@ -224,9 +224,21 @@ ATHD_DEV void gemm_epilogue(const GemmDesc& d, const f32x4_t (&acc)[TM][TN], int
                     for (int q = 0; q < 4; ++q) {
                         float v = acc[i][j][q] + bv[q];
                         if (f_gn) v = (v - gm) * gr * d.gn_w[n + q] + d.gn_b[n + q];
-                        if (f_gelu) v = gelu<FASTG>(v);
-                        if (f_row) v += d.row_add[(int64_t)ho * Nout + n + q];
                         o[q] = v;
+                    }
+                    if (f_gelu) {
+                        if constexpr (FASTG) {      // bf16 mode: the polynomial and scaling on packed pairs
+                            const athd_f2v g01 = gelu_fast_pk((athd_f2v){o[0], o[1]});
+                            const athd_f2v g23 = gelu_fast_pk((athd_f2v){o[2], o[3]});
+                            o[0] = g01.x; o[1] = g01.y; o[2] = g23.x; o[3] = g23.y;
+                        } else {
+#pragma unroll
+                            for (int q = 0; q < 4; ++q) o[q] = gelu<FASTG>(o[q]);
+                        }
+                    }
+                    if (f_row) {
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) o[q] += d.row_add[(int64_t)ho * Nout + n + q];
                     }
                     if (f_res) {
                         float rr[4];
