@@ -444,11 +444,16 @@ void encode(Run& r, const Dims& d, const Bufs& b, const float* wav) {
     }
     struct Pending { const double* st = nullptr; const float* w = nullptr; const float* b = nullptr; };
     Pending pf, pt;
-    auto ln = [&](float* x, int64_t N, const float* w, const float* bb, Pending* pend, void* out) {
+    auto ln2 = [&](float* x, int64_t N, const float* w, const float* bb, Pending* pend, void* out, const float* w2,
+                   const float* b2, void* out2) {
         LnDesc l;
         l.x = x; l.nb = (int)B; l.N = N; l.C = 512; l.w = w; l.b = bb; l.out = out; l.out_bf16 = ab;
         if (pend && pend->st) { l.gn_stats = pend->st; l.gn_w = pend->w; l.gn_b = pend->b; *pend = Pending(); }
+        l.w2 = w2; l.b2 = b2; l.out2 = out2;
         layernorm_launch(l, r.s);
+    };
+    auto ln = [&](float* x, int64_t N, const float* w, const float* bb, Pending* pend, void* out) {
+        ln2(x, N, w, bb, pend, out, nullptr, nullptr, nullptr);
     };
     // attention + FFN of one branch given LN'ed query rows Hq and key/value source (projected inside)
     auto block = [&](const TLayerW& L, float* X, int64_t N, void* Hq, void* Hkv, int64_t Nk, Pending* pend, bool tb) {
@@ -523,12 +528,13 @@ void encode(Run& r, const Dims& d, const Bufs& b, const float* wav) {
         } else {
             join();
             // all four norms read the pre-layer X / XT (time branch attends to old_x, demucs transformer.py)
+            // (bf16 mode: each pair is one pass over X / XT with two affines, layernorm_launch's out2)
             r.s = s_f;
-            ln(b.X, d.Nf, Lf.n1w, Lf.n1b, &pf, b.H[0]);      // applies pending GroupNorm to X
-            ln(b.X, d.Nf, Lt.n2w, Lt.n2b, nullptr, b.H[1]);  // kv of the time branch = norm2_t(old_x)
+            ln2(b.X, d.Nf, Lf.n1w, Lf.n1b, &pf, b.H[0], Lt.n2w, Lt.n2b, b.H[1]);   // pending GN applied to X; norm1(x) and
+                                                                                // the time branch's kv = norm2_t(old_x)
             r.s = s_t;
-            ln(b.XT, d.Nt, Lt.n1w, Lt.n1b, &pt, b.H[2]);     // applies pending GroupNorm to XT
-            ln(b.XT, d.Nt, Lf.n2w, Lf.n2b, nullptr, b.H[3]); // kv of the freq branch = norm2(xt)
+            ln2(b.XT, d.Nt, Lt.n1w, Lt.n1b, &pt, b.H[2], Lf.n2w, Lf.n2b, b.H[3]);  // norm1_t(xt) and the freq branch's kv
+                                                                                // = norm2(xt)
             join();
             r.s = s_f;
             block(Lf, b.X, d.Nf, b.H[0], b.H[3], d.Nt, &pf, false);

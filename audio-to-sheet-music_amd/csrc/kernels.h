@@ -62,6 +62,9 @@ struct LnDesc {
     const double* gn_stats = nullptr; const float* gn_w = nullptr; const float* gn_b = nullptr;
     const float* pos = nullptr;
     void* out = nullptr; int out_bf16 = 0;
+    // optional second affine of the same normalised rows -> out2 (C = 512, bf16, no pos): the cross layers' two
+    // norms of one input (forward.cpp), one read of x instead of two
+    const float* w2 = nullptr; const float* b2 = nullptr; void* out2 = nullptr;
 };
 void layernorm_launch(const LnDesc& d, hipStream_t s);
 // y = bf16(x), n % 8 == 0 (round to nearest even)

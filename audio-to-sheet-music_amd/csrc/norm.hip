@@ -363,9 +363,13 @@ __global__ __launch_bounds__(256) void layernorm_rows_kernel(const LnDesc d) {
         const int64_t row = row0 + r < rows ? row0 + r : rows - 1;
         ld8(d.x + row * C + 8 * lane, v[r]);
     }
-    float wv[8], bv[8];
+    float wv[8], bv[8], wv2[8], bv2[8];
     ld8(d.w + 8 * lane, wv);
     ld8(d.b + 8 * lane, bv);
+    if (d.out2) {
+        ld8(d.w2 + 8 * lane, wv2);
+        ld8(d.b2 + 8 * lane, bv2);
+    }
     if (d.gn_stats) {
         float gw[8], gb[8];
         ld8(d.gn_w + 8 * lane, gw);
@@ -400,6 +404,13 @@ __global__ __launch_bounds__(256) void layernorm_rows_kernel(const LnDesc d) {
         float y[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) y[j] = (v[r][j] - mean) * rstd * wv[j] + bv[j] + pv[j];
+        if (d.out2) {
+            float y2[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) y2[j] = (v[r][j] - mean) * rstd * wv2[j] + bv2[j];
+            reinterpret_cast<uint4*>((bf16_t*)d.out2 + row * C)[lane] =
+                make_uint4(pack2bf(y2[0], y2[1]), pack2bf(y2[2], y2[3]), pack2bf(y2[4], y2[5]), pack2bf(y2[6], y2[7]));
+        }
         if (d.out_bf16) {
             reinterpret_cast<uint4*>((bf16_t*)d.out + row * C)[lane] =
                 make_uint4(pack2bf(y[0], y[1]), pack2bf(y[2], y[3]), pack2bf(y[4], y[5]), pack2bf(y[6], y[7]));
@@ -415,14 +426,24 @@ __global__ __launch_bounds__(256) void layernorm_rows_kernel(const LnDesc d) {
 // 1, 2 and 4 within noise (tools/gpu_r03f.sh)
 constexpr int LN_RW = 4;
 
-void layernorm_launch(const LnDesc& d, hipStream_t s) {
-    const int64_t rows = (int64_t)d.nb * d.N;
+void layernorm_launch(const LnDesc& d0, hipStream_t s) {
+    const int64_t rows = (int64_t)d0.nb * d0.N;
+    LnDesc d = d0;
+    if (d.out2 && !(d.C == 512 && d.out_bf16 && !d.pos)) {   // (only the C = 512 bf16 row kernel has out2)
+        LnDesc d2 = d0;
+        d2.gn_stats = nullptr; d2.w = d0.w2; d2.b = d0.b2; d2.out = d0.out2; d2.out2 = nullptr; d2.pos = nullptr;
+        d.out2 = nullptr;
+        layernorm_launch(d, s);
+        layernorm_launch(d2, s);          // reads x after the first launch applied the pending GroupNorm
+        return;
+    }
     if (d.C == 512) {
         const dim3 grid((unsigned)((rows + 4 * LN_RW - 1) / (4 * LN_RW)));
         KScope ks(s);
         if (ks.on()) {
             double by = (double)rows * d.C * (4 + (d.out_bf16 ? 2 : 4)) + (d.gn_stats ? (double)rows * d.C * 4 : 0.0);
             if (d.pos) by += (double)d.N * d.C * 4;
+            if (d.out2) by += (double)rows * d.C * 2;
             ks.begin(klabel("layernorm_rows_kernel<%d>", LN_RW), 0.0, by);
         }
         hipLaunchKernelGGL(layernorm_rows_kernel<LN_RW>, grid, dim3(256), 0, s, d);

@@ -194,6 +194,9 @@ def main():
     ap.add_argument("--no-extras", action="store_true", help="skip the SDR, f32 and section measurements")
     ap.add_argument("--dump-kernels", default=None, help="write the warmup step's per-kernel profile (JSON)")
     ap.add_argument("--kernel", default=None, help="roofline kernel (default: largest summed time in warmup)")
+    ap.add_argument("--pipelines", type=int, default=1,
+                    help="N = 1: run the steps as this many concurrent forward pipelines (each its own context, "
+                         "workspace, input batch, stream and graph), step i on pipeline i %% n")
     ap.add_argument("--eager", action="store_true",
                     help="launch every step's kernels from the host instead of replaying the captured HIP graph")
     ap.add_argument("--segments", type=int, default=0,
@@ -234,8 +237,27 @@ def main():
     graph = None
     if world == 1 and not args.eager:
         graph, _ = model.capture_prompts(wav, STEMS, out=out)
+    # further pipelines (N = 1, --pipelines > 1): own model context, batch, output, stream and graph each
+    pipes = []
+    if world == 1 and graph is not None and args.pipelines > 1:
+        for k in range(1, args.pipelines):
+            mk = AudioTextHTDemucs(dtype=args.dtype, text_table={s: table[i] for i, s in enumerate(STEMS)},
+                                   decode_items=B * len(STEMS))
+            mk.load_state_dict(sd)
+            mk = mk.to(dev).eval()
+            wk = torch.as_tensor(synthetic_batch(B, SEG, seed0=1000 + B * (world + k))).to(dev)
+            gk, _ = mk.capture_prompts(wk, STEMS)
+            pipes.append((torch.cuda.Stream(dev), gk, mk, wk))
+    nstep = [0]
 
     def step():
+        if pipes:
+            k = nstep[0] % (len(pipes) + 1)
+            nstep[0] += 1
+            if k > 0:
+                with torch.cuda.stream(pipes[k - 1][0]):
+                    return pipes[k - 1][1].replay()
+            return graph.replay()
         if graph is not None:
             return graph.replay()
         if world == 1:
@@ -285,6 +307,7 @@ def main():
 
     barrier()
     torch.cuda.synchronize()
+    nstep[0] = 0
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -390,7 +413,8 @@ def main():
                                   if world > 1 else ""),
                    "global_batch": N, "seq_len": SEG, "prompts": 4, "parallelism": f"segment-sharded dp{world}",
                    "gather_timed": world > 1,
-                   "launch": "hipGraph replay of one athd_forward_prompts" if graph is not None else "eager"},
+                   "launch": "hipGraph replay of one athd_forward_prompts" if graph is not None else "eager",
+                   "pipelines": len(pipes) + 1},
         "stems_per_s": round(4 * value, 3),
         "roofline": roofline,
         "step_essential_tflops": round(step_tf, 2),
