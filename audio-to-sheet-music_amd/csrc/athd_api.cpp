@@ -295,18 +295,52 @@ int athd_finalize(athd_ctx* c) {
         }
     }
     // ---- text cross-attention (closed form: single key => softmax == 1) ----
-    c->ta_vw = c->up_key("text_attn.v_proj.weight");
-    c->ta_vb = c->up_key("text_attn.v_proj.bias");
+    // v = Wv t + bv, vi = Wiv v + biv (the value third of in_proj), a = Wo vi + bo, c0 = W0 a + b0: affine in t, composed
+    // in double into a = Ma t + ma and c0 = Mc t + mc (384 x 512), uploaded transposed for text_vec_kernel
     {
-        const auto& w = c->W("text_attn.attn.in_proj_weight").v;
-        const auto& b = c->W("text_attn.attn.in_proj_bias").v;
-        c->ta_ivw = c->up_f32(std::vector<float>(w.begin() + 768 * 384, w.end()));
-        c->ta_ivb = c->up_f32(std::vector<float>(b.begin() + 768, b.end()));
+        const auto& wv = c->W("text_attn.v_proj.weight").v;          // [384][512]
+        const auto& bv = c->W("text_attn.v_proj.bias").v;
+        const auto& wi = c->W("text_attn.attn.in_proj_weight").v;     // [1152][384]: rows 768.. = value
+        const auto& bi = c->W("text_attn.attn.in_proj_bias").v;
+        const auto& wo = c->W("text_attn.attn.out_proj.weight").v;    // [384][384]
+        const auto& bo = c->W("text_attn.attn.out_proj.bias").v;
+        const auto& w0 = c->W("text_attn.out_mlp.0.weight").v;        // [384][384]
+        const auto& b0 = c->W("text_attn.out_mlp.0.bias").v;
+        constexpr int D = 384, TD = 512;
+        // M' = L . M, m' = L . m + l for L [D][D], M [D][TD]
+        auto compose = [&](const float* L, const float* l, const std::vector<double>& M, const std::vector<double>& m,
+                           std::vector<double>& Mo, std::vector<double>& mo) {
+            Mo.assign((size_t)D * TD, 0.0);
+            mo.assign(D, 0.0);
+            for (int r = 0; r < D; ++r) {
+                double* row = &Mo[(size_t)r * TD];
+                double acc = l[r];
+                for (int q = 0; q < D; ++q) {
+                    const double lv = L[(size_t)r * D + q];
+                    const double* mr = &M[(size_t)q * TD];
+                    for (int k = 0; k < TD; ++k) row[k] += lv * mr[k];
+                    acc += lv * m[q];
+                }
+                mo[r] = acc;
+            }
+        };
+        std::vector<double> M0((size_t)D * TD), m0(D), M1, m1, Ma, ma, Mc, mc;
+        for (size_t i = 0; i < M0.size(); ++i) M0[i] = wv[i];
+        for (int r = 0; r < D; ++r) m0[r] = bv[r];
+        compose(wi.data() + 768 * 384, bi.data() + 768, M0, m0, M1, m1);
+        compose(wo.data(), bo.data(), M1, m1, Ma, ma);
+        compose(w0.data(), b0.data(), Ma, ma, Mc, mc);
+        auto upT = [&](const std::vector<double>& M) {
+            std::vector<float> t((size_t)TD * D);
+            for (int r = 0; r < D; ++r)
+                for (int k = 0; k < TD; ++k) t[(size_t)k * D + r] = (float)M[(size_t)r * TD + k];
+            return c->up_f32(t);
+        };
+        c->ta_maT = upT(Ma);
+        c->ta_mcT = upT(Mc);
+        c->ta_ma = c->up_f32(std::vector<float>(ma.begin(), ma.end()));
+        c->ta_mc = c->up_f32(std::vector<float>(mc.begin(), mc.end()));
     }
-    c->ta_ow = c->up_key("text_attn.attn.out_proj.weight");
-    c->ta_ob = c->up_key("text_attn.attn.out_proj.bias");
-    c->ta_m0w = c->up_key("text_attn.out_mlp.0.weight");
-    c->ta_m0b = c->up_key("text_attn.out_mlp.0.bias");
     c->ta_m2b = c->up_key("text_attn.out_mlp.2.bias");
     c->mlp0 = c->lin_gemm("text_attn.out_mlp.0.weight", "text_attn.out_mlp.0.bias");
     c->mlp2 = c->lin_gemm("text_attn.out_mlp.2.weight", "text_attn.out_mlp.2.bias");

@@ -143,8 +143,9 @@ struct athd_ctx {
     GemmW up, down, up_t, down_t;
     float *nin_w, *nin_b, *nint_w, *nint_b;
     TLayerW L[5], Lt[5];
-    float *ta_vw, *ta_vb, *ta_ivw, *ta_ivb, *ta_ow, *ta_ob, *ta_nw, *ta_nb;
-    float *ta_m0w, *ta_m0b, *ta_m2b;      // out_mlp.0 weight / bias and out_mlp.2 bias in f32 (per-prompt row biases)
+    // text cross-attention row vectors (text_vec_kernel): a = Ma t + ma, c0 = W0 a + b0 = Mc t + mc, composed in double
+    // at finalize and stored transposed [512][384]; out_mlp.2 bias; norm_out affine
+    float *ta_maT, *ta_ma, *ta_mcT, *ta_mc, *ta_m2b, *ta_nw, *ta_nb;
     GemmW mlp0, mlp2;
     DecW fdec[4], tdec[4];
     float *fout_w, *fout_b, *tout_w, *tout_b;

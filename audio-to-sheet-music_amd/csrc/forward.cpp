@@ -334,7 +334,9 @@ void encode(Run& r, const Dims& d, const Bufs& b, const float* wav) {
 
     // ---- encoders (ATHTDemucs_v2.py:197-217; HEncLayer + DConv) ----
     // fork: the time encoder runs on the second stream (own ybuf_t / hbuf_t) beside the frequency encoder; the
-    // branches join before the transformer's up-projections
+    // branches join before the transformer's up-projections.  (The waveform statistics stay before the fork: run as
+    // the time stream's first kernels, beside the STFT, they measured 3 % slower per step - the time encoder's
+    // kernels then take CUs ahead of the frequency encoder's level-0 rows.)
     if (!second_stream(r)) return;
     hipStream_t const s_enc = r.s, s_tenc = serial_branches(r) ? r.s : c->s_time;
     (void)hipEventRecord(c->ev_f, s_enc);
@@ -542,17 +544,23 @@ void encode(Run& r, const Dims& d, const Bufs& b, const float* wav) {
             block(Lt, b.XT, d.Nt, b.H[2], b.H[1], d.Nf, &pt, true);
         }
     }
-    gn_apply_launch(b.X, (int)B, d.Nf, 512, pf.st, pf.w, pf.b, s_f);
-    gn_apply_launch(b.XT, (int)B, d.Nt, 512, pt.st, pt.w, pt.b, s_t);
+    // the last layer's pending GroupNorm: in the bf16 mode applied by the downsamplers' A load (gemm2 a_gn; X / XT
+    // have no other reader), in the f32 mode written back first
+    if (!r.actbf) {
+        gn_apply_launch(b.X, (int)B, d.Nf, 512, pf.st, pf.w, pf.b, s_f);
+        gn_apply_launch(b.XT, (int)B, d.Nt, 512, pt.st, pt.w, pt.b, s_t);
+    }
     {
         r.s = s_t;                               // the time branch's channel downsampler on its own stream
         GemmDesc gt = r.lin(c->down_t, b.XT, 0, (int)B, d.Nt, 512);
         gt.C = b.xt_enc;
+        if (r.actbf) { gt.a_gn_stats = pt.st; gt.a_gn_count = d.Nt * 512; gt.a_gn_w = pt.w; gt.a_gn_b = pt.b; }
         r.gemm(gt, "downsampler_t");
         if (b.xt_enc_b) to_bf16_launch(b.xt_enc, b.xt_enc_b, B * d.Nt * 384, s_t);
         r.s = s_f;
         GemmDesc g = r.lin(c->down, b.X, 0, (int)B, d.Nf, 512);
         g.C = b.x_enc;
+        if (r.actbf) { g.a_gn_stats = pf.st; g.a_gn_count = d.Nf * 512; g.a_gn_w = pf.w; g.a_gn_b = pf.b; }
         r.gemm(g, "downsampler");
         if (b.x_enc_b) to_bf16_launch(b.x_enc, b.x_enc_b, B * d.Nf * 384, s_f);
     }
@@ -617,8 +625,8 @@ void decode_chunk(Run& r, const Dims& d, const Bufs& b, int64_t s0, int64_t Bc, 
     const int64_t Ts = d.Tspec;
     const int ab = r.actbf ? 1 : 0;
     // ---- text cross-attention, closed form (ATHTDemucs_v2.py:38-58) ----
-    text_vec_launch(text_per_item ? text + s0 * 512 : text, NI, P, text_per_item ? 1 : 0, c->ta_vw, c->ta_vb, c->ta_ivw,
-                    c->ta_ivb, c->ta_ow, c->ta_ob, c->ta_m0w, c->ta_m0b, c->ta_m2b, b.avec, b.tc0, b.tc2, r.s);
+    text_vec_launch(text_per_item ? text + s0 * 512 : text, NI, P, text_per_item ? 1 : 0, c->ta_maT, c->ta_ma, c->ta_mcT,
+                    c->ta_mc, c->ta_m2b, b.avec, b.tc0, b.tc2, r.s);
     // The prompt enters only through the row vector a = attn_out (one key: softmax == 1), so with u = x + a
     // (ATHTDemucs_v2.py:46-48):  h = GELU(W0 u + b0) = GELU(W0 x + c0),  y = u + W2 h + b2 = x + W2 h + c2  (c0, c2 per
     // prompt, text_vec_kernel).  text.mlp0 multiplies the SEGMENT's x once and its epilogue writes the P prompts' h

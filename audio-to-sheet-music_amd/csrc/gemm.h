@@ -48,6 +48,12 @@ struct GemmDesc {
     int ntaps = 1, in_stride = 1, in_off = 0, dil = 1;
     int H_out = 1;            // output rows computed per batch
     const float* a_norm = nullptr;    // optional per-batch {sub, div} on in-bounds A: (a - sub[b]) / div[b]
+    // optional GroupNorm(1) on f32 A as it is loaded (gemm2's fp32-A path, ntaps == 1): a' = (a - mean[b]) * rstd[b] *
+    // a_gn_w[ci] + a_gn_b[ci], statistics {sum, sumsq} over a_gn_count elements per batch
+    const double* a_gn_stats = nullptr;
+    int64_t a_gn_count = 0;
+    const float* a_gn_w = nullptr;
+    const float* a_gn_b = nullptr;
     // B operand (packed weights [N][Kp]) and bias
     const void* Wp = nullptr;
     int N = 0, K = 0, Kp = 0;

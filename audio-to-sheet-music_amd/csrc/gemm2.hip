@@ -74,13 +74,29 @@ __global__ __launch_bounds__(256) void gemm2_kernel(const GemmDesc d) {
     const bool flat = d.C_in < 8;                             // (gemm2_supported: fp32 A, a_hs == C_in, dil 1)
     float4 ra[AQ][2];   // fp32-A staging
     unsigned rv[AQ];    // per-element in-bounds mask (normalisation applies to in-bounds values only; padding stays 0)
+    int ra_ci = 0;      // channel of the staged chunk (A GroupNorm)
+    float agm[AQ], agr[AQ];                                   // A GroupNorm mean / rstd of each staged row's batch
     (void)ra;
     (void)rv;
+    (void)ra_ci;
+    if constexpr (!A_BF16) {
+        if (d.a_gn_stats) {
+#pragma unroll
+            for (int q = 0; q < AQ; ++q) {
+                const double m = d.a_gn_stats[2 * a_b[q]] / (double)d.a_gn_count;
+                double var = d.a_gn_stats[2 * a_b[q] + 1] / (double)d.a_gn_count - m * m;
+                if (var < 0) var = 0;
+                agm[q] = (float)m;
+                agr[q] = (float)(1.0 / sqrt(var + 1e-5));
+            }
+        }
+    }
 
     auto issue = [&](int kt, int st) {
         char* sA = smem + st * STAGE;
         char* sB = sA + BM * ROWB;
         const bool kok = k_cur < d.K;
+        ra_ci = ci;
 #pragma unroll
         for (int q = 0; q < AQ; ++q) {
             const int row = a_h0[q] + tap * d.dil;
@@ -145,6 +161,16 @@ __global__ __launch_bounds__(256) void gemm2_kernel(const GemmDesc d) {
 #pragma unroll
                     for (int j = 0; j < 8; ++j) v[j] = ((rv[q] >> j) & 1u) ? (v[j] - sub) / dv : 0.f;
                 }
+                if (d.a_gn_stats && rv[q]) {           // (ntaps == 1: the chunk is channels ra_ci .. + 7)
+                    const float4 w0 = *reinterpret_cast<const float4*>(d.a_gn_w + ra_ci);
+                    const float4 w1 = *reinterpret_cast<const float4*>(d.a_gn_w + ra_ci + 4);
+                    const float4 c0 = *reinterpret_cast<const float4*>(d.a_gn_b + ra_ci);
+                    const float4 c1 = *reinterpret_cast<const float4*>(d.a_gn_b + ra_ci + 4);
+                    const float gw[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+                    const float gb[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) v[j] = ((rv[q] >> j) & 1u) ? (v[j] - agm[q]) * agr[q] * gw[j] + gb[j] : 0.f;
+                }
                 bf16_t h[8];
 #pragma unroll
                 for (int j = 0; j < 8; ++j) h[j] = f2bf(v[j]);
@@ -204,6 +230,7 @@ bool gemm2_supported(const GemmDesc& d) {
         return false;
     if (flat && (d.a_bs % 4 != 0 || d.a_ld % 4 != 0)) return false;      // 16-B aligned chunk starts
     if (d.a_bf16 && d.a_norm) return false;
+    if (d.a_gn_stats && (d.a_bf16 || d.ntaps != 1 || d.C_in % 8 != 0 || flat)) return false;
     if (d.act == ACT_GLU && d.N % 32 != 0) return false;
     return true;
 }

@@ -450,21 +450,33 @@ ATHD_DEV void gemm_epilogue_res(const GemmDesc& d, const f32x4_t (&acc)[TM][TN],
     const float* res = (const float*)d.res;
     float* C = (float*)d.C;
     float* sink = reinterpret_cast<float*>(g_epi_sink + lane);
-    float4 rc[TN], rn[TN];
+    // residual ring: the loads of row fragment i + RD - 1 are issued before the stores of fragment i, so RD - 1
+    // fragments of loads are in flight across the stores (round 2: one; the epilogue then streamed at ~20 GB/s per
+    // CU, an HBM round trip per fragment).  The K-loop's operand fragments are dead here, so the ring's registers
+    // do not raise the kernel's VGPR count.
+#ifndef ATHD_RES_RD
+#define ATHD_RES_RD 3      // 3: two fragments ahead (244-246 VGPRs; 4 spills in the K-loop kernels)
+#endif
+    constexpr int RD = TM < ATHD_RES_RD ? TM : ATHD_RES_RD;
+    float4 rr[RD][TN];
 #pragma unroll
-    for (int j = 0; j < TN; ++j) rc[j] = *reinterpret_cast<const float4*>(res + rb[0] + ncol[j]);
+    for (int i = 0; i + 1 < RD; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) rr[i][j] = *reinterpret_cast<const float4*>(res + rb[i] + ncol[j]);
     float p1[TM], p2[TM];
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
-        if (i + 1 < TM) {
+        if (i + RD - 1 < TM) {
 #pragma unroll
-            for (int j = 0; j < TN; ++j) rn[j] = *reinterpret_cast<const float4*>(res + rb[i + 1] + ncol[j]);
+            for (int j = 0; j < TN; ++j)
+                rr[(i + RD - 1) % RD][j] = *reinterpret_cast<const float4*>(res + rb[i + RD - 1] + ncol[j]);
         }
         float s1 = 0.f, s2 = 0.f;
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
-            const float4 o = make_float4(rc[j].x + sc[j].x * (acc[i][j][0] + bj[j].x), rc[j].y + sc[j].y * (acc[i][j][1] + bj[j].y),
-                                         rc[j].z + sc[j].z * (acc[i][j][2] + bj[j].z), rc[j].w + sc[j].w * (acc[i][j][3] + bj[j].w));
+            const float4 rc = rr[i % RD][j];
+            const float4 o = make_float4(rc.x + sc[j].x * (acc[i][j][0] + bj[j].x), rc.y + sc[j].y * (acc[i][j][1] + bj[j].y),
+                                         rc.z + sc[j].z * (acc[i][j][2] + bj[j].z), rc.w + sc[j].w * (acc[i][j][3] + bj[j].w));
             const bool st = ok[i] && colok[j];
             if (f_stats && st) {
                 s1 += (o.x + o.y) + (o.z + o.w);
@@ -474,10 +486,6 @@ ATHD_DEV void gemm_epilogue_res(const GemmDesc& d, const f32x4_t (&acc)[TM][TN],
         }
         p1[i] = s1;
         p2[i] = s2;
-        if (i + 1 < TM) {
-#pragma unroll
-            for (int j = 0; j < TN; ++j) rc[j] = rn[j];
-        }
     }
     if constexpr (f_stats) {
         if (one_group) {

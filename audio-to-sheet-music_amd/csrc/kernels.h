@@ -71,9 +71,8 @@ void layernorm_launch(const LnDesc& d, hipStream_t s);
 void to_bf16_launch(const float* x, uint16_t* y, int64_t n, hipStream_t s);
 // a[item] = out_proj(in_v(v_proj(text[item])))   (TextCrossAttention closed form, 384 <- 512), and the prompt's
 // out_mlp row biases c0[item] = W0 a + b0, c2[item] = a + b2 (c0 == nullptr: a only)
-void text_vec_launch(const float* text, int NI, int P, int text_per_item, const float* wv, const float* bv,
-                     const float* wiv, const float* biv, const float* wo, const float* bo, const float* w0,
-                     const float* b0, const float* b2, float* a, float* c0, float* c2, hipStream_t s);
+void text_vec_launch(const float* text, int NI, int P, int text_per_item, const float* maT, const float* ma,
+                     const float* mcT, const float* mc, const float* b2, float* a, float* c0, float* c2, hipStream_t s);
 // decoder merge: out[item][ho][w][c] = resize_H(act(GN(src)))[ho][w][c] + 0.1 * resize_H(skip[item/P][..][c])
 struct MergeDesc {
     const void* src = nullptr; int src_bf16 = 0; int H_src = 0;   // logical ConvT output rows

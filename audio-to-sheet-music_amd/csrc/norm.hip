@@ -166,15 +166,15 @@ __global__ __launch_bounds__(256) void gn_gelu_mom_kernel(const float* __restric
     for (int j = 0; j < H; ++j) {
         cfloat* gr = (cfloat*)(gram + j * H);
         asm volatile("" : "+s"(gr), "+v"(qf));              // row j's loads after row j-1's products
-        float t = 0.f;
+        float t4[4] = {0.f, 0.f, 0.f, 0.f};                 // 4 independent chains (the FMA latency, not issue)
 #pragma unroll
         for (int k0 = 0; k0 < H; k0 += 24) {               // (at most 24 row values in SGPRs at a time)
             cfloat* gk = gr + k0;
-            if (k0 > 0) asm volatile("" : "+s"(gk), "+v"(t));
+            if (k0 > 0) asm volatile("" : "+s"(gk), "+v"(t4[0]));
 #pragma unroll
-            for (int k = 0; k < 24; ++k) t = fmaf(gk[k], x[k0 + k], t);
+            for (int k = 0; k < 24; ++k) t4[k & 3] = fmaf(gk[k], x[k0 + k], t4[k & 3]);
         }
-        qf = fmaf(x[j], t, qf);
+        qf = fmaf(x[j], (t4[0] + t4[1]) + (t4[2] + t4[3]), qf);
         lv = fmaf(gr[H * (H - j) + j], x[j], lv);            // gram[H*H + j]      = (W^T b)_j
         lw = fmaf(gr[H * (H - j) + H + j], x[j], lw);        // gram[H*H + H + j]  = (W^T 1)_j
     }
@@ -479,60 +479,54 @@ void to_bf16_launch(const float* x, uint16_t* y, int64_t n, hipStream_t s) {
     hipLaunchKernelGGL(to_bf16_kernel, dim3(blocks), dim3(256), 0, s, x, y, n8);
 }
 
-__global__ __launch_bounds__(256) void text_vec_kernel(const float* __restrict__ text, int P, int per_item,
-                                                       const float* __restrict__ wv, const float* __restrict__ bv,
-                                                       const float* __restrict__ wiv, const float* __restrict__ biv,
-                                                       const float* __restrict__ wo, const float* __restrict__ bo,
-                                                       const float* __restrict__ w0, const float* __restrict__ b0,
+// The chain v = Wv t + bv -> vi = Wiv v + biv -> a = Wo vi + bo -> c0 = W0 a + b0 is affine in the text row t, so
+// athd_finalize composes it in double into two 384 x 512 maps: a = Ma t + ma, c0 = Mc t + mc (stored transposed,
+// [k][o]).  Grid (rows, 2 maps x 6 chunks of 64 outputs): lane o of a chunk sums a quarter of k per wave (coalesced
+// [k][o] reads), the quarters meet in LDS.  text_per_item = 0 (forward_prompts): one row per PROMPT, written for
+// every item of that prompt (item % P).  (Round 2 ran the four matvecs serially per item with [o][k] reads: 110 us.)
+__global__ __launch_bounds__(256) void text_vec_kernel(const float* __restrict__ text, int NI, int P, int per_item,
+                                                       const float* __restrict__ maT, const float* __restrict__ ma,
+                                                       const float* __restrict__ mcT, const float* __restrict__ mc,
                                                        const float* __restrict__ b2, float* __restrict__ a,
                                                        float* __restrict__ c0, float* __restrict__ c2) {
     constexpr int D = 384, TD = 512;
     __shared__ float t[TD];
-    __shared__ float v[D];
-    __shared__ float vi[D];
-    __shared__ float av[D];
-    const int item = blockIdx.x;
-    const float* tp = text + (int64_t)(per_item ? item : (item % P)) * TD;
+    __shared__ float red[4][64];
+    const int src = blockIdx.x;                       // item (per_item) or prompt
+    const int step = per_item ? NI : P;               // items sharing this row: src, src + step, ...
+    const int mat = blockIdx.y / 6, o = (blockIdx.y % 6) * 64 + (threadIdx.x & 63), kq = threadIdx.x >> 6;
+    const float* tp = text + (int64_t)src * TD;
     for (int i = threadIdx.x; i < TD; i += 256) t[i] = tp[i];
     __syncthreads();
-    for (int o = threadIdx.x; o < D; o += 256) {
-        float s = 0.f;
-        for (int k = 0; k < TD; ++k) s += wv[(int64_t)o * TD + k] * t[k];
-        v[o] = s + bv[o];
-    }
+    const float* mT = mat == 0 ? maT : mcT;
+    float s = 0.f;
+#pragma unroll 8
+    for (int k = kq * 128; k < kq * 128 + 128; ++k) s += mT[(int64_t)k * D + o] * t[k];
+    red[kq][threadIdx.x & 63] = s;
     __syncthreads();
-    for (int o = threadIdx.x; o < D; o += 256) {
-        float s = 0.f;
-        for (int k = 0; k < D; ++k) s += wiv[(int64_t)o * D + k] * v[k];
-        vi[o] = s + biv[o];
-    }
-    __syncthreads();
-    for (int o = threadIdx.x; o < D; o += 256) {
-        float s = 0.f;
-        for (int k = 0; k < D; ++k) s += wo[(int64_t)o * D + k] * vi[k];
-        av[o] = s + bo[o];
-        a[(int64_t)item * D + o] = av[o];
-    }
-    if (!c0) return;                      // (block-uniform)
-    __syncthreads();
-    // the prompt's row biases of the out_mlp (ATHTDemucs_v2.py:46-48 with queries + a, a constant over tokens):
-    //   mlp0(x + a) = W0 x + (W0 a + b0)   ->  c0 = W0 a + b0
-    //   (x + a) + mlp2(h) = x + W2 h + (a + b2)   ->  c2 = a + b2
-    for (int o = threadIdx.x; o < D; o += 256) {
-        float s = 0.f;
-        for (int k = 0; k < D; ++k) s += w0[(int64_t)o * D + k] * av[k];
-        c0[(int64_t)item * D + o] = s + b0[o];
-        c2[(int64_t)item * D + o] = av[o] + b2[o];
+    if (threadIdx.x >= 64) return;
+    const float v = ((red[0][threadIdx.x] + red[1][threadIdx.x]) + (red[2][threadIdx.x] + red[3][threadIdx.x])) +
+                    (mat == 0 ? ma[o] : mc[o]);
+    if (mat == 0) {
+        //   (x + a) + mlp2(h) = x + W2 h + (a + b2)   ->  c2 = a + b2   (ATHTDemucs_v2.py:46-48)
+        const float r2 = v + b2[o];
+        for (int it = src; it < NI; it += step) {
+            a[(int64_t)it * D + o] = v;
+            c2[(int64_t)it * D + o] = r2;
+        }
+    } else if (c0) {
+        //   mlp0(x + a) = W0 x + (W0 a + b0)   ->  c0 = W0 a + b0
+        for (int it = src; it < NI; it += step) c0[(int64_t)it * D + o] = v;
     }
 }
 
-void text_vec_launch(const float* text, int NI, int P, int text_per_item, const float* wv, const float* bv,
-                     const float* wiv, const float* biv, const float* wo, const float* bo, const float* w0,
-                     const float* b0, const float* b2, float* a, float* c0, float* c2, hipStream_t s) {
+void text_vec_launch(const float* text, int NI, int P, int text_per_item, const float* maT, const float* ma,
+                     const float* mcT, const float* mc, const float* b2, float* a, float* c0, float* c2, hipStream_t s) {
+    const int nsrc = text_per_item ? NI : (P < NI ? P : NI);
     KScope ks(s);
-    if (ks.on()) ks.begin("text_vec_kernel", 2.0 * NI * (512.0 * 384 + 384.0 * 384 * 3), (512.0 * 384 + 384.0 * 384 * 3) * 4);
-    hipLaunchKernelGGL(text_vec_kernel, dim3(NI), dim3(256), 0, s, text, P, text_per_item, wv, bv, wiv, biv, wo, bo, w0,
-                       b0, b2, a, c0, c2);
+    if (ks.on()) ks.begin("text_vec_kernel", 2.0 * nsrc * 2 * 512.0 * 384, 2 * 512.0 * 384 * 4);
+    hipLaunchKernelGGL(text_vec_kernel, dim3(nsrc, 12), dim3(256), 0, s, text, NI, P, text_per_item, maT, ma, mcT, mc, b2,
+                       a, c0, c2);
 }
 
 // --------------------------------------------------------------------------------------------- decoder merge
