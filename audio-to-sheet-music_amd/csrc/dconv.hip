@@ -305,4 +305,158 @@ int dconv_small_launch(void* x, int x_bf16, float* h, int64_t nb, int64_t L, int
     return (int)hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------------------------------------
+// Wide levels (C = 192, 384; bf16 mode): the DConv 1x1 apply  x += LayerScale(GLU(GN(W1 hb + b1)))  as a weights-
+// resident MFMA pass (the pattern of convt4.hip) instead of a tiled GEMM: K = H = C/8 (24, 48) is one or two 32-wide
+// K-steps, so the tiled GEMM (gemm3 / gemm5, one K-tile per 256-row tile) was all prologue and epilogue at ~7 GB/s
+// per CU.  Here the packed 1x1 weights ([2C][64] bf16, GLU-interleaved columns, 48 / 96 KB) are loaded into LDS once
+// per workgroup (XOR-swizzled 16-B chunks, conflict-free fragment reads as gemm3), and every wave walks 16-row units
+// with no workgroup barrier: per unit the lane's activation fragment (row m, 8 hidden channels per K-step) comes from
+// global memory, all of the row's residual channels are loaded up front, and the 2C columns are processed one
+// GLU pair (32 packed columns -> 16 output channels) at a time: 2 x KS MFMAs, GroupNorm -> GLU -> LayerScale ->
+// residual on the lane's 4 channels of row m, one 8-B store.
+struct DcApply {
+    const uint16_t* hb;        // [M][H] bf16 GELU(GN(h))
+    const uint16_t* w;         // [2C][kp] packed GLU-interleaved 1x1 weights (kp == 64)
+    const float* bias;         // [2C] packed
+    const double* st;          // per group {sum, sumsq} of the 1x1 output
+    const float* gn_w;         // [2C] packed
+    const float* gn_b;
+    const float* scale;        // [C] LayerScale
+    uint16_t* x;               // [M][C] bf16 residual stream, updated in place
+    int64_t M, L, gn_count;
+    int kp;
+};
+
+template <int C, int NW>
+__global__ __launch_bounds__(NW * 64) void dconv_apply_kernel(const DcApply d) {
+    constexpr int H = C / 8, KS = (H + 31) / 32, NP = C / 16;      // K-steps, GLU pairs (16 output channels each)
+    __shared__ __attribute__((aligned(16))) char wl[2 * C * 128];
+    // per packed column: bias, GroupNorm weight, bias; per output channel: LayerScale
+    __shared__ __attribute__((aligned(16))) float cst[3 * 2 * C + C];
+    for (int i = threadIdx.x; i < 2 * C * 8; i += NW * 64) {
+        const int row = i >> 3, ch = i & 7;
+        const uint4 v = *reinterpret_cast<const uint4*>(d.w + (int64_t)row * d.kp + ch * 8);
+        *reinterpret_cast<uint4*>(wl + row * 128 + ((ch ^ (row & 7)) * 16)) = v;
+    }
+    for (int i = threadIdx.x; i < 2 * C; i += NW * 64) {
+        cst[i] = d.bias[i];
+        cst[2 * C + i] = d.gn_w[i];
+        cst[4 * C + i] = d.gn_b[i];
+    }
+    for (int i = threadIdx.x; i < C; i += NW * 64) cst[6 * C + i] = d.scale[i];
+    __syncthreads();
+    const int lane = threadIdx.x & 63, fr = lane & 15, g = lane >> 4;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t nunits = (d.M + 15) / 16;
+    const int64_t stride = (int64_t)gridDim.x * NW;
+    typedef __attribute__((ext_vector_type(8))) __bf16 bf16v8;
+    auto wfrag = [&](int t, int ks) -> bf16v8 {
+        return *reinterpret_cast<const bf16v8*>(wl + (16 * t + fr) * 128 + (((4 * ks + g) ^ (fr & 7)) * 16));
+    };
+    for (int64_t u = (int64_t)blockIdx.x * NW + wave; u < nunits; u += stride) {
+        const int64_t m = u * 16 + fr;
+        const bool ok = m < d.M;
+        const int64_t mm = ok ? m : d.M - 1;
+        // activation fragments: hidden channels 32 ks + 8 g .. + 7 of row mm (zero past H)
+        bf16v8 af[KS];
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            const int k0 = 32 * ks + 8 * g;
+            af[ks] = k0 < H ? *reinterpret_cast<const bf16v8*>(d.hb + mm * H + k0) : bf16v8{};
+        }
+        // the row's residual channels 16 p + 4 g .. + 3, PG pairs per group; the next group's loads are issued
+        // before the current group's MFMAs (the first group's before the GroupNorm parameters)
+        constexpr int PG = 6, NG = NP / PG;
+        static_assert(NP % PG == 0, "pair groups");
+        const uint16_t* xr = d.x + mm * C + 4 * g;
+        uint2 rr[PG];
+#pragma unroll
+        for (int p = 0; p < PG; ++p) rr[p] = *reinterpret_cast<const uint2*>(xr + 16 * p);
+        float gm, gr;
+        gn_params(d.st, mm / d.L, d.gn_count, gm, gr);
+        uint2* const xo = reinterpret_cast<uint2*>(d.x + mm * C + 4 * g);
+#pragma unroll 1
+        for (int gi = 0; gi < NG; ++gi) {
+            uint2 rn[PG];
+            if (gi + 1 < NG) {
+#pragma unroll
+                for (int p = 0; p < PG; ++p) rn[p] = *reinterpret_cast<const uint2*>(xr + 16 * (PG * (gi + 1) + p));
+            }
+            // (an opaque per-group LDS base: the column constants are read here, not hoisted out of the loops)
+            int cb = 0;
+            asm volatile("v_mov_b32 %0, 0" : "=v"(cb));
+            const float* cs = cst + cb;
+#pragma unroll
+            for (int pp = 0; pp < PG; ++pp) {
+                const int p = PG * gi + pp;
+                f32x4_t aa = {0.f, 0.f, 0.f, 0.f}, ag = aa;
+#pragma unroll
+                for (int ks = 0; ks < KS; ++ks) {
+                    aa = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfrag(2 * p, ks), af[ks], aa, 0, 0, 0);
+                    ag = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfrag(2 * p + 1, ks), af[ks], ag, 0, 0, 0);
+                }
+                const int na = 32 * p + 4 * g, oc = 16 * p + 4 * g;
+                const float4 ba = *reinterpret_cast<const float4*>(cs + na), bg = *reinterpret_cast<const float4*>(cs + na + 16);
+                const float4 wa = *reinterpret_cast<const float4*>(cs + 2 * C + na), wg = *reinterpret_cast<const float4*>(cs + 2 * C + na + 16);
+                const float4 ca = *reinterpret_cast<const float4*>(cs + 4 * C + na), cg = *reinterpret_cast<const float4*>(cs + 4 * C + na + 16);
+                const float4 sc = *reinterpret_cast<const float4*>(cs + 6 * C + oc);
+                const float bav[4] = {ba.x, ba.y, ba.z, ba.w}, bgv[4] = {bg.x, bg.y, bg.z, bg.w};
+                const float wav[4] = {wa.x, wa.y, wa.z, wa.w}, wgv[4] = {wg.x, wg.y, wg.z, wg.w};
+                const float cav[4] = {ca.x, ca.y, ca.z, ca.w}, cgv[4] = {cg.x, cg.y, cg.z, cg.w};
+                const float scv[4] = {sc.x, sc.y, sc.z, sc.w};
+                const uint2 q = rr[pp];
+                const float r4[4] = {__uint_as_float(q.x << 16), __uint_as_float(q.x & 0xFFFF0000u),
+                                     __uint_as_float(q.y << 16), __uint_as_float(q.y & 0xFFFF0000u)};
+                float o[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float a = (aa[e] + bav[e] - gm) * gr * wav[e] + cav[e];
+                    const float gt = (ag[e] + bgv[e] - gm) * gr * wgv[e] + cgv[e];
+                    o[e] = r4[e] + scv[e] * (a * sigmoid_fast(gt));
+                }
+                if (ok) xo[4 * p] = make_uint2(pack2bf(o[0], o[1]), pack2bf(o[2], o[3]));
+            }
+            if (gi + 1 < NG) {
+#pragma unroll
+                for (int p = 0; p < PG; ++p) rr[p] = rn[p];
+            }
+        }
+    }
+}
+
+bool dconv_apply_supported(int C, int H, int kp, int64_t M) {
+    return (C == 192 || C == 384) && H == C / 8 && kp == 64 && M > 0;
+}
+
+int dconv_apply_launch(const uint16_t* hb, const uint16_t* w, int kp, const float* bias, const double* st,
+                       const float* gn_w, const float* gn_b, const float* scale, uint16_t* x, int64_t M, int64_t L,
+                       int C, hipStream_t s) {
+    if (!dconv_apply_supported(C, C / 8, kp, M)) return -1;
+    DcApply d;
+    d.hb = hb; d.w = w; d.bias = bias; d.st = st; d.gn_w = gn_w; d.gn_b = gn_b; d.scale = scale; d.x = x;
+    d.M = M; d.L = L; d.gn_count = L * 2 * C; d.kp = kp;
+    static int cus = 0;
+    if (cus == 0) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        if (cus <= 0) cus = 256;
+    }
+    KScope ks(s);
+    if (ks.on()) {
+        const double H = C / 8;
+        ks.begin(klabel("dconv_apply_kernel<%d>", C), 2.0 * M * 2 * C * H, (double)M * (H * 2 + 2.0 * C * 2));
+    }
+    const int64_t units = (M + 15) / 16;
+    if (C == 192) {      // 48 KB of weights: two 8-wave workgroups per CU
+        const int64_t blocks = std::min<int64_t>(2LL * cus, (units + 7) / 8);
+        hipLaunchKernelGGL((dconv_apply_kernel<192, 8>), dim3((unsigned)blocks), dim3(512), 0, s, d);
+    } else {             // 96 KB: one 16-wave workgroup per CU
+        const int64_t blocks = std::min<int64_t>((int64_t)cus, (units + 15) / 16);
+        hipLaunchKernelGGL((dconv_apply_kernel<384, 16>), dim3((unsigned)blocks), dim3(1024), 0, s, d);
+    }
+    return (int)hipGetLastError();
+}
+
 }  // namespace athd

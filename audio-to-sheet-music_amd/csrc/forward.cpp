@@ -297,7 +297,14 @@ void dconv(Run& r, const EncW& e, void* x, int64_t nb, int64_t L, float* hbuf, u
         }
         g2.act = ACT_GLU; g2.gn_stats = st_y; g2.gn_count = L * 2 * C; g2.gn_w = e.dc.g2w[dd]; g2.gn_b = e.dc.g2b[dd];
         g2.res = x; g2.res_bf16 = ab; g2.res_scale = e.dc.scale[dd];
-        r.gemm(g2, "dconv.conv1x1.apply");
+        // bf16 mode: the weights-resident apply pass (dconv.hip dconv_apply_kernel), else the GEMM with its epilogue
+        int rc = -1;
+        if (hb) {
+            KSite site("dconv.conv1x1.apply");
+            rc = dconv_apply_launch(hbuf_b, (const uint16_t*)e.dc.c1[dd].w, e.dc.c1[dd].Kp, e.dc.c1[dd].bias, st_y,
+                                    e.dc.g2w[dd], e.dc.g2b[dd], e.dc.scale[dd], (uint16_t*)x, nb * L, L, C, r.s);
+        }
+        if (rc != 0) r.gemm(g2, "dconv.conv1x1.apply");
     }
 }
 
