@@ -331,6 +331,7 @@ struct DcApply {
 template <int C, int NW>
 __global__ __launch_bounds__(NW * 64) void dconv_apply_kernel(const DcApply d) {
     constexpr int H = C / 8, KS = (H + 31) / 32, NP = C / 16;      // K-steps, GLU pairs (16 output channels each)
+    constexpr int HS = H % 8 == 0 ? H : (H + 15) / 16 * 16;       // hidden row stride (H = 12: padded to 16)
     __shared__ __attribute__((aligned(16))) char wl[2 * C * 128];
     // per packed column: bias, GroupNorm weight, bias; per output channel: LayerScale
     __shared__ __attribute__((aligned(16))) float cst[3 * 2 * C + C];
@@ -363,7 +364,7 @@ __global__ __launch_bounds__(NW * 64) void dconv_apply_kernel(const DcApply d) {
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
             const int k0 = 32 * ks + 8 * g;
-            af[ks] = k0 < H ? *reinterpret_cast<const bf16v8*>(d.hb + mm * H + k0) : bf16v8{};
+            af[ks] = k0 < H ? *reinterpret_cast<const bf16v8*>(d.hb + mm * HS + k0) : bf16v8{};
         }
         // the row's residual channels 16 p + 4 g .. + 3, PG pairs per group; the next group's loads are issued
         // before the current group's MFMAs (the first group's before the GroupNorm parameters)
@@ -425,8 +426,154 @@ __global__ __launch_bounds__(NW * 64) void dconv_apply_kernel(const DcApply d) {
     }
 }
 
+// Wide levels: the DConv conv3 (C -> H = C/8, 3 taps at dilation dil, zero padding at the GroupNorm row's ends)
+// + the GroupNorm statistics of h, as a weights-resident pass (the pattern above; the tiled 256 x 32 GEMM streamed
+// the taps' 64-wide K-tiles through LDS at ~2 TB/s).  The packed conv3 weights (H rows padded to 16 NT, K = 3C) sit in
+// LDS with XOR-swizzled 16-B chunks; each wave walks a contiguous range of 16-row units (the tap rows +-dil stay in its
+// L2 neighbourhood), loads its B fragments x[m + (tap - 1) dil][32 ks + 8 g ..] straight from global memory, and keeps
+// the GroupNorm sums in fp64 per lane until the group changes (one wave reduction + atomic pair per change).
+struct DcConv3 {
+    const uint16_t* x;         // [M][C] bf16
+    const uint16_t* w;         // [>= 16 NT][kp] packed conv3 weights, K = tap * C + ci
+    const float* bias;         // [H]
+    float* h;                  // [M][H] f32
+    double* st;                // per group {sum, sumsq}
+    int64_t M, L;
+    int kp, dil;
+};
+
+template <int C, int NW>
+__global__ __launch_bounds__(NW * 64) void dconv_conv3_kernel(const DcConv3 d) {
+    constexpr int H = C / 8, NT = (H + 15) / 16, KS = C / 32, K = 3 * C;
+    constexpr int RB = (K / 8 + 7) / 8 * 128;               // LDS row bytes (chunks padded to a multiple of 8: the
+                                                            // XOR swizzle stays inside the row, e.g. C = 96: 36 -> 40)
+    __shared__ __attribute__((aligned(16))) char wl[16 * NT * RB];
+    for (int i = threadIdx.x; i < 16 * NT * (K / 8); i += NW * 64) {
+        const int row = i / (K / 8), q = i % (K / 8);
+        const uint4 v = *reinterpret_cast<const uint4*>(d.w + (int64_t)row * d.kp + q * 8);
+        *reinterpret_cast<uint4*>(wl + row * RB + ((q ^ (row & 7)) * 16)) = v;
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63, fr = lane & 15, g = lane >> 4;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    typedef __attribute__((ext_vector_type(8))) __bf16 bf16v8;
+    const int64_t nunits = (d.M + 15) / 16;
+    const int64_t nw = (int64_t)gridDim.x * NW, wid = (int64_t)blockIdx.x * NW + wave;
+    const int64_t u0 = nunits * wid / nw, u1 = nunits * (wid + 1) / nw;
+    float bj[NT][4];
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) bj[j][e] = 16 * j + 4 * g + e < H ? d.bias[16 * j + 4 * g + e] : 0.f;
+    int64_t cur_b = -1;
+    double r1 = 0.0, r2 = 0.0;
+    auto flush = [&]() {
+        if (cur_b >= 0) {
+            const double t1 = wave_sum_d(r1), t2 = wave_sum_d(r2);
+            if (lane == 0) {
+                atomicAdd(&d.st[2 * cur_b], t1);
+                atomicAdd(&d.st[2 * cur_b + 1], t2);
+            }
+        }
+        r1 = r2 = 0.0;
+    };
+    for (int64_t u = u0; u < u1; ++u) {
+        const int64_t m = u * 16 + fr;
+        const bool ok = m < d.M;
+        const int64_t mm = ok ? m : d.M - 1;
+        const int64_t gb = mm / d.L;
+        const int t = (int)(mm - gb * d.L);
+        f32x4_t acc[NT];
+#pragma unroll
+        for (int j = 0; j < NT; ++j) acc[j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+        for (int tap = 0; tap < 3; ++tap) {
+            const int tt = t + (tap - 1) * d.dil;
+            const bool in = tt >= 0 && tt < (int)d.L;
+            const uint16_t* xr = d.x + (mm + (in ? (int64_t)(tap - 1) * d.dil : 0)) * C + 8 * g;
+            bf16v8 bf[KS];
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) bf[ks] = in ? *reinterpret_cast<const bf16v8*>(xr + 32 * ks) : bf16v8{};
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+                const int q = (tap * C + 32 * ks) / 8 + g;
+#pragma unroll
+                for (int j = 0; j < NT; ++j) {
+                    const bf16v8 af = *reinterpret_cast<const bf16v8*>(wl + (16 * j + fr) * RB + ((q ^ (fr & 7)) * 16));
+                    acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf[ks], acc[j], 0, 0, 0);
+                }
+            }
+        }
+        // the unit's rows belong to group gb0 (first row) or, past a boundary, gb0 + 1 (L >= 16)
+        const int64_t gb0 = (u * 16) / d.L;
+        float s1a = 0.f, s2a = 0.f, s1b = 0.f, s2b = 0.f;
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+            float v[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = acc[j][e] + bj[j][e];
+            const int c0 = 16 * j + 4 * g;
+            if (ok && c0 < H) {
+                *reinterpret_cast<float4*>(d.h + mm * H + c0) = make_float4(v[0], v[1], v[2], v[3]);
+                const float p1 = (v[0] + v[1]) + (v[2] + v[3]);
+                const float p2 = (v[0] * v[0] + v[1] * v[1]) + (v[2] * v[2] + v[3] * v[3]);
+                if (gb == gb0) { s1a += p1; s2a += p2; } else { s1b += p1; s2b += p2; }
+            }
+        }
+        if (gb0 != cur_b) {
+            flush();
+            cur_b = gb0;
+        }
+        r1 += (double)s1a;
+        r2 += (double)s2a;
+        const bool split = __any(gb != gb0);
+        if (split) {
+            flush();
+            cur_b = gb0 + 1;
+            r1 = (double)s1b;
+            r2 = (double)s2b;
+        }
+    }
+    flush();
+}
+
+bool dconv_conv3_supported(int C, int H, int kp, int64_t L) {
+    return (C == 96 || C == 192 || C == 384) && H == C / 8 && kp >= 3 * C && L >= 16;
+}
+
+int dconv_conv3_launch(const uint16_t* x, const uint16_t* w, int kp, const float* bias, float* h, double* st,
+                       int64_t M, int64_t L, int C, int dil, hipStream_t s) {
+    if (!dconv_conv3_supported(C, C / 8, kp, L) || M <= 0) return -1;
+    DcConv3 d;
+    d.x = x; d.w = w; d.bias = bias; d.h = h; d.st = st; d.M = M; d.L = L; d.kp = kp; d.dil = dil;
+    static int cus = 0;
+    if (cus == 0) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        if (cus <= 0) cus = 256;
+    }
+    KScope ks(s);
+    if (ks.on()) {
+        const double H = C / 8;
+        ks.begin(klabel("dconv_conv3_kernel<%d>", C), 2.0 * M * H * 3 * C, (double)M * (C * 2 + H * 4));
+    }
+    const int64_t units = (M + 15) / 16;
+    if (C == 96) {       // 9 KB of weights
+        const int64_t blocks = std::min<int64_t>(3LL * cus, (units + 7) / 8);
+        hipLaunchKernelGGL((dconv_conv3_kernel<96, 8>), dim3((unsigned)blocks), dim3(512), 0, s, d);
+    } else if (C == 192) {      // 36 KB of weights: 2 eight-wave workgroups per CU
+        const int64_t blocks = std::min<int64_t>(2LL * cus, (units + 7) / 8);
+        hipLaunchKernelGGL((dconv_conv3_kernel<192, 8>), dim3((unsigned)blocks), dim3(512), 0, s, d);
+    } else {             // 110 KB: one 16-wave workgroup per CU
+        const int64_t blocks = std::min<int64_t>((int64_t)cus, (units + 15) / 16);
+        hipLaunchKernelGGL((dconv_conv3_kernel<384, 16>), dim3((unsigned)blocks), dim3(1024), 0, s, d);
+    }
+    return (int)hipGetLastError();
+}
+
 bool dconv_apply_supported(int C, int H, int kp, int64_t M) {
-    return (C == 192 || C == 384) && H == C / 8 && kp == 64 && M > 0;
+    return (C == 96 || C == 192 || C == 384) && H == C / 8 && kp == 64 && M > 0;
 }
 
 int dconv_apply_launch(const uint16_t* hb, const uint16_t* w, int kp, const float* bias, const double* st,
@@ -449,7 +596,10 @@ int dconv_apply_launch(const uint16_t* hb, const uint16_t* w, int kp, const floa
         ks.begin(klabel("dconv_apply_kernel<%d>", C), 2.0 * M * 2 * C * H, (double)M * (H * 2 + 2.0 * C * 2));
     }
     const int64_t units = (M + 15) / 16;
-    if (C == 192) {      // 48 KB of weights: two 8-wave workgroups per CU
+    if (C == 96) {       // (time-branch level 1: hidden rows padded to 16 channels by gn_gelu_mom; 27 KB of LDS)
+        const int64_t blocks = std::min<int64_t>(3LL * cus, (units + 7) / 8);
+        hipLaunchKernelGGL((dconv_apply_kernel<96, 8>), dim3((unsigned)blocks), dim3(512), 0, s, d);
+    } else if (C == 192) {      // 48 KB of weights: two 8-wave workgroups per CU
         const int64_t blocks = std::min<int64_t>(2LL * cus, (units + 7) / 8);
         hipLaunchKernelGGL((dconv_apply_kernel<192, 8>), dim3((unsigned)blocks), dim3(512), 0, s, d);
     } else {             // 96 KB: one 16-wave workgroup per CU

@@ -111,9 +111,10 @@ size_t plan(Arena& ar, const Dims& d, Bufs& b, bool actbf) {
         b.saved_t[i] = act(B * d.L[i + 1] * C);
         const int64_t rows = B * d.F[i + 1] * Ts, rows_t = B * d.L[i + 1];
         ymax = std::max(ymax, rows * C);
-        hmax = std::max(hmax, rows * (C / 8));
+        const int64_t hs = C == 96 ? 16 : C / 8;     // (C = 96: hidden rows padded to 16 for the MFMA passes)
+        hmax = std::max(hmax, rows * hs);
         ymax_t = std::max(ymax_t, rows_t * C);
-        hmax_t = std::max(hmax_t, rows_t * (C / 8));
+        hmax_t = std::max(hmax_t, rows_t * hs);
     }
     b.sk4 = act(B * d.F[1] * Ts * 4);
     b.sk4t = act(B * d.L[1] * 4);
@@ -255,7 +256,10 @@ void dconv(Run& r, const EncW& e, void* x, int64_t nb, int64_t L, float* hbuf, u
         const int dil = 1 << dd;
         double* st_h = r.stats(nb);
         double* st_y = r.stats(nb);
-        if (C <= 96) {   // narrow levels: HBM-bound VALU kernels (dconv.hip)
+        // C = 96 in the bf16 mode (the time branch's level 1; the freq level 1 is fused in fenc_row): the MFMA passes
+        // of the wide levels below (conv3, GN+GELU with the 1x1's moments, apply), the hidden rows padded to 16
+        const bool wide96 = C == 96 && r.actbf && hbuf_b && e.dc.gram1b[dd] && e.dc.c3[dd].w && L >= 64;
+        if (C <= 96 && !wide96) {   // narrow levels: HBM-bound VALU kernels (dconv.hip)
             KSite site(dd == 0 ? "dconv0" : "dconv1");
             r.check(dconv_small_launch(x, ab, hbuf, nb, L, C, dil, e.dc.w3f[dd], e.dc.c3[dd].bias, e.dc.g1w[dd],
                                        e.dc.g1b[dd], e.dc.w1f[dd], e.dc.b1f[dd], e.dc.gram1[dd], e.dc.g2wf[dd], e.dc.g2bf[dd],
@@ -267,10 +271,16 @@ void dconv(Run& r, const EncW& e, void* x, int64_t nb, int64_t L, float* hbuf, u
         g.ntaps = 3; g.in_stride = 1; g.in_off = -dil; g.dil = dil; g.H_out = (int)L;
         g.Wp = e.dc.c3[dd].w; g.N = Hh; g.K = e.dc.c3[dd].K; g.Kp = e.dc.c3[dd].Kp; g.bias = e.dc.c3[dd].bias;
         g.C = hbuf; g.H_out_total = (int)L; g.ldo = Hh; g.stats = st_h;
-        r.gemm(g, "dconv.conv3");
+        int rc3 = -1;
+        if (r.actbf) {       // bf16 mode: the weights-resident conv3 pass (dconv.hip), else the tiled GEMM
+            KSite site("dconv.conv3");
+            rc3 = dconv_conv3_launch((const uint16_t*)x, (const uint16_t*)e.dc.c3[dd].w, e.dc.c3[dd].Kp,
+                                     e.dc.c3[dd].bias, hbuf, st_h, nb * L, L, C, dil, r.s);
+        }
+        if (rc3 != 0) r.gemm(g, "dconv.conv3");
         // bf16 mode: GELU(GN(h)) written once as bf16, so both 1x1 passes read half the bytes and run on the bf16
         // MFMA GEMMs (gemm3 / gemm5) instead of converting fp32 A on load
-        const bool hb = r.actbf && hbuf_b && Hh % 8 == 0;
+        const bool hb = r.actbf && hbuf_b && (Hh % 8 == 0 || wide96);
         // the 1x1's GroupNorm statistics from its moments, taken by the GN+GELU pass (no statistics GEMM pass)
         bool mom = false;
         {

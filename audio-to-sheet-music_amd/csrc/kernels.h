@@ -178,6 +178,10 @@ int convt4_launch(const ConvT4Desc& d, hipStream_t s);
 // x: [nb][L][C] f32 or bf16 (x_bf16), updated in place; h: [nb][L][C/8] f32 scratch
 // dconv.hip: the wide levels' (C = 192, 384) DConv 1x1 apply x += scale * GLU(GN(W1 hb + b1)) in bf16 (hb [M][C/8],
 // x [M][C], GroupNorm groups of L rows); -1 if the shape is not covered
+// the wide levels' conv3 (C -> C/8, 3 taps at dilation dil, zero padding at each group's ends) + GroupNorm {sum,
+// sumsq} of h per group of L rows; x bf16 [M][C], h f32 [M][C/8]; -1 if the shape is not covered
+int dconv_conv3_launch(const uint16_t* x, const uint16_t* w, int kp, const float* bias, float* h, double* st,
+                       int64_t M, int64_t L, int C, int dil, hipStream_t s);
 int dconv_apply_launch(const uint16_t* hb, const uint16_t* w, int kp, const float* bias, const double* st,
                        const float* gn_w, const float* gn_b, const float* scale, uint16_t* x, int64_t M, int64_t L,
                        int C, hipStream_t s);

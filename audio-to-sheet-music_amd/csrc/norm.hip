@@ -124,93 +124,134 @@ void gn_gelu_bf16_launch(const float* h, bf16_t* out, int nb, int64_t per_batch,
 //   sum_n y_n = sum b + u.x,   sum_n y_n^2 = sum b^2 + 2 v.x + x^T G x,   x = the bf16 GELU(GN(h)) row the GEMM reads.
 // One lane per position (row of H channels); groups of L >= 64 positions, so a wave spans at most two groups (its
 // sums go to the first active lane's group and, for lanes past a boundary, to the last lane's group).
+constexpr int GN_MOM_RMAX = 4;
+
 template <int H>
 __global__ __launch_bounds__(256) void gn_gelu_mom_kernel(const float* __restrict__ h, bf16_t* __restrict__ out,
-                                                          int64_t npos, int64_t L, const double* __restrict__ st,
+                                                          int64_t npos, int64_t L, int R,
+                                                          const double* __restrict__ st,
                                                           const float* __restrict__ w, const float* __restrict__ bb,
                                                           const float* __restrict__ gram, double* __restrict__ st_y) {
     __shared__ float wb[2 * H];
+    // per (pass, wave) the segmented sums of its <= 2 groups; merged in position order into one atomic pair per
+    // group and workgroup (one pair per wave put up to ~260 waves on each group's line: atomic-bound at large L)
+    __shared__ double rs[GN_MOM_RMAX * 4 * 2][2];
+    __shared__ int64_t rgid[GN_MOM_RMAX * 4 * 2];
     for (int i = threadIdx.x; i < 2 * H; i += 256) wb[i] = i < H ? w[i] : bb[i - H];
     __syncthreads();
-    const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    const bool act = p < npos;
-    const int64_t pp = act ? p : npos - 1;
-    const int64_t g = pp / L;
-    float mean, rstd;
-    gn_params(st, g, L * H, mean, rstd);
-    float x[H];
-    const float4* hr = reinterpret_cast<const float4*>(h + pp * H);
+    const int wv = threadIdx.x >> 6;
+#pragma unroll 1
+    for (int it = 0; it < R; ++it) {
+        const int64_t p0 = ((int64_t)blockIdx.x * R + it) * 256;
+        const int64_t p = p0 + threadIdx.x;
+        const bool act = p < npos;
+        const int64_t pp = act ? p : npos - 1;
+        const int64_t g = pp / L;
+        float mean, rstd;
+        gn_params(st, g, L * H, mean, rstd);
+        float x[H];
+        const float4* hr = reinterpret_cast<const float4*>(h + pp * H);
 #pragma unroll
-    for (int q = 0; q < H / 4; ++q) {
-        const float4 v = hr[q];
-        x[4 * q] = v.x; x[4 * q + 1] = v.y; x[4 * q + 2] = v.z; x[4 * q + 3] = v.w;
-    }
-    uint32_t pk[H / 2];
-#pragma unroll
-    for (int j = 0; j < H; j += 2) {
-        pk[j / 2] = pack2bf(gelu_fast((x[j] - mean) * rstd * wb[j] + wb[H + j]),
-                            gelu_fast((x[j + 1] - mean) * rstd * wb[j + 1] + wb[H + j + 1]));
-        x[j] = __uint_as_float(pk[j / 2] << 16);                 // the bf16 values the 1x1 GEMM multiplies
-        x[j + 1] = __uint_as_float(pk[j / 2] & 0xFFFF0000u);
-    }
-    if (act) {
-        uint4* o = reinterpret_cast<uint4*>(out + pp * H);
-#pragma unroll
-        for (int q = 0; q < H / 8; ++q) o[q] = make_uint4(pk[4 * q], pk[4 * q + 1], pk[4 * q + 2], pk[4 * q + 3]);
-    }
-    // the moments are wave-uniform: scalar loads, one G row per step (the pointer is made opaque per row, so the
-    // compiler cannot hoist all H*H loads to the front, which needed ~2300 registers and spilled)
-    typedef __attribute__((address_space(4))) const float cfloat;    // constant address space: scalar loads
-    float qf = 0.f, lv = 0.f, lw = 0.f;
-#pragma unroll
-    for (int j = 0; j < H; ++j) {
-        cfloat* gr = (cfloat*)(gram + j * H);
-        asm volatile("" : "+s"(gr), "+v"(qf));              // row j's loads after row j-1's products
-        float t4[4] = {0.f, 0.f, 0.f, 0.f};                 // 4 independent chains (the FMA latency, not issue)
-#pragma unroll
-        for (int k0 = 0; k0 < H; k0 += 24) {               // (at most 24 row values in SGPRs at a time)
-            cfloat* gk = gr + k0;
-            if (k0 > 0) asm volatile("" : "+s"(gk), "+v"(t4[0]));
-#pragma unroll
-            for (int k = 0; k < 24; ++k) t4[k & 3] = fmaf(gk[k], x[k0 + k], t4[k & 3]);
+        for (int q = 0; q < H / 4; ++q) {
+            const float4 v = hr[q];
+            x[4 * q] = v.x; x[4 * q + 1] = v.y; x[4 * q + 2] = v.z; x[4 * q + 3] = v.w;
         }
-        qf = fmaf(x[j], (t4[0] + t4[1]) + (t4[2] + t4[3]), qf);
-        lv = fmaf(gr[H * (H - j) + j], x[j], lv);            // gram[H*H + j]      = (W^T b)_j
-        lw = fmaf(gr[H * (H - j) + H + j], x[j], lw);        // gram[H*H + H + j]  = (W^T 1)_j
-    }
-    cfloat* gt = (cfloat*)(gram + H * H + 2 * H);
-    const float sb = gt[0], sb2 = gt[1];
-    const double s1 = act ? (double)(sb + lw) : 0.0;
-    const double s2 = act ? (double)(sb2 + (2.f * lv + qf)) : 0.0;
-    // segmented wave sums: group gA of the first lane, gB of the last active lane (gA <= g <= gB, gB <= gA + 1)
-    const int64_t gA = __builtin_amdgcn_readfirstlane((int)g);
-    const int64_t last = (int64_t)blockIdx.x * 256 + (threadIdx.x & ~63) + 63;
-    const int64_t gB = (last < npos ? last : npos - 1) / L;
-    const bool inA = g == gA;
-    const double a1 = wave_sum_d(inA ? s1 : 0.0), a2 = wave_sum_d(inA ? s2 : 0.0);
-    if ((threadIdx.x & 63) == 0) {
-        atomicAdd(&st_y[2 * gA], a1);
-        atomicAdd(&st_y[2 * gA + 1], a2);
-    }
-    if (gB != gA) {
-        const double b1 = wave_sum_d(inA ? 0.0 : s1), b2 = wave_sum_d(inA ? 0.0 : s2);
+        constexpr int OS = H % 8 == 0 ? H : (H + 15) / 16 * 16;     // output row stride (H = 12: rows padded to 16)
+        uint32_t pk[OS / 2];
+#pragma unroll
+        for (int j = 0; j < H; j += 2) {
+            pk[j / 2] = pack2bf(gelu_fast((x[j] - mean) * rstd * wb[j] + wb[H + j]),
+                                gelu_fast((x[j + 1] - mean) * rstd * wb[j + 1] + wb[H + j + 1]));
+            x[j] = __uint_as_float(pk[j / 2] << 16);                 // the bf16 values the 1x1 GEMM multiplies
+            x[j + 1] = __uint_as_float(pk[j / 2] & 0xFFFF0000u);
+        }
+#pragma unroll
+        for (int j = H / 2; j < OS / 2; ++j) pk[j] = 0u;
+        if (act) {
+            uint4* o = reinterpret_cast<uint4*>(out + pp * OS);
+#pragma unroll
+            for (int q = 0; q < OS / 8; ++q) o[q] = make_uint4(pk[4 * q], pk[4 * q + 1], pk[4 * q + 2], pk[4 * q + 3]);
+        }
+        // the moments are wave-uniform: scalar loads, one G row per step (the pointer is made opaque per row, so the
+        // compiler cannot hoist all H*H loads to the front, which needed ~2300 registers and spilled)
+        typedef __attribute__((address_space(4))) const float cfloat;    // constant address space: scalar loads
+        float qf = 0.f, lv = 0.f, lw = 0.f;
+#pragma unroll
+        for (int j = 0; j < H; ++j) {
+            cfloat* gr = (cfloat*)(gram + j * H);
+            asm volatile("" : "+s"(gr), "+v"(qf));              // row j's loads after row j-1's products
+            float t4[4] = {0.f, 0.f, 0.f, 0.f};                 // 4 independent chains (the FMA latency, not issue)
+#pragma unroll
+            for (int k0 = 0; k0 < H; k0 += 24) {               // (at most 24 row values in SGPRs at a time)
+                cfloat* gk = gr + k0;
+                if (k0 > 0) asm volatile("" : "+s"(gk), "+v"(t4[0]));
+#pragma unroll
+                for (int k = 0; k < (H - k0 < 24 ? H - k0 : 24); ++k) t4[k & 3] = fmaf(gk[k], x[k0 + k], t4[k & 3]);
+            }
+            qf = fmaf(x[j], (t4[0] + t4[1]) + (t4[2] + t4[3]), qf);
+            lv = fmaf(gr[H * (H - j) + j], x[j], lv);            // gram[H*H + j]      = (W^T b)_j
+            lw = fmaf(gr[H * (H - j) + H + j], x[j], lw);        // gram[H*H + H + j]  = (W^T 1)_j
+        }
+        cfloat* gt = (cfloat*)(gram + H * H + 2 * H);
+        const float sb = gt[0], sb2 = gt[1];
+        const double s1 = act ? (double)(sb + lw) : 0.0;
+        const double s2 = act ? (double)(sb2 + (2.f * lv + qf)) : 0.0;
+        // segmented wave sums: group gA of the first lane, gB of the last active lane (gA <= g <= gB, gB <= gA + 1)
+        const int64_t gA = __builtin_amdgcn_readfirstlane((int)g);
+        const int64_t last = p0 + wv * 64 + 63;
+        const int64_t gB = (last < npos ? last : npos - 1) / L;
+        const bool inA = g == gA;
+        const double a1 = wave_sum_d(inA ? s1 : 0.0), a2 = wave_sum_d(inA ? s2 : 0.0);
+        double b1 = 0.0, b2 = 0.0;
+        if (gB != gA) {
+            b1 = wave_sum_d(inA ? 0.0 : s1);
+            b2 = wave_sum_d(inA ? 0.0 : s2);
+        }
         if ((threadIdx.x & 63) == 0) {
-            atomicAdd(&st_y[2 * gB], b1);
-            atomicAdd(&st_y[2 * gB + 1], b2);
+            const int e = (it * 4 + wv) * 2;
+            rgid[e] = gA; rs[e][0] = a1; rs[e][1] = a2;
+            rgid[e + 1] = gB != gA ? gB : -1; rs[e + 1][0] = b1; rs[e + 1][1] = b2;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {          // entries in position order: groups non-decreasing
+        int64_t cg = -1;
+        double c1 = 0.0, c2 = 0.0;
+        for (int e = 0; e < R * 8; ++e) {
+            const int64_t ge = rgid[e];
+            if (ge < 0) continue;
+            if (ge != cg) {
+                if (cg >= 0) {
+                    atomicAdd(&st_y[2 * cg], c1);
+                    atomicAdd(&st_y[2 * cg + 1], c2);
+                }
+                cg = ge;
+                c1 = c2 = 0.0;
+            }
+            c1 += rs[e][0];
+            c2 += rs[e][1];
+        }
+        if (cg >= 0) {
+            atomicAdd(&st_y[2 * cg], c1);
+            atomicAdd(&st_y[2 * cg + 1], c2);
         }
     }
 }
 
 int gn_gelu_mom_launch(const float* h, uint16_t* out, int nb, int64_t L, int H, const double* stats, const float* w,
                        const float* b, const float* gram, double* st_y, hipStream_t s) {
-    if (L < 64 || (H != 24 && H != 48)) return -1;
+    if (L < 64 || (H != 12 && H != 24 && H != 48)) return -1;
     const int64_t npos = (int64_t)nb * L;
-    const dim3 grid((unsigned)((npos + 255) / 256));
+    // 256-position passes per workgroup: as many as keep >= 2048 workgroups (8 per CU), at most GN_MOM_RMAX
+    const int64_t passes = (npos + 255) / 256;
+    const int R = (int)std::max<int64_t>(1, std::min<int64_t>(GN_MOM_RMAX, passes / 2048));
+    const dim3 grid((unsigned)((passes + R - 1) / R));
     KScope ks(s);
     if (ks.on())
         ks.begin(klabel("gn_gelu_mom_kernel<%d>", H), 2.0 * npos * (H * H + 2 * H), (double)npos * H * (4 + 2));
-    if (H == 24) hipLaunchKernelGGL(gn_gelu_mom_kernel<24>, grid, dim3(256), 0, s, h, out, npos, L, stats, w, b, gram, st_y);
-    else hipLaunchKernelGGL(gn_gelu_mom_kernel<48>, grid, dim3(256), 0, s, h, out, npos, L, stats, w, b, gram, st_y);
+    if (H == 12) hipLaunchKernelGGL(gn_gelu_mom_kernel<12>, grid, dim3(256), 0, s, h, out, npos, L, R, stats, w, b, gram, st_y);
+    else if (H == 24) hipLaunchKernelGGL(gn_gelu_mom_kernel<24>, grid, dim3(256), 0, s, h, out, npos, L, R, stats, w, b, gram, st_y);
+    else hipLaunchKernelGGL(gn_gelu_mom_kernel<48>, grid, dim3(256), 0, s, h, out, npos, L, R, stats, w, b, gram, st_y);
     return (int)hipGetLastError();
 }
 

@@ -1,23 +1,26 @@
-"""Per-call-site kernel times of two bench.py --dump-kernels runs (the warm-up forward, every launch evented, branches
-serialised): python tools/sites_diff.py A_sites.json B_sites.json [--top N]"""
+"""Compare two per-call-site kernel time dumps (bench.py --dump-kernels X.json -> X_sites.json).
+
+    python tools/sites_diff.py OLD_sites.json NEW_sites.json [-n 20]
+"""
 import argparse
 import json
 
 
+def load(p):
+    return {r["kernel"]: r["ms"] for r in json.load(open(p))}
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("a")
-    ap.add_argument("b")
-    ap.add_argument("--top", type=int, default=20)
-    x = ap.parse_args()
-    A = {r["kernel"]: r["ms"] for r in json.load(open(x.a))}
-    B = {r["kernel"]: r["ms"] for r in json.load(open(x.b))}
-    keys = set(A) | set(B)
-    print(f"total: {sum(A.values()):.3f} ms -> {sum(B.values()):.3f} ms")
-    rows = sorted(keys, key=lambda k: -abs(B.get(k, 0.0) - A.get(k, 0.0)))
-    for k in rows[:x.top]:
-        a, b = A.get(k, 0.0), B.get(k, 0.0)
-        print(f"{a:8.3f} {b:8.3f} {b - a:+8.3f}  {k}")
+    ap.add_argument("old")
+    ap.add_argument("new")
+    ap.add_argument("-n", type=int, default=20)
+    a = ap.parse_args()
+    fa, fb = load(a.old), load(a.new)
+    print(f"total {sum(fa.values()):.3f} -> {sum(fb.values()):.3f} ms")
+    keys = sorted(set(fa) | set(fb), key=lambda k: -abs(fb.get(k, 0) - fa.get(k, 0)))
+    for k in keys[:a.n]:
+        print(f"{k:72s} {fa.get(k, 0):8.3f} {fb.get(k, 0):8.3f}")
 
 
 if __name__ == "__main__":
