@@ -196,6 +196,22 @@ int athd_finalize(athd_ctx* c) {
             e.cout = C;
             e.conv = c->conv_gemm(p + ".conv.weight", p + ".conv.bias", C, e.cin, 8);
             e.rewrite = c->conv_gemm(p + ".rewrite.weight", p + ".rewrite.bias", 2 * C, C, 1, true);
+            if (c->mode == 1 && (C == 48 || C == 96)) {
+                // K slot 32 ks + 8 g + i <- channel 32 ks + 4 g + i (i < 4) or 32 ks + 16 + 4 g + (i - 4): the order in
+                // which the fused DConv apply holds a row's updated channels (dconv.hip dconv_apply_kernel<C, NW, true>)
+                const auto& w = c->W(p + ".rewrite.weight").v;     // [2C][C]
+                const int K2 = (C + 31) / 32 * 32;
+                std::vector<float> q((size_t)2 * C * K2, 0.f);
+                for (int n = 0; n < 2 * C; ++n) {
+                    const int src = athd_ctx::glu_src(n, 2 * C);
+                    for (int k = 0; k < K2; ++k) {
+                        const int ks = k / 32, g = (k % 32) / 8, i = k % 8;
+                        const int ch = 32 * ks + (i < 4 ? 4 * g + i : 16 + 4 * g + (i - 4));
+                        if (ch < C) q[(size_t)n * K2 + k] = w[(size_t)src * C + ch];
+                    }
+                }
+                e.rewrite_perm = c->up_gemm(q, 2 * C, K2, athd_ctx::glu_order(c->W(p + ".rewrite.bias").v));
+            }
             if (br == 1 && i == 0) {                      // tconv0_kernel: [C][2][8] -> [C][tap * 2 + ci]
                 const auto& w0 = c->W(p + ".conv.weight").v;
                 std::vector<float> t0((size_t)C * 16);

@@ -39,6 +39,7 @@ struct DConvW {
 struct EncW {
     int cin = 0, cout = 0;
     GemmW conv, rewrite;
+    GemmW rewrite_perm;            // bf16 mode, C = 48, 96: rewrite in the K order of the fused DConv apply (dconv.hip)
     float* conv_f32 = nullptr;     // time level 0 only: [cout][tap * cin + ci] fp32 (tconv0.hip)
     DConvW dc;
 };

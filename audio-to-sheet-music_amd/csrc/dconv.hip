@@ -326,15 +326,25 @@ struct DcApply {
     uint16_t* x;               // [M][C] bf16 residual stream, updated in place
     int64_t M, L, gn_count;
     int kp;
+    // fused rewrite (RW, C = 48 / 96, the layer's second DConv layer): out = GLU(Wr x + br) of the updated rows
+    // instead of storing x; rw [2C][rkp] GLU-interleaved rows with the K order of dconv_rewrite_perm
+    const uint16_t* rw = nullptr;
+    const float* rbias = nullptr;  // [2C] packed
+    uint16_t* out = nullptr;       // [M][C] bf16
+    uint16_t* c4 = nullptr;        // optional [M][4]: channels 0..3 of out again (the decoder's compact skip)
+    int rkp = 0;
 };
 
-template <int C, int NW>
+template <int C, int NW, bool RW = false>
 __global__ __launch_bounds__(NW * 64) void dconv_apply_kernel(const DcApply d) {
     constexpr int H = C / 8, KS = (H + 31) / 32, NP = C / 16;      // K-steps, GLU pairs (16 output channels each)
-    constexpr int HS = H % 8 == 0 ? H : (H + 15) / 16 * 16;       // hidden row stride (H = 12: padded to 16)
-    __shared__ __attribute__((aligned(16))) char wl[2 * C * 128];
-    // per packed column: bias, GroupNorm weight, bias; per output channel: LayerScale
-    __shared__ __attribute__((aligned(16))) float cst[3 * 2 * C + C];
+    constexpr int HS = H % 8 == 0 ? H : (H + 15) / 16 * 16;       // hidden row stride (H = 6, 12: padded to 16)
+    constexpr int RK = (C + 31) / 32;                              // rewrite K-steps
+    constexpr int RPB = RW ? (RK * 4 + 7) / 8 * 128 : 0;           // rewrite LDS row bytes (chunks padded to 8 k)
+    __shared__ __attribute__((aligned(16))) char wl[2 * C * 128 + 2 * C * RPB];
+    // per packed column: bias, GroupNorm weight, bias; per output channel: LayerScale; (RW) per packed rewrite column:
+    // bias
+    __shared__ __attribute__((aligned(16))) float cst[3 * 2 * C + C + (RW ? 2 * C : 0)];
     for (int i = threadIdx.x; i < 2 * C * 8; i += NW * 64) {
         const int row = i >> 3, ch = i & 7;
         const uint4 v = *reinterpret_cast<const uint4*>(d.w + (int64_t)row * d.kp + ch * 8);
@@ -346,6 +356,16 @@ __global__ __launch_bounds__(NW * 64) void dconv_apply_kernel(const DcApply d) {
         cst[4 * C + i] = d.gn_b[i];
     }
     for (int i = threadIdx.x; i < C; i += NW * 64) cst[6 * C + i] = d.scale[i];
+    char* const wr = wl + 2 * C * 128;
+    if constexpr (RW) {
+        for (int i = threadIdx.x; i < 2 * C * (RPB / 16); i += NW * 64) {
+            const int row = i / (RPB / 16), ch = i % (RPB / 16);
+            const uint4 v = ch < RK * 4 ? *reinterpret_cast<const uint4*>(d.rw + (int64_t)row * d.rkp + ch * 8)
+                                        : make_uint4(0u, 0u, 0u, 0u);
+            *reinterpret_cast<uint4*>(wr + row * RPB + ((ch ^ (row & 7)) * 16)) = v;
+        }
+        for (int i = threadIdx.x; i < 2 * C; i += NW * 64) cst[7 * C + i] = d.rbias[i];
+    }
     __syncthreads();
     const int lane = threadIdx.x & 63, fr = lane & 15, g = lane >> 4;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -368,8 +388,10 @@ __global__ __launch_bounds__(NW * 64) void dconv_apply_kernel(const DcApply d) {
         }
         // the row's residual channels 16 p + 4 g .. + 3, PG pairs per group; the next group's loads are issued
         // before the current group's MFMAs (the first group's before the GroupNorm parameters)
-        constexpr int PG = 6, NG = NP / PG;
+        constexpr int PG = NP % 6 == 0 ? 6 : NP, NG = NP / PG;
         static_assert(NP % PG == 0, "pair groups");
+        static_assert(!RW || NG == 1, "the fused rewrite keeps all of the row's pairs in registers");
+        uint2 xk[RW ? NP : 1];            // (RW) the updated bf16 x channels 16 p + 4 g .. + 3 of row m
         const uint16_t* xr = d.x + mm * C + 4 * g;
         uint2 rr[PG];
 #pragma unroll
@@ -416,11 +438,48 @@ __global__ __launch_bounds__(NW * 64) void dconv_apply_kernel(const DcApply d) {
                     const float gt = (ag[e] + bgv[e] - gm) * gr * wgv[e] + cgv[e];
                     o[e] = r4[e] + scv[e] * (a * sigmoid_fast(gt));
                 }
-                if (ok) xo[4 * p] = make_uint2(pack2bf(o[0], o[1]), pack2bf(o[2], o[3]));
+                if constexpr (RW) xk[pp] = make_uint2(pack2bf(o[0], o[1]), pack2bf(o[2], o[3]));
+                else if (ok) xo[4 * p] = make_uint2(pack2bf(o[0], o[1]), pack2bf(o[2], o[3]));
             }
             if (gi + 1 < NG) {
 #pragma unroll
                 for (int p = 0; p < PG; ++p) rr[p] = rn[p];
+            }
+        }
+        if constexpr (RW) {
+            // rewrite: the lane's x values of K-step ks are channels 32 ks + 4 g + {0..3} (pair 2 ks) and
+            // 32 ks + 16 + 4 g + {0..3} (pair 2 ks + 1), which is the K order the packed rewrite weights carry, so the
+            // B fragments are the registers as they are
+            bf16v8 bx[RK];
+#pragma unroll
+            for (int ks = 0; ks < RK; ++ks) {
+                const uint2 lo = xk[2 * ks], hi = 2 * ks + 1 < NP ? xk[2 * ks + 1 < NP ? 2 * ks + 1 : 0] : make_uint2(0u, 0u);
+                const uint32_t w4[4] = {lo.x, lo.y, hi.x, hi.y};
+                bx[ks] = __builtin_bit_cast(bf16v8, w4);
+            }
+            uint16_t* const orow = d.out + mm * C + 4 * g;
+#pragma unroll
+            for (int q = 0; q < NP; ++q) {
+                f32x4_t aa = {0.f, 0.f, 0.f, 0.f}, ag = aa;
+#pragma unroll
+                for (int ks = 0; ks < RK; ++ks) {
+                    const bf16v8 fa = *reinterpret_cast<const bf16v8*>(wr + (32 * q + fr) * RPB + (((4 * ks + g) ^ (fr & 7)) * 16));
+                    const bf16v8 fg = *reinterpret_cast<const bf16v8*>(wr + (32 * q + 16 + fr) * RPB + (((4 * ks + g) ^ (fr & 7)) * 16));
+                    aa = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, bx[ks], aa, 0, 0, 0);
+                    ag = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fg, bx[ks], ag, 0, 0, 0);
+                }
+                const int na = 32 * q + 4 * g;
+                const float4 ba = *reinterpret_cast<const float4*>(cst + 7 * C + na);
+                const float4 bg = *reinterpret_cast<const float4*>(cst + 7 * C + na + 16);
+                const float bav[4] = {ba.x, ba.y, ba.z, ba.w}, bgv[4] = {bg.x, bg.y, bg.z, bg.w};
+                float o[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) o[e] = (aa[e] + bav[e]) * sigmoid_fast(ag[e] + bgv[e]);
+                const uint2 v = make_uint2(pack2bf(o[0], o[1]), pack2bf(o[2], o[3]));
+                if (ok) {
+                    *reinterpret_cast<uint2*>(orow + 16 * q) = v;
+                    if (q == 0 && g == 0 && d.c4) *reinterpret_cast<uint2*>(d.c4 + mm * 4) = v;
+                }
             }
         }
     }
@@ -436,7 +495,7 @@ struct DcConv3 {
     const uint16_t* x;         // [M][C] bf16
     const uint16_t* w;         // [>= 16 NT][kp] packed conv3 weights, K = tap * C + ci
     const float* bias;         // [H]
-    float* h;                  // [M][H] f32
+    float* h;                  // [M][HF] f32 (HF = H, or 8 for H = 6)
     double* st;                // per group {sum, sumsq}
     int64_t M, L;
     int kp, dil;
@@ -444,13 +503,15 @@ struct DcConv3 {
 
 template <int C, int NW>
 __global__ __launch_bounds__(NW * 64) void dconv_conv3_kernel(const DcConv3 d) {
-    constexpr int H = C / 8, NT = (H + 15) / 16, KS = C / 32, K = 3 * C;
+    constexpr int H = C / 8, NT = (H + 15) / 16, KS = (C + 31) / 32, K = 3 * C;
+    constexpr int HF = H % 4 == 0 ? H : (H + 7) / 8 * 8;   // f32 hidden row stride (16-B stores)
     constexpr int RB = (K / 8 + 7) / 8 * 128;               // LDS row bytes (chunks padded to a multiple of 8: the
                                                             // XOR swizzle stays inside the row, e.g. C = 96: 36 -> 40)
     __shared__ __attribute__((aligned(16))) char wl[16 * NT * RB];
-    for (int i = threadIdx.x; i < 16 * NT * (K / 8); i += NW * 64) {
-        const int row = i / (K / 8), q = i % (K / 8);
-        const uint4 v = *reinterpret_cast<const uint4*>(d.w + (int64_t)row * d.kp + q * 8);
+    for (int i = threadIdx.x; i < 16 * NT * (RB / 16); i += NW * 64) {    // (padding chunks zeroed: the masked
+        const int row = i / (RB / 16), q = i % (RB / 16);                      // K-steps of C = 48 multiply them by 0)
+        const uint4 v = q < K / 8 ? *reinterpret_cast<const uint4*>(d.w + (int64_t)row * d.kp + q * 8)
+                                  : make_uint4(0u, 0u, 0u, 0u);
         *reinterpret_cast<uint4*>(wl + row * RB + ((q ^ (row & 7)) * 16)) = v;
     }
     __syncthreads();
@@ -493,7 +554,8 @@ __global__ __launch_bounds__(NW * 64) void dconv_conv3_kernel(const DcConv3 d) {
             const uint16_t* xr = d.x + (mm + (in ? (int64_t)(tap - 1) * d.dil : 0)) * C + 8 * g;
             bf16v8 bf[KS];
 #pragma unroll
-            for (int ks = 0; ks < KS; ++ks) bf[ks] = in ? *reinterpret_cast<const bf16v8*>(xr + 32 * ks) : bf16v8{};
+            for (int ks = 0; ks < KS; ++ks)
+                bf[ks] = in && 32 * ks + 8 * g < C ? *reinterpret_cast<const bf16v8*>(xr + 32 * ks) : bf16v8{};
 #pragma unroll
             for (int ks = 0; ks < KS; ++ks) {
                 const int q = (tap * C + 32 * ks) / 8 + g;
@@ -513,8 +575,8 @@ __global__ __launch_bounds__(NW * 64) void dconv_conv3_kernel(const DcConv3 d) {
 #pragma unroll
             for (int e = 0; e < 4; ++e) v[e] = acc[j][e] + bj[j][e];
             const int c0 = 16 * j + 4 * g;
-            if (ok && c0 < H) {
-                *reinterpret_cast<float4*>(d.h + mm * H + c0) = make_float4(v[0], v[1], v[2], v[3]);
+            if (ok && c0 < H) {        // (H = 6: channels 6, 7 of the second chunk are 0 - zero weight rows and bias)
+                *reinterpret_cast<float4*>(d.h + mm * HF + c0) = make_float4(v[0], v[1], v[2], v[3]);
                 const float p1 = (v[0] + v[1]) + (v[2] + v[3]);
                 const float p2 = (v[0] * v[0] + v[1] * v[1]) + (v[2] * v[2] + v[3] * v[3]);
                 if (gb == gb0) { s1a += p1; s2a += p2; } else { s1b += p1; s2b += p2; }
@@ -538,7 +600,7 @@ __global__ __launch_bounds__(NW * 64) void dconv_conv3_kernel(const DcConv3 d) {
 }
 
 bool dconv_conv3_supported(int C, int H, int kp, int64_t L) {
-    return (C == 96 || C == 192 || C == 384) && H == C / 8 && kp >= 3 * C && L >= 16;
+    return (C == 48 || C == 96 || C == 192 || C == 384) && H == C / 8 && kp >= 3 * C && L >= 16;
 }
 
 int dconv_conv3_launch(const uint16_t* x, const uint16_t* w, int kp, const float* bias, float* h, double* st,
@@ -559,7 +621,10 @@ int dconv_conv3_launch(const uint16_t* x, const uint16_t* w, int kp, const float
         ks.begin(klabel("dconv_conv3_kernel<%d>", C), 2.0 * M * H * 3 * C, (double)M * (C * 2 + H * 4));
     }
     const int64_t units = (M + 15) / 16;
-    if (C == 96) {       // 9 KB of weights
+    if (C == 48) {       // 6 KB of weights
+        const int64_t blocks = std::min<int64_t>(3LL * cus, (units + 7) / 8);
+        hipLaunchKernelGGL((dconv_conv3_kernel<48, 8>), dim3((unsigned)blocks), dim3(512), 0, s, d);
+    } else if (C == 96) {       // 10 KB of weights
         const int64_t blocks = std::min<int64_t>(3LL * cus, (units + 7) / 8);
         hipLaunchKernelGGL((dconv_conv3_kernel<96, 8>), dim3((unsigned)blocks), dim3(512), 0, s, d);
     } else if (C == 192) {      // 36 KB of weights: 2 eight-wave workgroups per CU
@@ -573,16 +638,21 @@ int dconv_conv3_launch(const uint16_t* x, const uint16_t* w, int kp, const float
 }
 
 bool dconv_apply_supported(int C, int H, int kp, int64_t M) {
-    return (C == 96 || C == 192 || C == 384) && H == C / 8 && kp == 64 && M > 0;
+    return (C == 48 || C == 96 || C == 192 || C == 384) && H == C / 8 && kp == 64 && M > 0;
 }
 
 int dconv_apply_launch(const uint16_t* hb, const uint16_t* w, int kp, const float* bias, const double* st,
                        const float* gn_w, const float* gn_b, const float* scale, uint16_t* x, int64_t M, int64_t L,
-                       int C, hipStream_t s) {
+                       int C, hipStream_t s, const DcRewrite* rwd) {
     if (!dconv_apply_supported(C, C / 8, kp, M)) return -1;
+    if (rwd && !(C == 48 || C == 96)) return -1;
     DcApply d;
     d.hb = hb; d.w = w; d.bias = bias; d.st = st; d.gn_w = gn_w; d.gn_b = gn_b; d.scale = scale; d.x = x;
     d.M = M; d.L = L; d.gn_count = L * 2 * C; d.kp = kp;
+    if (rwd) {
+        if (rwd->kp < (C + 31) / 32 * 32) return -1;
+        d.rw = rwd->w; d.rkp = rwd->kp; d.rbias = rwd->bias; d.out = rwd->out; d.c4 = rwd->c4;
+    }
     static int cus = 0;
     if (cus == 0) {
         int dev = 0;
@@ -593,10 +663,21 @@ int dconv_apply_launch(const uint16_t* hb, const uint16_t* w, int kp, const floa
     KScope ks(s);
     if (ks.on()) {
         const double H = C / 8;
-        ks.begin(klabel("dconv_apply_kernel<%d>", C), 2.0 * M * 2 * C * H, (double)M * (H * 2 + 2.0 * C * 2));
+        if (rwd)
+            ks.begin(klabel("dconv_apply_kernel<%d,rewrite>", C), 2.0 * M * 2 * C * (H + C),
+                     (double)M * (H * 2 + 2.0 * C * 2 + (rwd->c4 ? 8 : 0)));
+        else
+            ks.begin(klabel("dconv_apply_kernel<%d>", C), 2.0 * M * 2 * C * H, (double)M * (H * 2 + 2.0 * C * 2));
     }
     const int64_t units = (M + 15) / 16;
-    if (C == 96) {       // (time-branch level 1: hidden rows padded to 16 channels by gn_gelu_mom; 27 KB of LDS)
+    if (rwd) {           // C = 48: 25 KB of LDS, C = 96: 77 KB
+        const int64_t blocks = std::min<int64_t>((C == 48 ? 3LL : 2LL) * cus, (units + 7) / 8);
+        if (C == 48) hipLaunchKernelGGL((dconv_apply_kernel<48, 8, true>), dim3((unsigned)blocks), dim3(512), 0, s, d);
+        else hipLaunchKernelGGL((dconv_apply_kernel<96, 8, true>), dim3((unsigned)blocks), dim3(512), 0, s, d);
+    } else if (C == 48) {
+        const int64_t blocks = std::min<int64_t>(3LL * cus, (units + 7) / 8);
+        hipLaunchKernelGGL((dconv_apply_kernel<48, 8>), dim3((unsigned)blocks), dim3(512), 0, s, d);
+    } else if (C == 96) {       // (time-branch level 1: hidden rows padded to 16 channels by gn_gelu_mom; 27 KB of LDS)
         const int64_t blocks = std::min<int64_t>(3LL * cus, (units + 7) / 8);
         hipLaunchKernelGGL((dconv_apply_kernel<96, 8>), dim3((unsigned)blocks), dim3(512), 0, s, d);
     } else if (C == 192) {      // 48 KB of weights: two 8-wave workgroups per CU

@@ -111,7 +111,7 @@ size_t plan(Arena& ar, const Dims& d, Bufs& b, bool actbf) {
         b.saved_t[i] = act(B * d.L[i + 1] * C);
         const int64_t rows = B * d.F[i + 1] * Ts, rows_t = B * d.L[i + 1];
         ymax = std::max(ymax, rows * C);
-        const int64_t hs = C == 96 ? 16 : C / 8;     // (C = 96: hidden rows padded to 16 for the MFMA passes)
+        const int64_t hs = C <= 96 ? 16 : C / 8;     // (C = 48, 96: hidden rows padded to 16 for the MFMA passes)
         hmax = std::max(hmax, rows * hs);
         ymax_t = std::max(ymax_t, rows_t * C);
         hmax_t = std::max(hmax_t, rows_t * hs);
@@ -249,7 +249,11 @@ bool second_stream(Run& r) {
     return r.err == 0;
 }
 
-void dconv(Run& r, const EncW& e, void* x, int64_t nb, int64_t L, float* hbuf, uint16_t* hbuf_b) {
+// rw: the layer's rewrite fused into the second DConv layer's apply pass (bf16 mode, C = 48, 96): returns true when it
+// ran there (x then holds the first layer's output only), false when the caller must run the rewrite
+bool dconv(Run& r, const EncW& e, void* x, int64_t nb, int64_t L, float* hbuf, uint16_t* hbuf_b,
+           const DcRewrite* rw = nullptr) {
+    bool fused = false;
     const int ab = r.actbf ? 1 : 0;
     const int C = e.cout, Hh = C / 8;
     for (int dd = 0; dd < 2; ++dd) {
@@ -258,7 +262,7 @@ void dconv(Run& r, const EncW& e, void* x, int64_t nb, int64_t L, float* hbuf, u
         double* st_y = r.stats(nb);
         // C = 96 in the bf16 mode (the time branch's level 1; the freq level 1 is fused in fenc_row): the MFMA passes
         // of the wide levels below (conv3, GN+GELU with the 1x1's moments, apply), the hidden rows padded to 16
-        const bool wide96 = C == 96 && r.actbf && hbuf_b && e.dc.gram1b[dd] && e.dc.c3[dd].w && L >= 64;
+        const bool wide96 = (C == 48 || C == 96) && r.actbf && hbuf_b && e.dc.gram1b[dd] && e.dc.c3[dd].w && L >= 64;
         if (C <= 96 && !wide96) {   // narrow levels: HBM-bound VALU kernels (dconv.hip)
             KSite site(dd == 0 ? "dconv0" : "dconv1");
             r.check(dconv_small_launch(x, ab, hbuf, nb, L, C, dil, e.dc.w3f[dd], e.dc.c3[dd].bias, e.dc.g1w[dd],
@@ -311,11 +315,17 @@ void dconv(Run& r, const EncW& e, void* x, int64_t nb, int64_t L, float* hbuf, u
         int rc = -1;
         if (hb) {
             KSite site("dconv.conv1x1.apply");
+            const DcRewrite* rwd = dd == 1 && wide96 ? rw : nullptr;
             rc = dconv_apply_launch(hbuf_b, (const uint16_t*)e.dc.c1[dd].w, e.dc.c1[dd].Kp, e.dc.c1[dd].bias, st_y,
-                                    e.dc.g2w[dd], e.dc.g2b[dd], e.dc.scale[dd], (uint16_t*)x, nb * L, L, C, r.s);
+                                    e.dc.g2w[dd], e.dc.g2b[dd], e.dc.scale[dd], (uint16_t*)x, nb * L, L, C, r.s, rwd);
+            if (rc == 0 && rwd) fused = true;
+            if (rc != 0 && rwd)      // (without the rewrite, then the caller's GEMM)
+                rc = dconv_apply_launch(hbuf_b, (const uint16_t*)e.dc.c1[dd].w, e.dc.c1[dd].Kp, e.dc.c1[dd].bias,
+                                        st_y, e.dc.g2w[dd], e.dc.g2b[dd], e.dc.scale[dd], (uint16_t*)x, nb * L, L, C, r.s);
         }
         if (rc != 0) r.gemm(g2, "dconv.conv1x1.apply");
     }
+    return fused;
 }
 
 // the fused narrow freq level (fenc_row.hip) applies: bf16 mode, C in {48, 96}, T <= 272, padded conv3 packed
@@ -427,13 +437,18 @@ void encode(Run& r, const Dims& d, const Bufs& b, const float* wav) {
             gt.C = b.ybuf_t; gt.c_bf16 = eab; gt.H_out_total = (int)Lo; gt.ldo = C; gt.act = ACT_GELU;
             r.gemm(gt, "tenc.conv");
         }
-        dconv(r, et, b.ybuf_t, B, Lo, b.hbuf_t, b.hbuf_b_t);
+        DcRewrite rwt;
+        rwt.w = (const uint16_t*)et.rewrite_perm.w; rwt.kp = et.rewrite_perm.Kp; rwt.bias = et.rewrite_perm.bias;
+        rwt.out = (uint16_t*)b.saved_t[i]; rwt.c4 = i == 0 ? (uint16_t*)b.sk4t : nullptr;
+        const bool fused_rw = dconv(r, et, b.ybuf_t, B, Lo, b.hbuf_t, b.hbuf_b_t, et.rewrite_perm.w ? &rwt : nullptr);
+        if (!fused_rw) {
         GemmDesc grt;
         grt.A = b.ybuf_t; grt.a_bf16 = eab; grt.nb = (int)B; grt.H_in = (int)Lo; grt.W = 1; grt.C_in = C; grt.a_ld = C; grt.H_out = (int)Lo;
         grt.Wp = et.rewrite.w; grt.N = 2 * C; grt.K = C; grt.Kp = et.rewrite.Kp; grt.bias = et.rewrite.bias;
         grt.C = b.saved_t[i]; grt.c_bf16 = eab; grt.H_out_total = (int)Lo; grt.ldo = C; grt.act = ACT_GLU;
         grt.c4 = i == 0 ? b.sk4t : nullptr;
         r.gemm(grt, "tenc.rewrite");
+        }
         r.s = s_enc;
     }
     (void)hipEventRecord(c->ev_t, s_tenc);        // join

@@ -176,15 +176,24 @@ bool convt4_supported(int cin, int cout, int64_t nb, int64_t H, int64_t W);
 int convt4_launch(const ConvT4Desc& d, hipStream_t s);
 // dconv.hip: one DConv layer (conv3 -> GN -> GELU -> 1x1 -> GN -> GLU -> LayerScale -> residual) for C in {48, 96}
 // x: [nb][L][C] f32 or bf16 (x_bf16), updated in place; h: [nb][L][C/8] f32 scratch
-// dconv.hip: the wide levels' (C = 192, 384) DConv 1x1 apply x += scale * GLU(GN(W1 hb + b1)) in bf16 (hb [M][C/8],
-// x [M][C], GroupNorm groups of L rows); -1 if the shape is not covered
-// the wide levels' conv3 (C -> C/8, 3 taps at dilation dil, zero padding at each group's ends) + GroupNorm {sum,
-// sumsq} of h per group of L rows; x bf16 [M][C], h f32 [M][C/8]; -1 if the shape is not covered
+// dconv.hip, bf16 mode, MFMA passes (C = 48, 96, 192, 384): the DConv 1x1 apply x += scale * GLU(GN(W1 hb + b1))
+// (hb [M][HS] with HS = C/8, or 16 for C = 48, 96; x [M][C]; GroupNorm groups of L rows); -1 if the shape is not
+// covered.  With rw (C = 48, 96) the updated rows are not stored: the encoder layer's rewrite out = GLU(Wr x + br)
+// runs on them in registers (rw: [2C][kp] GLU-interleaved rows in the K order of ctx.h rewrite_perm).
+struct DcRewrite {
+    const uint16_t* w;
+    int kp;
+    const float* bias;
+    uint16_t* out;     // [M][C] bf16
+    uint16_t* c4;      // optional [M][4]
+};
+// conv3 (C -> C/8, 3 taps at dilation dil, zero padding at each group's ends) + GroupNorm {sum, sumsq} of h per group
+// of L rows; x bf16 [M][C], h f32 [M][HF] (HF = C/8, or 8 for C = 48); -1 if the shape is not covered
 int dconv_conv3_launch(const uint16_t* x, const uint16_t* w, int kp, const float* bias, float* h, double* st,
                        int64_t M, int64_t L, int C, int dil, hipStream_t s);
 int dconv_apply_launch(const uint16_t* hb, const uint16_t* w, int kp, const float* bias, const double* st,
                        const float* gn_w, const float* gn_b, const float* scale, uint16_t* x, int64_t M, int64_t L,
-                       int C, hipStream_t s);
+                       int C, hipStream_t s, const DcRewrite* rw = nullptr);
 int dconv_small_launch(void* x, int x_bf16, float* h, int64_t nb, int64_t L, int C, int dil, const float* w3,
                        const float* b3, const float* g1w, const float* g1b, const float* w1, const float* b1,
                        const float* gram1, const float* g2w, const float* g2b, const float* scale, double* st_h,

@@ -126,9 +126,9 @@ void gn_gelu_bf16_launch(const float* h, bf16_t* out, int nb, int64_t per_batch,
 // sums go to the first active lane's group and, for lanes past a boundary, to the last lane's group).
 constexpr int GN_MOM_RMAX = 4;
 
-template <int H>
+template <int H, bool MULTI>
 __global__ __launch_bounds__(256) void gn_gelu_mom_kernel(const float* __restrict__ h, bf16_t* __restrict__ out,
-                                                          int64_t npos, int64_t L, int R,
+                                                          int64_t npos, int64_t L, int R_,
                                                           const double* __restrict__ st,
                                                           const float* __restrict__ w, const float* __restrict__ bb,
                                                           const float* __restrict__ gram, double* __restrict__ st_y) {
@@ -140,6 +140,7 @@ __global__ __launch_bounds__(256) void gn_gelu_mom_kernel(const float* __restric
     for (int i = threadIdx.x; i < 2 * H; i += 256) wb[i] = i < H ? w[i] : bb[i - H];
     __syncthreads();
     const int wv = threadIdx.x >> 6;
+    const int R = MULTI ? R_ : 1;     // (MULTI = false: one pass, no loop - the H = 24, 48 loop bodies spill SGPRs)
 #pragma unroll 1
     for (int it = 0; it < R; ++it) {
         const int64_t p0 = ((int64_t)blockIdx.x * R + it) * 256;
@@ -149,10 +150,11 @@ __global__ __launch_bounds__(256) void gn_gelu_mom_kernel(const float* __restric
         const int64_t g = pp / L;
         float mean, rstd;
         gn_params(st, g, L * H, mean, rstd);
-        float x[H];
-        const float4* hr = reinterpret_cast<const float4*>(h + pp * H);
+        constexpr int HF = H % 4 == 0 ? H : (H + 7) / 8 * 8;       // f32 input row stride (H = 6: 8, dconv_conv3)
+        float x[HF];
+        const float4* hr = reinterpret_cast<const float4*>(h + pp * HF);
 #pragma unroll
-        for (int q = 0; q < H / 4; ++q) {
+        for (int q = 0; q < HF / 4; ++q) {
             const float4 v = hr[q];
             x[4 * q] = v.x; x[4 * q + 1] = v.y; x[4 * q + 2] = v.z; x[4 * q + 3] = v.w;
         }
@@ -240,18 +242,19 @@ __global__ __launch_bounds__(256) void gn_gelu_mom_kernel(const float* __restric
 
 int gn_gelu_mom_launch(const float* h, uint16_t* out, int nb, int64_t L, int H, const double* stats, const float* w,
                        const float* b, const float* gram, double* st_y, hipStream_t s) {
-    if (L < 64 || (H != 12 && H != 24 && H != 48)) return -1;
+    if (L < 64 || (H != 6 && H != 12 && H != 24 && H != 48)) return -1;
     const int64_t npos = (int64_t)nb * L;
     // 256-position passes per workgroup: as many as keep >= 2048 workgroups (8 per CU), at most GN_MOM_RMAX
     const int64_t passes = (npos + 255) / 256;
-    const int R = (int)std::max<int64_t>(1, std::min<int64_t>(GN_MOM_RMAX, passes / 2048));
+    const int R = H <= 12 ? (int)std::max<int64_t>(1, std::min<int64_t>(GN_MOM_RMAX, passes / 2048)) : 1;
     const dim3 grid((unsigned)((passes + R - 1) / R));
     KScope ks(s);
     if (ks.on())
         ks.begin(klabel("gn_gelu_mom_kernel<%d>", H), 2.0 * npos * (H * H + 2 * H), (double)npos * H * (4 + 2));
-    if (H == 12) hipLaunchKernelGGL(gn_gelu_mom_kernel<12>, grid, dim3(256), 0, s, h, out, npos, L, R, stats, w, b, gram, st_y);
-    else if (H == 24) hipLaunchKernelGGL(gn_gelu_mom_kernel<24>, grid, dim3(256), 0, s, h, out, npos, L, R, stats, w, b, gram, st_y);
-    else hipLaunchKernelGGL(gn_gelu_mom_kernel<48>, grid, dim3(256), 0, s, h, out, npos, L, R, stats, w, b, gram, st_y);
+    if (H == 6) hipLaunchKernelGGL((gn_gelu_mom_kernel<6, true>), grid, dim3(256), 0, s, h, out, npos, L, R, stats, w, b, gram, st_y);
+    else if (H == 12) hipLaunchKernelGGL((gn_gelu_mom_kernel<12, true>), grid, dim3(256), 0, s, h, out, npos, L, R, stats, w, b, gram, st_y);
+    else if (H == 24) hipLaunchKernelGGL((gn_gelu_mom_kernel<24, false>), grid, dim3(256), 0, s, h, out, npos, L, R, stats, w, b, gram, st_y);
+    else hipLaunchKernelGGL((gn_gelu_mom_kernel<48, false>), grid, dim3(256), 0, s, h, out, npos, L, R, stats, w, b, gram, st_y);
     return (int)hipGetLastError();
 }
 
