@@ -83,6 +83,8 @@ struct Bufs {
     float* Ybt;         // the time branch's text cross-attention scratch (it runs on the second stream)
     void* Hmt;
     float *G, *D, *FO;
+    float* FO2 = nullptr;             // second freq-output buffer (chunks > 1): chunk c's iSTFT reads FO[c & 1] while
+                                      // chunk c + 1's decoder writes the other one
     float* ola_part;    // boundary partial sums of the fused iSTFT (spectral.hip)
     LrStep* lrsteps;    // level-1 low-rank decoder step table (fdec_lr.hip)
     void *S, *Z, *Zs;   // freq level 1 re-associated (fdec_lr.hip): per-tap products of the 32 / 8 source rows
@@ -173,6 +175,7 @@ size_t plan(Arena& ar, const Dims& d, Bufs& b, bool actbf) {
     b.Z = act(NI * 32 * Ts * 8 * DEC_CH[2]);
     b.Zs = act(d.Bc * 8 * Ts * 8 * DEC_CH[2]);
     b.FO = ar.take<float>(NI * Ts * Ts * 2);
+    if (d.chunks > 1) b.FO2 = ar.take<float>(NI * Ts * Ts * 2);
     b.ola_part = ar.take<float>(istft_ola_part_floats(NI, (int)Ts));
     b.lrsteps = ar.take<LrStep>(Ts + 1);
     return ar.off;
@@ -649,7 +652,7 @@ void conv_t(Run& r, const DecW& w, const void* A, int a_bf16, int nb, int H_in, 
 }
 
 void decode_chunk(Run& r, const Dims& d, const Bufs& b, int64_t s0, int64_t Bc, const float* text, bool text_per_item,
-                  float* out) {
+                  float* out, float* FO) {
     athd_ctx* c = r.c;
     KSection sec_dec("decoder");
     const int P = d.P;
@@ -750,7 +753,7 @@ void decode_chunk(Run& r, const Dims& d, const Bufs& b, int64_t s0, int64_t Bc, 
             // level-3 skip = saved[0][:, :4]: the compact copy the encoder wrote (4 channels per row)
             dl.fold = c->flast; dl.skip = eoff(b.sk4, s0 * 512 * Ts * 4, ea); dl.skip_bf16 = ab; dl.H_skip = skH[2];
             dl.C_skip = 4;
-            dl.out = b.FO;
+            dl.out = FO;
             r.check(fdec_tail_launch(dl, r.s), "fdec_tail");
         }
     }
@@ -810,16 +813,20 @@ void decode_chunk(Run& r, const Dims& d, const Bufs& b, int64_t s0, int64_t Bc, 
             xt2 = b.Gt;
         }
     }
-    (void)hipEventRecord(c->ev_t, s_t);              // join
-    (void)hipStreamWaitEvent(s_main, c->ev_t, 0);
-    r.s = s_main;
+    // join on the SECOND stream: the iSTFT runs there after both branches, so the next chunk's decoder (main stream)
+    // overlaps it; its time branch follows it on the second stream in stream order (xt2 is the time decoder's buffer),
+    // and forward_impl joins the second stream back into the caller's after the last chunk
+    (void)hipEventRecord(c->ev_f, s_main);
+    (void)hipStreamWaitEvent(s_t, c->ev_f, 0);
+    r.s = s_t;
     // ---- mask + iSTFT + overlap-add + denorm + branch sum (ATHTDemucs_v2.py:297-324), one fused pass ----
     b.xt2 = xt2;
     {
         KStage kst("istft");
-        istft_ola_launch(b.FO, NI, (int)Ts, P, d.T, b.specT + s0 * 2048 * Ts * 4, c->tw, r.actbf ? nullptr : c->tw64,
+        istft_ola_launch(FO, NI, (int)Ts, P, d.T, b.specT + s0 * 2048 * Ts * 4, c->tw, r.actbf ? nullptr : c->tw64,
                          c->win, c->win2, xt2, b.tnorm_std + 2 * s0, out + s0 * P * 2 * d.T, b.ola_part, r.s);
     }
+    r.s = s_main;
 }
 
 // Debug aid: ATHD_DUMP=<dir> makes the forward synchronise at the end and write the main intermediates of the
@@ -891,7 +898,11 @@ int forward_impl(athd_ctx* c, const float* wav, int64_t B, int64_t T, const floa
     for (int64_t ch = 0; ch < d.chunks && r.err == 0; ++ch) {
         const int64_t s0 = ch * d.Bc;
         const int64_t bc = std::min(d.Bc, B - s0);
-        decode_chunk(r, d, b, s0, bc, text, per_item, out);
+        decode_chunk(r, d, b, s0, bc, text, per_item, out, (ch & 1) && b.FO2 ? b.FO2 : b.FO);
+    }
+    if (r.err == 0 && !serial_branches(r)) {      // the last chunk's iSTFT (second stream) joins the caller's stream
+        (void)hipEventRecord(c->ev_t, c->s_time);
+        (void)hipStreamWaitEvent(r.s, c->ev_t, 0);
     }
     if (d.chunks == 1) dump_all(d, b, r.s);
     if (r.err) return c->fail(ATHD_EHIP, "launch failed in " + r.what + " (code " + std::to_string(r.err) + ")");
