@@ -198,6 +198,22 @@ def test_batch_independence(models):
     assert torch.allclose(full[1:2], one, atol=1e-5, rtol=1e-5)
 
 
+def test_decode_chunks_match_one_chunk(models):
+    """Several decode chunks (each chunk's iSTFT on the second stream, overlapping the next chunk's decoder, the freq
+    output double-buffered) == one chunk, f32 to fp32 rounding."""
+    from athd.synth import synthetic_batch
+    wav = torch.as_tensor(synthetic_batch(3, 40000, seed0=77)).cuda()
+    prompts = ["drums", "bass", "other", "vocals"]
+    m = models["f32"]
+    one = m.forward_prompts(wav, prompts)           # 12 items: one chunk at the default 64
+    m.set_decode_items(4)                           # 3 chunks of one segment x 4 prompts
+    try:
+        many = m.forward_prompts(wav, prompts)
+    finally:
+        m.set_decode_items(None)
+    assert torch.allclose(many, one, atol=1e-5, rtol=1e-4)
+
+
 def test_bench_batch_one_chunk(models):
     """The bench configuration (B=64 x 6 s x 4 prompts = 256 items, one decode chunk, the largest buffers and
     launch grids of the path) agrees with the same segments run as a 2-segment batch (bf16: >= 40 dB, see
@@ -207,7 +223,11 @@ def test_bench_batch_one_chunk(models):
     base = synthetic_batch(8, 264600, seed0=4242)
     wav = torch.as_tensor(np.concatenate([base] * 8)).cuda()          # (64, 2, 264600)
     m = models["bf16"]
-    full = m.forward_prompts(wav, prompts)
+    m.set_decode_items(256)                     # the bench's setting: all 256 items in one decode chunk
+    try:
+        full = m.forward_prompts(wav, prompts)
+    finally:
+        m.set_decode_items(None)
     pick = [0, 63]
     few = m.forward_prompts(wav[pick], prompts)
     for i, j in enumerate(pick):
