@@ -240,6 +240,104 @@ __global__ __launch_bounds__(256) void gn_gelu_mom_kernel(const float* __restric
     }
 }
 
+// H = 48 with the quadratic form split over the workgroup's 4 waves: a workgroup takes 64 positions, wave w
+// writes GELU(GN(h)) of channels [w H/4, (w + 1) H/4) of all 64 (one lane per position) and its bf16-rounded values
+// into an LDS row per position, then takes G rows [w H/4, (w + 1) H/4) (scalar loads, as above) against the whole row;
+// wave 0 adds the 4 partial forms.  4x the waves of gn_gelu_mom_kernel and a quarter of its serial G-row chain per
+// wave: level 3 has only 66 k / 132 k positions, so the one-wave-per-64-positions form left the CUs idle (fenc3
+// 0.104 -> 0.075 ms, tenc3 0.103 -> 0.051 for two launches; at H = 24 the split measured slower and is not used).
+template <int H>
+__global__ __launch_bounds__(256) void gn_gelu_mom_split_kernel(const float* __restrict__ h, bf16_t* __restrict__ out,
+                                                                int64_t npos, int64_t L,
+                                                                const double* __restrict__ st,
+                                                                const float* __restrict__ w,
+                                                                const float* __restrict__ bb,
+                                                                const float* __restrict__ gram,
+                                                                double* __restrict__ st_y) {
+    constexpr int QJ = H / 4;
+    static_assert(QJ % 2 == 0, "channel pairs");
+    __shared__ float wb[2 * H];
+    __shared__ float xs[64][H + 1];          // (odd pitch: the row reads of 64 lanes hit distinct banks)
+    __shared__ float red[4][64][3];
+    for (int i = threadIdx.x; i < 2 * H; i += 256) wb[i] = i < H ? w[i] : bb[i - H];
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t p = (int64_t)blockIdx.x * 64 + lane;
+    const bool act = p < npos;
+    const int64_t pp = act ? p : npos - 1;
+    const int64_t g = pp / L;
+    float mean, rstd;
+    gn_params(st, g, L * H, mean, rstd);
+    {
+        const int c0 = QJ * wv;
+        const float2* hr = reinterpret_cast<const float2*>(h + pp * H + c0);
+        uint32_t* o = reinterpret_cast<uint32_t*>(out + pp * H + c0);
+#pragma unroll
+        for (int q = 0; q < QJ / 2; ++q) {
+            const float2 v = hr[q];
+            const int c = c0 + 2 * q;
+            const uint32_t pk = pack2bf(gelu_fast((v.x - mean) * rstd * wb[c] + wb[H + c]),
+                                        gelu_fast((v.y - mean) * rstd * wb[c + 1] + wb[H + c + 1]));
+            if (act) o[q] = pk;
+            xs[lane][c] = __uint_as_float(pk << 16);
+            xs[lane][c + 1] = __uint_as_float(pk & 0xFFFF0000u);
+        }
+    }
+    __syncthreads();
+    float x[H];
+#pragma unroll
+    for (int k = 0; k < H; ++k) x[k] = xs[lane][k];
+    typedef __attribute__((address_space(4))) const float cfloat;    // constant address space: scalar loads
+    float qf = 0.f, lv = 0.f, lw = 0.f;
+    const int j0 = __builtin_amdgcn_readfirstlane(QJ * wv);
+#pragma unroll
+    for (int jj = 0; jj < QJ; ++jj) {
+        const int j = j0 + jj;
+        cfloat* gr = (cfloat*)(gram + j * H);
+        asm volatile("" : "+s"(gr), "+v"(qf));              // row j's loads after row j-1's products
+        float t4[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int k0 = 0; k0 < H; k0 += 24) {
+            cfloat* gk = gr + k0;
+            if (k0 > 0) asm volatile("" : "+s"(gk), "+v"(t4[0]));
+#pragma unroll
+            for (int k = 0; k < (H - k0 < 24 ? H - k0 : 24); ++k) t4[k & 3] = fmaf(gk[k], x[k0 + k], t4[k & 3]);
+        }
+        const float xj = xs[lane][j];
+        qf = fmaf(xj, (t4[0] + t4[1]) + (t4[2] + t4[3]), qf);
+        lv = fmaf(gr[H * (H - j) + j], xj, lv);             // gram[H*H + j]      = (W^T b)_j
+        lw = fmaf(gr[H * (H - j) + H + j], xj, lw);         // gram[H*H + H + j]  = (W^T 1)_j
+    }
+    red[wv][lane][0] = qf;
+    red[wv][lane][1] = lv;
+    red[wv][lane][2] = lw;
+    __syncthreads();
+    if (wv != 0) return;
+    qf = (red[0][lane][0] + red[1][lane][0]) + (red[2][lane][0] + red[3][lane][0]);
+    lv = (red[0][lane][1] + red[1][lane][1]) + (red[2][lane][1] + red[3][lane][1]);
+    lw = (red[0][lane][2] + red[1][lane][2]) + (red[2][lane][2] + red[3][lane][2]);
+    cfloat* gt = (cfloat*)(gram + H * H + 2 * H);
+    const float sb = gt[0], sb2 = gt[1];
+    const double s1 = act ? (double)(sb + lw) : 0.0;
+    const double s2 = act ? (double)(sb2 + (2.f * lv + qf)) : 0.0;
+    const int64_t gA = __builtin_amdgcn_readfirstlane((int)g);
+    const int64_t last = (int64_t)blockIdx.x * 64 + 63;
+    const int64_t gB = (last < npos ? last : npos - 1) / L;
+    const bool inA = g == gA;
+    const double a1 = wave_sum_d(inA ? s1 : 0.0), a2 = wave_sum_d(inA ? s2 : 0.0);
+    if (lane == 0) {
+        atomicAdd(&st_y[2 * gA], a1);
+        atomicAdd(&st_y[2 * gA + 1], a2);
+    }
+    if (gB != gA) {
+        const double b1 = wave_sum_d(inA ? 0.0 : s1), b2 = wave_sum_d(inA ? 0.0 : s2);
+        if (lane == 0) {
+            atomicAdd(&st_y[2 * gB], b1);
+            atomicAdd(&st_y[2 * gB + 1], b2);
+        }
+    }
+}
+
 int gn_gelu_mom_launch(const float* h, uint16_t* out, int nb, int64_t L, int H, const double* stats, const float* w,
                        const float* b, const float* gram, double* st_y, hipStream_t s) {
     if (L < 64 || (H != 6 && H != 12 && H != 24 && H != 48)) return -1;
@@ -250,11 +348,12 @@ int gn_gelu_mom_launch(const float* h, uint16_t* out, int nb, int64_t L, int H, 
     const dim3 grid((unsigned)((passes + R - 1) / R));
     KScope ks(s);
     if (ks.on())
-        ks.begin(klabel("gn_gelu_mom_kernel<%d>", H), 2.0 * npos * (H * H + 2 * H), (double)npos * H * (4 + 2));
+        ks.begin(klabel(H <= 24 ? "gn_gelu_mom_kernel<%d>" : "gn_gelu_mom_split_kernel<%d>", H), 2.0 * npos * (H * H + 2 * H),
+                 (double)npos * H * (4 + 2));
     if (H == 6) hipLaunchKernelGGL((gn_gelu_mom_kernel<6, true>), grid, dim3(256), 0, s, h, out, npos, L, R, stats, w, b, gram, st_y);
     else if (H == 12) hipLaunchKernelGGL((gn_gelu_mom_kernel<12, true>), grid, dim3(256), 0, s, h, out, npos, L, R, stats, w, b, gram, st_y);
     else if (H == 24) hipLaunchKernelGGL((gn_gelu_mom_kernel<24, false>), grid, dim3(256), 0, s, h, out, npos, L, R, stats, w, b, gram, st_y);
-    else hipLaunchKernelGGL((gn_gelu_mom_kernel<48, false>), grid, dim3(256), 0, s, h, out, npos, L, R, stats, w, b, gram, st_y);
+    else hipLaunchKernelGGL((gn_gelu_mom_split_kernel<48>), dim3((unsigned)((npos + 63) / 64)), dim3(256), 0, s, h, out, npos, L, stats, w, b, gram, st_y);
     return (int)hipGetLastError();
 }
 
