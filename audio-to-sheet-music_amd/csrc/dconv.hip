@@ -538,35 +538,13 @@ __global__ __launch_bounds__(NW * 64) void dconv_conv3_kernel(const DcConv3 d) {
         }
         r1 = r2 = 0.0;
     };
-    for (int64_t u = u0; u < u1; ++u) {
+    // unit epilogue: h store + GroupNorm sums (the unit's rows belong to group gb0 of its first row or, past a
+    // boundary, gb0 + 1: L >= 16)
+    auto finish = [&](int64_t u, const f32x4_t* acc) {
         const int64_t m = u * 16 + fr;
         const bool ok = m < d.M;
         const int64_t mm = ok ? m : d.M - 1;
         const int64_t gb = mm / d.L;
-        const int t = (int)(mm - gb * d.L);
-        f32x4_t acc[NT];
-#pragma unroll
-        for (int j = 0; j < NT; ++j) acc[j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 1
-        for (int tap = 0; tap < 3; ++tap) {
-            const int tt = t + (tap - 1) * d.dil;
-            const bool in = tt >= 0 && tt < (int)d.L;
-            const uint16_t* xr = d.x + (mm + (in ? (int64_t)(tap - 1) * d.dil : 0)) * C + 8 * g;
-            bf16v8 bf[KS];
-#pragma unroll
-            for (int ks = 0; ks < KS; ++ks)
-                bf[ks] = in && 32 * ks + 8 * g < C ? *reinterpret_cast<const bf16v8*>(xr + 32 * ks) : bf16v8{};
-#pragma unroll
-            for (int ks = 0; ks < KS; ++ks) {
-                const int q = (tap * C + 32 * ks) / 8 + g;
-#pragma unroll
-                for (int j = 0; j < NT; ++j) {
-                    const bf16v8 af = *reinterpret_cast<const bf16v8*>(wl + (16 * j + fr) * RB + ((q ^ (fr & 7)) * 16));
-                    acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf[ks], acc[j], 0, 0, 0);
-                }
-            }
-        }
-        // the unit's rows belong to group gb0 (first row) or, past a boundary, gb0 + 1 (L >= 16)
         const int64_t gb0 = (u * 16) / d.L;
         float s1a = 0.f, s2a = 0.f, s1b = 0.f, s2b = 0.f;
 #pragma unroll
@@ -595,6 +573,99 @@ __global__ __launch_bounds__(NW * 64) void dconv_conv3_kernel(const DcConv3 d) {
             r1 = (double)s1b;
             r2 = (double)s2b;
         }
+    };
+    // C = 96, 192: steps (unit, tap) in ping-pong buffers (below); C = 48, 384 measured slower that way (one box: 0.34
+    // -> 0.37 and 0.17 -> 0.18 ms) and keep one tap at a time with the zeroing at the load
+    constexpr bool PP = C == 96 || C == 192;
+    // lane row of unit u (clamped) and its position in the group row (32-bit: M < 2^31, launcher)
+    auto unit_row = [&](int64_t u, int64_t& mm, int& t) {
+        const int64_t m = u * 16 + fr;
+        mm = m < d.M ? m : d.M - 1;
+        t = (int)((uint32_t)mm % (uint32_t)d.L);
+    };
+    // B fragments of one tap: x[mm + (tap - 1) dil][32 ks + 8 g ..]; returns whether the tap row lies inside the group
+    // row.  PP: the loads are unconditional (rows outside the group read the lane's own row, K-steps past C its first
+    // chunk) and the fragments are zeroed where they are used, so a prefetched step is not waited for at the load.
+    auto load_tap = [&](int64_t mm, int t, int tap, bf16v8* bf) -> bool {
+        const int tt = t + (tap - 1) * d.dil;
+        const bool in = tt >= 0 && tt < (int)d.L;
+        const uint16_t* xr = d.x + (mm + (in ? (int64_t)(tap - 1) * d.dil : 0)) * C + 8 * g;
+        if constexpr (PP) {
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks)
+                bf[ks] = *reinterpret_cast<const bf16v8*>(xr + (32 * ks + 8 * g < C ? 32 * ks : 0));
+        } else {
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks)
+                bf[ks] = in && 32 * ks + 8 * g < C ? *reinterpret_cast<const bf16v8*>(xr + 32 * ks) : bf16v8{};
+        }
+        return in;
+    };
+    auto mfma_tap = [&](int tap, bool in, const bf16v8* bf, f32x4_t* acc) {
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            const int q = (tap * C + 32 * ks) / 8 + g;
+            const bf16v8 b = !PP || (in && 32 * ks + 8 * g < C) ? bf[ks] : bf16v8{};
+#pragma unroll
+            for (int j = 0; j < NT; ++j) {
+                const bf16v8 af = *reinterpret_cast<const bf16v8*>(wl + (16 * j + fr) * RB + ((q ^ (fr & 7)) * 16));
+                acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, b, acc[j], 0, 0, 0);
+            }
+        }
+    };
+    f32x4_t acc[NT];
+    if constexpr (PP) {
+        // the load side runs one step ahead of the compute side: the next step's fragments are in flight during
+        // this step's MFMAs and the unit epilogue (registers: 2 x 4 KS)
+        int64_t lu = u0, lmm = 0, cu = u0;
+        int ltap = 0, lt = 0, ctap = 0;
+        if (u0 < u1) unit_row(u0, lmm, lt);
+        auto advance = [&]() {
+            if (++ltap == 3) {
+                ltap = 0;
+                if (++lu < u1) unit_row(lu, lmm, lt);
+            }
+        };
+        auto compute = [&](bool in, const bf16v8* bf) {
+            if (ctap == 0) {
+#pragma unroll
+                for (int j = 0; j < NT; ++j) acc[j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+            }
+            mfma_tap(ctap, in, bf, acc);
+            if (ctap == 2) {
+                finish(cu, acc);
+                ctap = 0;
+                ++cu;
+            } else {
+                ++ctap;
+            }
+        };
+        bf16v8 ba[KS], bb[KS];
+        bool ia = false, ib = false;
+        if (lu < u1) { ia = load_tap(lmm, lt, ltap, ba); advance(); }
+#pragma unroll 1
+        while (cu < u1) {
+            if (lu < u1) { ib = load_tap(lmm, lt, ltap, bb); advance(); }
+            compute(ia, ba);
+            if (cu >= u1) break;
+            if (lu < u1) { ia = load_tap(lmm, lt, ltap, ba); advance(); }
+            compute(ib, bb);
+        }
+    } else {
+        for (int64_t u = u0; u < u1; ++u) {
+            int64_t mm;
+            int t;
+            unit_row(u, mm, t);
+#pragma unroll
+            for (int j = 0; j < NT; ++j) acc[j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+            for (int tap = 0; tap < 3; ++tap) {
+                bf16v8 bf[KS];
+                const bool in = load_tap(mm, t, tap, bf);
+                mfma_tap(tap, in, bf, acc);
+            }
+            finish(u, acc);
+        }
     }
     flush();
 }
@@ -605,7 +676,7 @@ bool dconv_conv3_supported(int C, int H, int kp, int64_t L) {
 
 int dconv_conv3_launch(const uint16_t* x, const uint16_t* w, int kp, const float* bias, float* h, double* st,
                        int64_t M, int64_t L, int C, int dil, hipStream_t s) {
-    if (!dconv_conv3_supported(C, C / 8, kp, L) || M <= 0) return -1;
+    if (!dconv_conv3_supported(C, C / 8, kp, L) || M <= 0 || M >= (1LL << 31)) return -1;
     DcConv3 d;
     d.x = x; d.w = w; d.bias = bias; d.h = h; d.st = st; d.M = M; d.L = L; d.kp = kp; d.dil = dil;
     static int cus = 0;
