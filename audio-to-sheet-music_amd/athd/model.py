@@ -42,7 +42,7 @@ class AudioTextHTDemucs:
         self.segment = segment
         self.dtype = dtype
         # (segment, prompt) items per decode chunk (athd_set_decode_items; None = the library default, 64).  256 puts
-        # a 64-segment x 4-prompt batch in one chunk (≈48 GB: athd_workspace_bytes, reported by bench.py as workspace_gb).
+        # a 64-segment x 4-prompt batch in one chunk (≈49 GB at round 3: athd_workspace_bytes, reported by bench.py as workspace_gb).
         self.decode_items = decode_items
         self.embedder = PromptEmbedder(clap_encoder, clap_tokenizer, text_table)
         self._weights: Dict[str, np.ndarray] = {}

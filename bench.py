@@ -221,7 +221,7 @@ def main():
     sd = synthetic_state_dict(seed=0)
     table = synthetic_text_table(4, seed=7)
     B = args.batch
-    # the whole per-GPU batch in one decode chunk (B x 4 items): fewer, larger decoder launches (≈48 GB: athd_workspace_bytes, reported as workspace_gb)
+    # the whole per-GPU batch in one decode chunk (B x 4 items): fewer, larger decoder launches (≈49 GB: athd_workspace_bytes, reported as workspace_gb)
     model = AudioTextHTDemucs(dtype=args.dtype, text_table={s: table[i] for i, s in enumerate(STEMS)},
                               decode_items=B * len(STEMS))
     model.load_state_dict(sd)

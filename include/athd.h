@@ -64,7 +64,7 @@ int athd_finalize(athd_ctx* ctx);
 
 /* (segment, prompt) items the decoder processes per chunk (default 64; 1..4096).  The encoder's buffers scale
  * with B and the decoder's with this setting: at B = 64, T = 264600 (6 s), P = 4 the workspace is about 18 GB
- * at 64 items and about 48 GB at 256 (the whole batch in one decode chunk: fewer, larger launches, the bench setting).
+ * at 64 items and about 49 GB at 256 (the whole batch in one decode chunk: fewer, larger launches, the bench setting).
  * Takes effect for the next athd_workspace_bytes / athd_forward* calls; the environment variable
  * ATHD_DECODE_ITEMS overrides it. */
 int athd_set_decode_items(athd_ctx* ctx, int64_t items);
