@@ -7,11 +7,15 @@ Mirrors `test_inference.py`:
                           go through `forward_prompts` (encode once, decode once per stem), the fades and the
                           additive overlap-add run in `athd_overlap_add` (same fp32 additions, same order)
   * `sdr_loss`         <- `src/loss.py:9-30` (device reduction, fp64 sums); `test_inference.py:153` uses -sdr_loss
-  * `test_inference`   <- `test_inference.py:43-155` minus the MUSDB decode / wav writing / plotting
+  * `separate_and_score` <- `test_inference.py:91-155` on an in-memory track
+  * `test_inference`   <- `test_inference.py:43-205` (same signature and defaults: checkpoint, first track of
+                          data_dir, per-stem SDR dict, extracted_{stem}.wav + mixture.wav; no plots)
+  * `load_config`, `main` <- `utils.py:18-23`, `test_inference.py:208-218`
 """
 from __future__ import annotations
 
 from dataclasses import dataclass
+from pathlib import Path
 from typing import Dict, List, Optional, Sequence
 
 import numpy as np
@@ -172,14 +176,76 @@ def sisdr_loss(estimated: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
 
 
 @torch.no_grad()
-def test_inference(model: AudioTextHTDemucs, mixture: torch.Tensor, references: Optional[torch.Tensor] = None,
-                   stems: Sequence[str] = STEMS, sample_rate: int = 44100, segment_seconds: float = 6.0,
-                   overlap: float = 0.1):
-    """`test_inference.py:43-155` on an in-memory track: mixture (2, L); references (S, 2, L) true stems (optional).
-    Returns (final (S, 2, L), {stem: SDR dB}) with SDR = -sdr_loss(estimate, reference) per stem (`:147-155`)."""
+def separate_and_score(model: AudioTextHTDemucs, mixture: torch.Tensor, references: Optional[torch.Tensor] = None,
+                       stems: Sequence[str] = STEMS, sample_rate: int = 44100, segment_seconds: float = 6.0,
+                       overlap: float = 0.1):
+    """The body of `test_inference.py:91-155` on an in-memory track: mixture (2, L); references (S, 2, L) true stems
+    (optional).  Returns (final (S, 2, L), {stem: SDR dB}) with SDR = -sdr_loss(estimate, reference) per stem for the
+    first min(S, 4) stems (`:147-155`), -30.0 for the others and when no references are given."""
     final = separate_track(model, mixture, stems, sample_rate, segment_seconds, overlap)
     scores = {s: -30.0 for s in stems}
     if references is not None:
-        for i, s in enumerate(stems[:4]):
+        for i, s in enumerate(list(stems)[:4]):
             scores[s] = float(-sdr_loss(final[i], references[i]).item())
     return final, scores
+
+
+def cleaned_track_name(filename) -> str:
+    """The output directory name of `test_inference.py:159-162`: `Path(filename).stem` without ".stem", "-" and
+    "'", spaces as "_"."""
+    name = Path(filename).stem.replace(".stem", "")
+    return name.replace("-", "").replace("'", "").replace(" ", "_")
+
+
+@torch.no_grad()
+def test_inference(checkpoint_path: str = "checkpoints/best_model.pt", data_dir: str = "data/quick_train",
+                   output_dir: str = "results", sample_rate: int = 44100, segment_seconds: float = 6.0,
+                   overlap: float = 0.1, device: Optional[str] = None, *,
+                   text_table: Optional[Dict[str, np.ndarray]] = None, clap=None, tokenizer=None,
+                   dtype: str = "bf16", stems: Sequence[str] = STEMS, return_final: bool = False):
+    """`test_inference.py:43-205` with the same positional signature and defaults (`:44-52`).
+
+    Loads the checkpoint (`load_model`, `:71`), takes the first track of `data_dir` (`dataset.files[0]`, `:85-90`;
+    MUSDB18-HQ directories / `.stem.npy` here, see athd/musdb.py), separates every stem with the 6 s window loop
+    (`:92-141`, batched through `forward_prompts`), scores stems 0..3 against the true stems with -sdr_loss (`:147-155`)
+    and writes `<output_dir>/<cleaned name>/extracted_{stem}.wav` for every stem and `mixture.wav` (`:157-175`, 16-bit
+    PCM like soundfile's WAV default).  Returns the `{stem: SDR dB}` dict (`:205`); with `return_final=True`
+    (sdr_scores, final (S, 2, L) on the device).  The keyword-only arguments are this build's: the prompt embeddings
+    (`text_table` or a local CLAP `clap`/`tokenizer`, athd/text.py: the reference's `from_pretrained` at `:27-28` is
+    not reachable offline) and the compute dtype.  The spectrogram plots of `:177-185` are not drawn (no display)."""
+    from .musdb import MusDBTracks, write_wav
+    if device is None:
+        device = "cuda"
+        if not torch.cuda.is_available():
+            raise RuntimeError("athd runs on a HIP device only (there is no CPU path)")
+    model = load_model(checkpoint_path, device, dtype=dtype, text_table=text_table, clap=clap, tokenizer=tokenizer)
+    tracks = MusDBTracks(data_dir, sample_rate=sample_rate)
+    all_stems = torch.from_numpy(tracks.load_stems(0)).permute(0, 2, 1).float().to(model.device)   # (5, C, T)
+    full_mixture = all_stems[0]
+    final, sdr_scores = separate_and_score(model, full_mixture, all_stems[1:], stems, sample_rate, segment_seconds,
+                                           overlap)
+    for i in range(min(len(stems), 4)):
+        print(f"{stems[i]:8s} | SDR: {sdr_scores[stems[i]]:6.2f} dB")
+    if output_dir:
+        f0 = tracks.files[0]       # an HQ directory stands for the reference's "<name>.stem.mp4"
+        full_dir = Path(output_dir) / cleaned_track_name(f0.name + ".stem.mp4" if f0.is_dir() else f0)
+        full_dir.mkdir(parents=True, exist_ok=True)
+        for i, s in enumerate(stems):
+            write_wav(full_dir / f"extracted_{s}.wav", final[i].cpu().numpy().T, sample_rate)
+        write_wav(full_dir / "mixture.wav", full_mixture.cpu().numpy().T, sample_rate)
+    return (sdr_scores, final) if return_final else sdr_scores
+
+
+def load_config(file_path) -> dict:
+    """`utils.py:18-23`: a YAML file through `yaml.safe_load`."""
+    import yaml
+    with open(file_path, "r") as f:
+        return yaml.safe_load(f)
+
+
+def main(config_path: str = "config.yaml", **kw):
+    """`test_inference.py:208-218`: the checkpoint, data and output paths and the audio constants from config.yaml."""
+    cfg = load_config(config_path)
+    return test_inference(checkpoint_path=str(Path(cfg["wandb"]["checkpoint_dir"]) / "best_model.pt"),
+                          data_dir=cfg["data"]["test_dir"], output_dir=cfg["wandb"]["output_dir"],
+                          sample_rate=cfg["data"]["sample_rate"], segment_seconds=cfg["data"]["segment_seconds"], **kw)

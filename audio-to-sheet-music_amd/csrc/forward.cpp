@@ -659,6 +659,11 @@ void decode_chunk(Run& r, const Dims& d, const Bufs& b, int64_t s0, int64_t Bc, 
     const int NI = (int)(Bc * P);
     const int64_t Ts = d.Tspec;
     const int ab = r.actbf ? 1 : 0;
+    // Chunk ordering: the previous chunk's time branch (second stream) recorded ev_t after its text cross-attention,
+    // i.e. after it read tc0 / tc2 / avec, and - in stream order - after the iSTFT of the chunk before it, the last
+    // reader of the FO buffer this chunk's fdec_tail rewrites (FO[c & 1] == FO[(c - 2) & 1]).  Waiting on it here
+    // orders both write-after-read pairs; at chunk 0 ev_t is the encoder's join, already waited on.
+    if (s0 > 0 && !serial_branches(r)) (void)hipStreamWaitEvent(r.s, c->ev_t, 0);
     // ---- text cross-attention, closed form (ATHTDemucs_v2.py:38-58) ----
     text_vec_launch(text_per_item ? text + s0 * 512 : text, NI, P, text_per_item ? 1 : 0, c->ta_maT, c->ta_ma, c->ta_mcT,
                     c->ta_mc, c->ta_m2b, b.avec, b.tc0, b.tc2, r.s);
@@ -762,6 +767,7 @@ void decode_chunk(Run& r, const Dims& d, const Bufs& b, int64_t s0, int64_t Bc, 
     float* xt2 = nullptr;                            // time_out(time decoder) [NI][T][2]
     r.s = s_t;
     text_attn(b.xt_enc + s0 * d.Nt * 384, b.xt_enc_b ? b.xt_enc_b + s0 * d.Nt * 384 : nullptr, d.Nt, b.xt_cond, b.Hmt, b.Ybt);
+    if (!serial_branches(r)) (void)hipEventRecord(c->ev_t, s_t);   // tc0 / tc2 read: the next chunk may rewrite them
     {
         const void* svt[4] = {eoff(b.saved_t[0], s0 * d.L[1] * 48, ea), eoff(b.saved_t[1], s0 * d.L[2] * 96, ea),
                               eoff(b.saved_t[2], s0 * d.L[3] * 192, ea), eoff(b.saved_t[3], s0 * d.L[4] * 384, ea)};

@@ -214,10 +214,35 @@ def test_decode_chunks_match_one_chunk(models):
     assert torch.allclose(many, one, atol=1e-5, rtol=1e-4)
 
 
-def test_bench_batch_one_chunk(models):
-    """The bench configuration (B=64 x 6 s x 4 prompts = 256 items, one decode chunk, the largest buffers and
-    launch grids of the path) agrees with the same segments run as a 2-segment batch (bf16: >= 40 dB, see
-    test_forward_prompts_matches_forward)."""
+@pytest.mark.parametrize("dt", ["f32", "bf16"])
+def test_decode_chunks_per_item_prompts(models, dt):
+    """athd_forward with a DIFFERENT prompt per segment over 5 decode chunks of one item each: every chunk rewrites
+    the prompt row vectors (text_vec_kernel) and every other chunk the freq output buffer, while the previous
+    chunk's time branch and iSTFT may still run on the second stream (forward.cpp decode_chunk orders both with
+    ev_t).  Equals one chunk (f32: fp32 rounding; bf16: >= 40 dB, order-dependent statistics)."""
+    from athd.synth import synthetic_batch
+    wav = torch.as_tensor(synthetic_batch(5, 40000, seed0=78)).cuda()
+    prompts = ["drums", "vocals", "bass", "other", "vocals"]
+    m = models[dt]
+    one = m(wav, prompts)                           # 5 items: one chunk at the default 64
+    m.set_decode_items(1)                           # 5 chunks of one (segment, prompt) item
+    try:
+        many = m(wav, prompts)
+        torch.cuda.synchronize()
+    finally:
+        m.set_decode_items(None)
+    if dt == "f32":
+        assert torch.allclose(many, one, atol=1e-5, rtol=1e-4)
+    else:
+        for i in range(5):
+            assert sdr_db(one[i].cpu().numpy(), many[i].cpu().numpy()) >= 40.0, i
+
+
+def test_bench_batch_one_chunk(models, oracle_model, text_table):
+    """The bench configuration exactly as timed: B=64 x 6 s x 4 prompts = 256 items in one decode chunk (the
+    largest buffers and launch grids of the path), captured as a HIP graph and REPLAYED (bench.py at N=1).  Rows 0
+    and 63 of the replayed output against the fp32 oracle's forward_prompts (bf16 gate BF16_SDR_DB), and against
+    the same segments run as a 2-segment eager batch."""
     from athd.synth import synthetic_batch
     prompts = ["drums", "bass", "other", "vocals"]
     base = synthetic_batch(8, 264600, seed0=4242)
@@ -225,15 +250,25 @@ def test_bench_batch_one_chunk(models):
     m = models["bf16"]
     m.set_decode_items(256)                     # the bench's setting: all 256 items in one decode chunk
     try:
-        full = m.forward_prompts(wav, prompts)
+        g, full = m.capture_prompts(wav, prompts)
+        full.zero_()
+        g.replay()
+        torch.cuda.synchronize()
     finally:
         m.set_decode_items(None)
     pick = [0, 63]
     few = m.forward_prompts(wav[pick], prompts)
+    ref = oracle_model.forward_prompts(wav[pick].cpu(), torch.as_tensor(text_table)).numpy()
+    res = {}
     for i, j in enumerate(pick):
         for p in range(len(prompts)):
-            assert sdr_db(few[i, p].cpu().numpy(), full[j, p].cpu().numpy()) >= 40.0, (j, prompts[p])
-    del full, few
+            got = full[j, p].cpu().numpy()
+            s_or = sdr_db(ref[i, p], got)
+            res[f"{j}/{prompts[p]}"] = s_or
+            assert s_or >= BF16_SDR_DB, (j, prompts[p], s_or)
+            assert sdr_db(few[i, p].cpu().numpy(), got) >= 40.0, (j, prompts[p])
+    _report("bench_config_graph_replay_vs_oracle/bf16", res)
+    del g, full, few
     torch.cuda.empty_cache()
 
 

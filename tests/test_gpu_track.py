@@ -107,7 +107,7 @@ def test_loss_known_answers_main_py():
 def test_separate_track_matches_oracle_loop(state_dict, text_table, oracle_model):
     """12.1 s track, 3 windows (2 full + a 10k-sample tail), 2 stems, f32 model vs the oracle running the
     reference loop window by window (B=1, one stem at a time)."""
-    from athd.inference import separate_track, test_inference
+    from athd.inference import separate_and_score, separate_track
     from athd.model import AudioTextHTDemucs
     from athd.synth import synthetic_mixture
     from athd.weights import STEMS
@@ -127,5 +127,49 @@ def test_separate_track_matches_oracle_loop(state_dict, text_table, oracle_model
             ref[si, :, st:en] += linear_fade(out, fi, fo)[0]
     for si in range(2):
         assert _sdr(ref[si], got[si]) >= 70.0, (stems[si], _sdr(ref[si], got[si]))
-    final, scores = test_inference(m, mix.cuda(), ref.cuda(), stems)
+    final, scores = separate_and_score(m, mix.cuda(), ref.cuda(), stems)
     assert all(v >= 29.99 for v in scores.values()), scores      # clamped at +30 dB like sdr_loss
+
+
+def test_test_inference_reference_signature(tmp_path, state_dict, text_table, oracle_model):
+    """`test_inference.py:43-205` through the reference's own signature: a torch.save checkpoint and a one-track
+    MUSDB18-HQ directory in, the per-stem SDR dict out, `<output_dir>/<cleaned name>/extracted_{stem}.wav` and
+    `mixture.wav` written (`:157-175`).  f32 estimates vs the oracle running the reference loop window by window
+    (>= 70 dB per stem), the returned SDRs == the oracle's sdr_loss of the device estimates, and the WAVs read back
+    equal to the 16-bit PCM image of `final`."""
+    from athd.inference import test_inference as run_test_inference
+    from athd.musdb import HQ_FILES, read_wav, write_wav
+    from athd.synth import synthetic_mixture
+    from athd.weights import STEMS
+    L = 2 * 260190 + 30000                               # 3 windows: 2 full + a 30000-sample tail
+    data = tmp_path / "quick_test"
+    d = data / "Art's Band - A Song"
+    d.mkdir(parents=True)
+    parts = [0.5 * synthetic_mixture(L, seed=500 + j) for j in range(4)]
+    for f, x in zip(HQ_FILES, [sum(parts)] + parts):
+        write_wav(d / f"{f}.wav", x, 44100, "FLOAT")
+    sd = {k: torch.as_tensor(np.asarray(v)) for k, v in state_dict.items()}
+    ckpt = tmp_path / "best_model.pt"
+    torch.save({"model_state_dict": sd, "epoch": 3}, ckpt)
+    table = {s: text_table[i] for i, s in enumerate(STEMS)}
+    scores, final = run_test_inference(str(ckpt), str(data), str(tmp_path / "results"), 44100, 6.0, 0.1, "cuda",
+                                       text_table=table, dtype="f32", return_final=True)
+    assert list(scores) == STEMS
+    mix = torch.as_tensor(read_wav(d / "mixture.wav")[0].T.copy())
+    for si, s in enumerate(STEMS):
+        te = torch.as_tensor(text_table[si][None])
+        ref = torch.zeros((2, L))
+        for st, en, fi, fo in chunk_plan(L):
+            ref[:, st:en] += linear_fade(oracle_model.forward(mix[:, st:en][None], te), fi, fo)[0]
+        got = final[si].cpu()
+        assert _sdr(ref, got) >= 70.0, (s, _sdr(ref, got))
+        truth = torch.as_tensor(read_wav(d / f"{s}.wav")[0].T.copy())
+        want = sdr_db(got, truth)
+        assert abs(scores[s] - want) < 1e-4, (s, scores[s], want)
+    out = tmp_path / "results" / "Arts_Band__A_Song"           # test_inference.py:159-163 name cleaning
+    for i, s in enumerate(STEMS):
+        back = read_wav(out / f"extracted_{s}.wav")[0]
+        img = np.clip(np.rint(final[i].cpu().numpy().T * 32767.0), -32768, 32767) / 32768.0
+        assert np.array_equal(back, img.astype(np.float32)), s
+    back = read_wav(out / "mixture.wav")[0]
+    assert np.array_equal(back, (np.clip(np.rint(mix.numpy().T * 32767.0), -32768, 32767) / 32768.0).astype(np.float32))

@@ -48,3 +48,36 @@ def test_model_rejects_cpu_device():
     from athd.model import AudioTextHTDemucs
     with pytest.raises(RuntimeError):
         AudioTextHTDemucs().to("cpu")
+
+
+def test_test_inference_signature_matches_reference():
+    """test_inference.py:44-52: same positional parameters and defaults (the build adds keyword-only ones)."""
+    import inspect
+    from athd.inference import test_inference as ti
+    ps = [p for p in inspect.signature(ti).parameters.values() if p.kind == p.POSITIONAL_OR_KEYWORD]
+    assert [(p.name, p.default) for p in ps] == [
+        ("checkpoint_path", "checkpoints/best_model.pt"), ("data_dir", "data/quick_train"), ("output_dir", "results"),
+        ("sample_rate", 44100), ("segment_seconds", 6.0), ("overlap", 0.1), ("device", None)]
+
+
+@pytest.mark.parametrize("name,want", [("Al James - Schoolboy Facination.stem.mp4", "Al_James__Schoolboy_Facination"),
+                                       ("/x/y/Mu's Band - Track-1.stem.npy", "Mus_Band__Track1"),
+                                       ("Dr. Who - Theme.stem.mp4", "Dr._Who__Theme")])
+def test_cleaned_track_name(name, want):
+    """test_inference.py:159-162."""
+    from athd.inference import cleaned_track_name
+    assert cleaned_track_name(name) == want
+
+
+def test_main_reads_config_keys(tmp_path, monkeypatch):
+    """test_inference.py:208-218: checkpoint_dir/best_model.pt, data.test_dir, wandb.output_dir, sample_rate and
+    segment_seconds come from config.yaml (utils.load_config = yaml.safe_load)."""
+    import athd.inference as inf
+    cfg = tmp_path / "config.yaml"
+    cfg.write_text("data:\n  test_dir: /d/test\n  segment_seconds: 6.0\n  sample_rate: 44100\n"
+                   "wandb:\n  checkpoint_dir: ck/2025/\n  output_dir: res/2025\n")
+    seen = {}
+    monkeypatch.setattr(inf, "test_inference", lambda **kw: seen.update(kw) or {"ok": 1})
+    assert inf.main(str(cfg)) == {"ok": 1}
+    assert seen == {"checkpoint_path": "ck/2025/best_model.pt", "data_dir": "/d/test", "output_dir": "res/2025",
+                    "sample_rate": 44100, "segment_seconds": 6.0}
