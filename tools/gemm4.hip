@@ -13,9 +13,9 @@
 // barrier (a __syncthreads() would drain them: it waits vmcnt(0)).  Register budget (2 waves per SIMD): 128
 // accumulators + 64 fragment registers + compact 32-bit addressing, no spills.
 // Same descriptor, implicit-conv A addressing and epilogue (C^T tiles, gemm_epi.h) as the other GEMM kernels.
-#include "common.h"
-#include "prof.h"
-#include "gemm.h"
+#include "../audio-to-sheet-music_amd/csrc/common.h"
+#include "../audio-to-sheet-music_amd/csrc/prof.h"
+#include "../audio-to-sheet-music_amd/csrc/gemm.h"
 #ifdef ATHD_G4_STAMP
 namespace athd {
 __device__ uint64_t* g4_stamp = nullptr;
@@ -27,7 +27,7 @@ constexpr int G4_NSTAMP = 24;
             athd::g4_stamp[(int64_t)blockIdx.x * athd::G4_NSTAMP + (i)] = __builtin_amdgcn_s_memtime();        \
     } while (0)
 #endif
-#include "gemm_epi.h"
+#include "../audio-to-sheet-music_amd/csrc/gemm_epi.h"
 
 #include <climits>
 #include <cstdlib>
