@@ -183,11 +183,14 @@ class AudioTextHTDemucs:
         return out
 
     @torch.no_grad()
-    def capture_prompts(self, wav: torch.Tensor, prompts: List[str], out: Optional[torch.Tensor] = None):
+    def capture_prompts(self, wav: torch.Tensor, prompts: List[str], out: Optional[torch.Tensor] = None,
+                        workspace: Optional[torch.Tensor] = None):
         """`forward_prompts` on these exact buffers captured into one HIP graph (torch.cuda.CUDAGraph over the
         library's launches: both branch streams, their event fork / joins and the statistics memset).  Returns
         (graph, out): `graph.replay()` re-runs every kernel of the forward on the same device buffers, so the caller
         refreshes `wav` in place between replays; the prompt rows, the workspace and `out` stay bound to the graph.
+        The graph owns its workspace (not the model's cached one), so replays may overlap eager calls on other streams;
+        graphs replayed only in order on ONE stream may share a caller-given `workspace` (e.g. ping-pong outputs).
         `wav` must already be a contiguous float32 (B, 2, T) tensor on the model's device (no copy is captured)."""
         if wav.dtype != torch.float32 or not wav.is_contiguous():
             raise ValueError("capture_prompts needs a contiguous float32 wav (B, 2, T)")
@@ -198,13 +201,23 @@ class AudioTextHTDemucs:
         P = table.shape[0]
         if out is None:
             out = torch.empty((B, P, 2, T), dtype=torch.float32, device=self.device)
-        ws = self._workspace(ctx.workspace_bytes(B, T, P))
+        # a workspace of the graph's own: an eager forward on this model (self._ws) may run on another stream while
+        # the graph replays, and the two must not share scratch memory
+        nbytes = ctx.workspace_bytes(B, T, P)
+        if workspace is None:
+            ws = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
+        elif workspace.dtype != torch.uint8 or workspace.numel() < nbytes or workspace.device != self.device:
+            raise ValueError(f"workspace must be a uint8 tensor of >= {nbytes} bytes on {self.device}")
+        else:
+            ws = workspace
         run = lambda: ctx.forward_prompts(wav.data_ptr(), B, T, table.data_ptr(), P, out.data_ptr(), ws.data_ptr(),
                                           ws.numel(), torch.cuda.current_stream(self.device).cuda_stream)
         run()                                   # eager once: one-time launch-configuration queries happen outside
         torch.cuda.synchronize(self.device)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        # thread_local: only this thread's calls are checked during capture (a process-group watchdog thread may
+        # query its events meanwhile); the library issues all of its HIP calls on this thread
+        with torch.cuda.graph(g, capture_error_mode="thread_local"):
             run()
         g._athd_keep = (wav, table, out, ws)    # the graph's device pointers stay valid while it lives
         return g, out

@@ -284,6 +284,10 @@ bool dconv(Run& r, const EncW& e, void* x, int64_t nb, int64_t L, float* hbuf, u
             rc3 = dconv_conv3_launch((const uint16_t*)x, (const uint16_t*)e.dc.c3[dd].w, e.dc.c3[dd].Kp,
                                      e.dc.c3[dd].bias, hbuf, st_h, nb * L, L, C, dil, r.s);
         }
+        if (rc3 > 0 || (rc3 != 0 && wide96)) {   // (wide96: the padded hidden rows exist in the MFMA pass only)
+            r.check(rc3 > 0 ? rc3 : ATHD_EHIP, "dconv_conv3");
+            return fused;
+        }
         if (rc3 != 0) r.gemm(g, "dconv.conv3");
         // bf16 mode: GELU(GN(h)) written once as bf16, so both 1x1 passes read half the bytes and run on the bf16
         // MFMA GEMMs (gemm3 / gemm5) instead of converting fp32 A on load
@@ -297,6 +301,10 @@ bool dconv(Run& r, const EncW& e, void* x, int64_t nb, int64_t L, float* hbuf, u
                                          st_y, r.s) == 0;
             if (mom) {
                 // (statistics of the 1x1 already in st_y)
+            } else if (wide96) {
+                // the padded-row layout of the narrow MFMA passes (hidden rows of 16) has no other GN+GELU pass
+                r.check(ATHD_EHIP, "dconv gn_gelu_mom (C = 48 / 96)");
+                return false;
             } else if (hb) {
                 gn_gelu_bf16_launch(hbuf, hbuf_b, (int)nb, L * Hh, Hh, st_h, e.dc.g1w[dd], e.dc.g1b[dd], r.s);
             } else {
@@ -319,12 +327,16 @@ bool dconv(Run& r, const EncW& e, void* x, int64_t nb, int64_t L, float* hbuf, u
         if (hb) {
             KSite site("dconv.conv1x1.apply");
             const DcRewrite* rwd = dd == 1 && wide96 ? rw : nullptr;
+            // rc -1: rejected before any launch (fall back); rc > 0: a HIP error after the in-place kernel was issued,
+            // so x may already hold the residual update: report it, never run a second apply over it
             rc = dconv_apply_launch(hbuf_b, (const uint16_t*)e.dc.c1[dd].w, e.dc.c1[dd].Kp, e.dc.c1[dd].bias, st_y,
                                     e.dc.g2w[dd], e.dc.g2b[dd], e.dc.scale[dd], (uint16_t*)x, nb * L, L, C, r.s, rwd);
             if (rc == 0 && rwd) fused = true;
-            if (rc != 0 && rwd)      // (without the rewrite, then the caller's GEMM)
+            if (rc == -1 && rwd)      // (without the rewrite, then the caller's GEMM)
                 rc = dconv_apply_launch(hbuf_b, (const uint16_t*)e.dc.c1[dd].w, e.dc.c1[dd].Kp, e.dc.c1[dd].bias,
                                         st_y, e.dc.g2w[dd], e.dc.g2b[dd], e.dc.scale[dd], (uint16_t*)x, nb * L, L, C, r.s);
+            if (rc > 0) { r.check(rc, "dconv_apply"); return fused; }
+            if (rc == -1 && wide96) { r.check(ATHD_EHIP, "dconv_apply (C = 48 / 96, padded hidden rows)"); return fused; }
         }
         if (rc != 0) r.gemm(g2, "dconv.conv1x1.apply");
     }

@@ -110,38 +110,143 @@ def cpu_baseline(sd, table):
                       f"forward(B=8) = {res[8] * 1e3:.0f} ms; {threads} torch threads"}
 
 
-def sdr_vs_oracle(model, sd, table, wav0):
-    """SDR (dB) of this model's output for one segment x 4 prompts against the fp32 oracle forward (north_star:
-    'SDR delta reported'); min and mean over the prompts."""
+def sdr_vs_oracle(out, sd, table, wav, rows=(0, 63)):
+    """SDR (dB) of the TIMED output - rows `rows` of the last step's (B, 4, 2, T) result, written by the replayed
+    graph (N = 1) or the eager launches - against the fp32 oracle's forward_prompts on the same segments (north_star:
+    'SDR delta reported'); min and mean over rows x prompts."""
     from oracle.athtdemucs_ref import AudioTextHTDemucsRef
-    got = model.forward_prompts(wav0, STEMS).cpu().double()[0]
-    ref = AudioTextHTDemucsRef(sd).forward_prompts(wav0.cpu(), torch.as_tensor(table)).double()[0]
-    s = [float(10 * torch.log10((ref[p] ** 2).sum() / ((ref[p] - got[p]) ** 2).sum())) for p in range(4)]
-    return {"min": round(min(s), 2), "mean": round(sum(s) / 4, 2), "per_prompt": [round(x, 2) for x in s],
-            "what": "SDR of the bench dtype's output vs the fp32 oracle, segment 0 x 4 prompts (unclamped)"}
+    rows = [r for r in rows if r < wav.shape[0]]
+    got = out[rows].cpu().double()
+    ref = AudioTextHTDemucsRef(sd).forward_prompts(wav[rows].cpu(), torch.as_tensor(table)).double()
+    s = [[float(10 * torch.log10((ref[i, p] ** 2).sum() / ((ref[i, p] - got[i, p]) ** 2).sum())) for p in range(4)]
+         for i in range(len(rows))]
+    flat = [x for r in s for x in r]
+    return {"min": round(min(flat), 2), "mean": round(sum(flat) / len(flat), 2),
+            "per_row_prompt": {str(r): [round(x, 2) for x in s[i]] for i, r in enumerate(rows)},
+            "what": f"SDR of the timed bench output (rows {rows} of the last timed step, prompts {STEMS}) vs the fp32 "
+                    "oracle forward_prompts (unclamped)"}
 
 
-def f32_line(sd, table, wav, steps=3):
-    """Throughput of the f32 parity mode (fp32 MFMA everywhere) on the same batch, outside the headline."""
-    from athd.model import AudioTextHTDemucs
-    m = AudioTextHTDemucs(dtype="f32", text_table={s: table[i] for i, s in enumerate(STEMS)})
-    m.load_state_dict(sd)
-    m = m.to(wav.device).eval()
-    m.forward_prompts(wav, STEMS)
+def roofline_of(model, fwd, dominant, peak_mfma, ms_step, sites, steps=ROOF_STEPS, sections=True):
+    """Roofline of call site `dominant`: every launch of it bracketed with HIP events on its launch stream over
+    `steps` forwards (with a profile open the library runs the freq / time branches serially on one stream, so the
+    events time the kernel alone), priced against the larger of its two floors (algorithmic flops at the MFMA peak,
+    algorithmic bytes at the HBM peak); plus the per-section sums of one more fully evented forward."""
+    model.profile_start(dominant)
+    for _ in range(steps):
+        fwd()
+    torch.cuda.synchronize()
+    prof = model.profile_stop()
+    kp = next((r for r in prof if r["kernel"] == dominant), None)
+    if kp is None or kp["launches"] == 0:
+        raise RuntimeError(f"roofline kernel {dominant!r} was not launched")
+    per_launch_ms = kp["ms"] / kp["launches"]
+    kernel_sym = dominant.split("@", 1)[0]
+    t_mfma = kp["flops"] / (peak_mfma * 1e12) if kernel_sym.startswith(MFMA_KERNELS) else 0.0
+    t_hbm = kp["bytes"] / (HBM_PEAK_GBS * 1e9)
+    if t_mfma >= t_hbm:
+        peak, bound, unit = peak_mfma, "mfma", "TFLOP/s"
+        ach = kp["flops"] / (kp["ms"] * 1e-3) / 1e12
+    else:
+        peak, bound, unit = HBM_PEAK_GBS, "hbm", "GB/s"
+        ach = kp["bytes"] / (kp["ms"] * 1e-3) / 1e9
+    same = [r for r in sites if r["kernel"].split("@", 1)[0] == kernel_sym]
+    all_sites = None
+    if same:
+        n_all = sum(r["launches"] for r in same)
+        all_sites = {"kernel": kernel_sym, "launches_per_step": n_all, "sites": len(same),
+                     "avg_launch_us": round(sum(r["ms"] for r in same) / n_all * 1e3, 2),
+                     "timing": "warm-up step, every launch evented, branches serialised"}
+    roof = {"bound": bound, "achieved": round(ach, 2), "peak": peak, "unit": unit, "frac": round(ach / peak, 4),
+            "kernel": kernel_sym, "call_site": dominant, "kernel_all_sites": all_sites,
+            "launches_per_step": kp["launches"] / steps, "avg_launch_us": round(per_launch_ms * 1e3, 2),
+            "share_of_step": round(kp["ms"] / steps / ms_step, 4),
+            "algorithmic_per_launch": {"flops": kp["flops"] / kp["launches"], "bytes": kp["bytes"] / kp["launches"]},
+            "floors_ms_per_launch": {"mfma": round(t_mfma * 1e3 / kp["launches"], 4),
+                                     "hbm": round(t_hbm * 1e3 / kp["launches"], 4)},
+            "timing": f"HIP events on the launch stream around every launch of the call site, {steps} forwards after "
+                      "the timed region (branches serialised on one stream)"}
+    if sections:
+        model.profile_start("@section")
+        fwd()
+        torch.cuda.synchronize()
+        sec = {}
+        for r in model.profile_stop():
+            if not r["ms"]:
+                continue
+            tf = r["flops"] / (r["ms"] * 1e-3) / 1e12
+            sec[r["kernel"]] = {"ms": round(r["ms"], 3), "tflops": round(tf, 1), "frac_mfma": round(tf / peak_mfma, 4),
+                                "hbm_gbs": round(r["bytes"] / (r["ms"] * 1e-3) / 1e9, 1)}
+        roof["sections"] = sec
+        roof["sections_timing"] = ("one forward after the timed region, every kernel bracketed by HIP events "
+                                   "(branches serialised), summed per section; flops / bytes = the kernels' "
+                                   "algorithmic work")
+    return roof
+
+
+def site_profile(model, fwd):
+    """Every launch of one forward evented, keyed by call site (kernel@stage.site)."""
+    model.profile_start("@sites")
+    fwd()
+    torch.cuda.synchronize()
+    return model.profile_stop()
+
+
+def f32_line(m32, wav, steps=3):
+    """Throughput of the f32 parity mode (fp32 MFMA everywhere) on the same batch, outside the headline, with its
+    own roofline call site (the largest summed time of one evented forward) and per-section sums."""
+    fwd = lambda: m32.forward_prompts(wav, STEMS)          # noqa: E731
+    fwd()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(steps):
-        m.forward_prompts(wav, STEMS)
+        fwd()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     ms = el / steps * 1e3
     tf = 2e9 * (ENC_GMAC + 4 * DEC_GMAC) * wav.shape[0] / (ms * 1e-3) / 1e12
-    out = {"value": round(wav.shape[0] * steps / el, 3), "unit": "segments/s", "ms_per_step": round(ms, 3),
-           "steps": steps, "warmup": 1, "step_essential_tflops": round(tf, 2),
-           "frac_of_f32_mfma_peak": round(tf / F32_PEAK_TFLOPS, 4)}
-    del m
-    torch.cuda.empty_cache()
-    return out
+    sites = site_profile(m32, fwd)
+    dom = max(sites, key=lambda r: r["ms"])["kernel"]
+    return {"value": round(wav.shape[0] * steps / el, 3), "unit": "segments/s", "ms_per_step": round(ms, 3),
+            "steps": steps, "warmup": 1, "step_essential_tflops": round(tf, 2),
+            "frac_of_f32_mfma_peak": round(tf / F32_PEAK_TFLOPS, 4),
+            "roofline": roofline_of(m32, fwd, dom, F32_PEAK_TFLOPS, ms, sites, steps=1)}
+
+
+def sdr_delta_split(m_bf16, m_f32, n_tracks=2):
+    """north_star's 'SDR delta' under the benchmark.py protocol (its offline proxy: no MUSDB18, no trained weights):
+    a synthetic MUSDB18-HQ split (n_tracks tracks of 4 seeded tone+noise stems, mixture = their sum) through
+    athd.dist.separate_dataset (6 s windows, 1.5 s overlap, weighted overlap-add, per-stem SDR / SI-SDR as
+    benchmark.py:655-688) with the bf16 (bench) and the f32 (parity) model: the aggregate metric of each, their
+    difference, and the SDR of the bf16 estimates against the f32 ones."""
+    import tempfile
+    from athd.benchmark import aggregate_results
+    from athd.dist import separate_dataset
+    from athd.musdb import HQ_FILES, MusDBTracks, write_wav
+    from athd.synth import synthetic_mixture
+    with tempfile.TemporaryDirectory() as tmp:
+        lens = [44100 * 20 + 777, 44100 * 13 + 5][:n_tracks]
+        for t, L in enumerate(lens):
+            d = os.path.join(tmp, f"Synthetic {t} - Track")
+            os.makedirs(d)
+            parts = [0.25 * synthetic_mixture(L, seed=3000 + 10 * t + j) for j in range(4)]
+            for f, x in zip(HQ_FILES, [sum(parts)] + parts):
+                write_wav(os.path.join(d, f + ".wav"), x, 44100, "FLOAT")
+        tracks = MusDBTracks(tmp)
+        out = {}
+        for name, m in (("bf16", m_bf16), ("f32", m_f32)):
+            results, est = separate_dataset(m, tracks, STEMS, max_batch=16, keep_estimates=True, log=None)
+            out[name] = (aggregate_results(results), est)
+    agg = {k: {f: {s: round(x, 4) for s, x in v[0][f].items()} for f in v[0]} for k, v in out.items()}
+    delta = {f: {s: round(agg["bf16"][f][s] - agg["f32"][f][s], 4) for s in agg["f32"][f]} for f in agg["f32"]}
+    est_sdr = []
+    for name in out["f32"][1]:
+        a, b = out["f32"][1][name].double(), out["bf16"][1][name].double()
+        est_sdr.append(float(10 * torch.log10((a ** 2).sum() / ((a - b) ** 2).sum())))
+    return {"protocol": "benchmark.py:155-204 (6 s windows, 1.5 s overlap, weighted OLA) via athd.dist.separate_dataset",
+           "data": f"{len(lens)} synthetic MUSDB18-HQ-layout tracks ({[round(L / 44100, 1) for L in lens]} s), seeded "
+                   "random weights", "aggregate": agg, "delta_bf16_minus_f32": delta,
+           "sdr_bf16_estimates_vs_f32_db": [round(x, 2) for x in est_sdr]}
 
 
 def dataset_pass(model, wav, n, batch, world, rank, dev):
@@ -221,34 +326,54 @@ def main():
     sd = synthetic_state_dict(seed=0)
     table = synthetic_text_table(4, seed=7)
     B = args.batch
+    tt = {s: table[i] for i, s in enumerate(STEMS)}
     # the whole per-GPU batch in one decode chunk (B x 4 items): fewer, larger decoder launches (≈49 GB: athd_workspace_bytes, reported as workspace_gb)
-    model = AudioTextHTDemucs(dtype=args.dtype, text_table={s: table[i] for i, s in enumerate(STEMS)},
-                              decode_items=B * len(STEMS))
+    model = AudioTextHTDemucs(dtype=args.dtype, text_table=tt, decode_items=B * len(STEMS))
     model.load_state_dict(sd)
     model = model.to(dev).eval()
     # B distinct synthetic segments per rank, resident in HBM before timing (weak scaling: each rank owns its block)
     wav = torch.as_tensor(synthetic_batch(B, SEG, seed0=1000 + B * rank)).to(dev)
     N = B * world
     out = torch.empty((N, len(STEMS), 2, SEG), dtype=torch.float32, device=dev) if rank == 0 else None
-    pending = PendingSends(limit=2)          # at most two batches in flight per rank (bounded send buffers)
+    ws_bytes = model._ensure_ctx().workspace_bytes(B, SEG, len(STEMS))
 
-    # N = 1: one athd_forward_prompts captured into a HIP graph (both branch streams and their event joins), replayed
-    # per step: the same kernels on the same buffers, without the host launch gaps between them
-    graph = None
-    if world == 1 and not args.eager:
-        graph, _ = model.capture_prompts(wav, STEMS, out=out)
+    # Every step is one athd_forward_prompts captured into a HIP graph (both branch streams and their event joins)
+    # and replayed: the same kernels on the same buffers, without the host launch gaps between them.
+    #  * N = 1: the graph writes the bench output directly.
+    #  * N > 1: the same graph replay is the forward_fn of athd.dist.separate_segments, so the point-to-point RCCL
+    #    gather to rank 0 runs exactly as in the product runner.  Rank 0's graph writes its own rows of the gathered
+    #    output; every other rank alternates two graphs (one workspace, two send buffers) so a step never overwrites
+    #    a buffer whose send may still be in flight (PendingSends(limit=1): the previous step's send is waited on,
+    #    stream-ordered, before the next replay).
+    graphs, gbufs = [], []
+    pending = PendingSends(limit=2)          # eager N > 1: at most two batches in flight per rank
+    if not args.eager:
+        gws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+        if rank == 0:
+            gbufs = [out[0:B]]
+        else:
+            gbufs = [torch.empty((B, len(STEMS), 2, SEG), dtype=torch.float32, device=dev) for _ in range(2)]
+            pending = PendingSends(limit=1)
+        for buf in gbufs:
+            graphs.append(model.capture_prompts(wav, STEMS, out=buf, workspace=gws)[0])
     # further pipelines (N = 1, --pipelines > 1): own model context, batch, output, stream and graph each
     pipes = []
-    if world == 1 and graph is not None and args.pipelines > 1:
+    if world == 1 and graphs and args.pipelines > 1:
         for k in range(1, args.pipelines):
-            mk = AudioTextHTDemucs(dtype=args.dtype, text_table={s: table[i] for i, s in enumerate(STEMS)},
-                                   decode_items=B * len(STEMS))
+            mk = AudioTextHTDemucs(dtype=args.dtype, text_table=tt, decode_items=B * len(STEMS))
             mk.load_state_dict(sd)
             mk = mk.to(dev).eval()
             wk = torch.as_tensor(synthetic_batch(B, SEG, seed0=1000 + B * (world + k))).to(dev)
             gk, _ = mk.capture_prompts(wk, STEMS)
             pipes.append((torch.cuda.Stream(dev), gk, mk, wk))
     nstep = [0]
+    ngraph = [0]
+
+    def graph_fwd(w, o):
+        k = ngraph[0] % len(graphs)
+        ngraph[0] += 1
+        graphs[k].replay()
+        return gbufs[k]
 
     def step():
         if pipes:
@@ -257,13 +382,12 @@ def main():
             if k > 0:
                 with torch.cuda.stream(pipes[k - 1][0]):
                     return pipes[k - 1][1].replay()
-            return graph.replay()
-        if graph is not None:
-            return graph.replay()
+            return graphs[0].replay()
         if world == 1:
-            return model.forward_prompts(wav, STEMS, out=out)
+            return graphs[0].replay() if graphs else model.forward_prompts(wav, STEMS, out=out)
         # shard + point-to-point gather of the separated waveforms to rank 0, transfers left in flight
-        return separate_segments(model, wav, STEMS, max_batch=B, n_total=N, out=out, pending=pending)
+        return separate_segments(model, wav, STEMS, max_batch=B, n_total=N, out=out, pending=pending,
+                                 forward_fn=graph_fwd if graphs else None)
 
     def fwd_only():
         return model.forward_prompts(wav, STEMS)
@@ -272,7 +396,7 @@ def main():
     for i in range(args.warmup):
         if i == args.warmup - 1:
             model.profile_start("@sites")        # (events around eager launches: the graph's launches are baked)
-            fwd_only() if graph is not None else step()
+            fwd_only() if graphs else step()
         else:
             step()
     pending.wait()
@@ -315,85 +439,30 @@ def main():
     torch.cuda.synchronize()
     barrier()
     el = time.perf_counter() - t0
-    # roofline kernel: every launch of it bracketed with HIP events on its launch stream, over ROOF_STEPS further
-    # forwards outside the timed region (with a profile open the library runs the freq / time branches serially on
-    # one stream, so the events time the kernel alone rather than sharing the chip with the other branch)
-    model.profile_start(dominant)
-    for _ in range(ROOF_STEPS):
-        fwd_only()
-    torch.cuda.synchronize()
-    prof = model.profile_stop()
-    sections = None
-    if not args.no_extras:
-        model.profile_start("@section")
-        fwd_only()
-        torch.cuda.synchronize()
-        sections = model.profile_stop()
     if world > 1:
         t = torch.tensor([el], device=dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         el = float(t.item())
     ms = el / args.steps * 1e3
     value = B * world * args.steps / el
+    # the timed output, for the parity check below (rank 0's rows of the last step; fwd_only below reuses the
+    # model's own workspace and output, not the graph's)
+    timed_rows = out[[0, B - 1]].clone() if rank == 0 else None
     peak_mfma = BF16_PEAK_TFLOPS if args.dtype == "bf16" else F32_PEAK_TFLOPS
     flops_step = 2e9 * (ENC_GMAC + 4 * DEC_GMAC) * B
     step_tf = flops_step / (ms * 1e-3) / 1e12
-    kp = next((r for r in prof if r["kernel"] == dominant), None)
-    if kp is None or kp["launches"] == 0:
-        raise RuntimeError(f"roofline kernel {dominant!r} was not launched in the timed region")
-    per_launch_ms = kp["ms"] / kp["launches"]
-    kernel_sym = dominant.split("@", 1)[0]
-    # the call site's bound is the larger of its two floors: algorithmic flops at the MFMA peak, algorithmic bytes at
-    # the HBM peak (e.g. the decoder's K = 288 ConvT GEMM moves 6.2 GB for 1.2 TFLOP: HBM-bound)
-    t_mfma = kp["flops"] / (peak_mfma * 1e12) if kernel_sym.startswith(MFMA_KERNELS) else 0.0
-    t_hbm = kp["bytes"] / (HBM_PEAK_GBS * 1e9)
-    if t_mfma >= t_hbm:
-        peak = peak_mfma
-        ach = kp["flops"] / (kp["ms"] * 1e-3) / 1e12
-        bound, unit = "mfma", "TFLOP/s"
-    else:
-        peak, bound, unit = HBM_PEAK_GBS, "hbm", "GB/s"
-        ach = kp["bytes"] / (kp["ms"] * 1e-3) / 1e9
+    roofline = roofline_of(model, fwd_only, dominant, peak_mfma, ms, sites, sections=not args.no_extras)
+    kernel_sym = roofline["kernel"]
     traffic, traffic_src = pmc_traffic(kernel_sym, B, args.dtype)
-    # the same kernel over ALL its call sites (warm-up profile): what rocprofv3's per-symbol average reports
-    same = [r for r in sites if r["kernel"].split("@", 1)[0] == kernel_sym]
-    all_sites = None
-    if same:
-        n_all = sum(r["launches"] for r in same)
-        all_sites = {"kernel": kernel_sym, "launches_per_step": n_all, "sites": len(same),
-                     "avg_launch_us": round(sum(r["ms"] for r in same) / n_all * 1e3, 2),
-                     "timing": "warm-up step, every launch evented, branches serialised"}
-    roofline = {"bound": bound, "achieved": round(ach, 2), "peak": peak, "unit": unit, "frac": round(ach / peak, 4),
-                "traffic": traffic, "kernel": kernel_sym, "call_site": dominant,
-                "kernel_all_sites": all_sites,
-                "traffic_note": "PMC bytes per launch of the kernel symbol (all call sites; rocprofv3 cannot split "
-                                "them)" if all_sites and all_sites["sites"] > 1 else "PMC bytes per launch",
-                "launches_per_step": kp["launches"] / ROOF_STEPS,
-                "avg_launch_us": round(per_launch_ms * 1e3, 2),
-                "share_of_step": round(kp["ms"] / ROOF_STEPS / ms, 4),
-                "algorithmic_per_launch": {"flops": kp["flops"] / kp["launches"],
-                                           "bytes": kp["bytes"] / kp["launches"]},
-                "floors_ms_per_launch": {"mfma": round(t_mfma * 1e3 / kp["launches"], 4),
-                                         "hbm": round(t_hbm * 1e3 / kp["launches"], 4)},
-                "timing": f"HIP events on the launch stream around every launch of the call site, {ROOF_STEPS} "
-                          "forwards after the timed region (branches serialised on one stream)",
-                "step": {"achieved_tflops": round(step_tf, 2), "peak": peak_mfma, "frac": round(step_tf / peak_mfma, 4),
-                         "basis": "essential FLOPs per step (SURVEY.md §8(d): 256.5 GFLOP per segment x 4 stems) / "
-                                  "timed ms per step"}}
+    roofline["traffic"] = traffic
+    roofline["traffic_note"] = ("PMC bytes per launch of the kernel symbol (all call sites; rocprofv3 cannot split "
+                                "them)" if roofline["kernel_all_sites"] and roofline["kernel_all_sites"]["sites"] > 1
+                                else "PMC bytes per launch")
     if traffic_src:
         roofline["traffic_source"] = traffic_src
-    if sections:
-        sec = {}
-        for r in sections:
-            if not r["ms"]:
-                continue
-            tf = r["flops"] / (r["ms"] * 1e-3) / 1e12
-            sec[r["kernel"]] = {"ms": round(r["ms"], 3), "tflops": round(tf, 1), "frac_mfma": round(tf / peak_mfma, 4),
-                                "hbm_gbs": round(r["bytes"] / (r["ms"] * 1e-3) / 1e9, 1)}
-        roofline["sections"] = sec
-        roofline["sections_timing"] = ("one forward after the timed region, every kernel bracketed by HIP events "
-                                       "(branches serialised), summed per section; flops / bytes = the kernels' "
-                                       "algorithmic work")
+    roofline["step"] = {"achieved_tflops": round(step_tf, 2), "peak": peak_mfma, "frac": round(step_tf / peak_mfma, 4),
+                        "basis": "essential FLOPs per step (SURVEY.md §8(d): 256.5 GFLOP per segment x 4 stems) / "
+                                 "timed ms per step"}
     rec = {
         "metric": "6s-segments/sec (each separated into 4 stems; encode once, decode 4x)",
         "value": round(value, 3),
@@ -413,17 +482,28 @@ def main():
                                   if world > 1 else ""),
                    "global_batch": N, "seq_len": SEG, "prompts": 4, "parallelism": f"segment-sharded dp{world}",
                    "gather_timed": world > 1,
-                   "launch": "hipGraph replay of one athd_forward_prompts" if graph is not None else "eager",
+                   "launch": (f"hipGraph replay of one athd_forward_prompts per step ({len(graphs)} graph(s) per rank)"
+                              if graphs else "eager"),
                    "pipelines": len(pipes) + 1},
         "stems_per_s": round(4 * value, 3),
         "roofline": roofline,
         "step_essential_tflops": round(step_tf, 2),
-        "workspace_gb": round(model._ws.numel() / 1e9, 2) if model._ws is not None else None,
+        "workspace_gb": round(ws_bytes / 1e9, 2),
     }
     if rank == 0 and not args.no_extras:
-        rec["sdr_db_vs_oracle"] = sdr_vs_oracle(model, sd, table, wav[:1].contiguous())
+        full = torch.zeros((B, len(STEMS), 2, SEG), dtype=torch.float32)
+        full[[0, B - 1]] = timed_rows.cpu()
+        rec["sdr_db_vs_oracle"] = sdr_vs_oracle(full, sd, table, wav.cpu(), rows=(0, B - 1))
         if world == 1 and args.dtype == "bf16":
-            rec["f32"] = f32_line(sd, table, wav)
+            m32 = AudioTextHTDemucs(dtype="f32", text_table=tt)
+            m32.load_state_dict(sd)
+            m32 = m32.to(dev).eval()
+            rec["f32"] = f32_line(m32, wav)
+            model._ws = None                     # (the bench workspace is not needed for the short split below)
+            torch.cuda.empty_cache()
+            rec["sdr_delta_benchmark_protocol"] = sdr_delta_split(model, m32)
+            del m32
+            torch.cuda.empty_cache()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         rec["cpu_baseline"] = cpu_baseline(sd, table)
     if rank == 0:

@@ -205,6 +205,36 @@ def _worker(rank, world, port, q, split_dir=None, out_dir=None):
         assert peak <= 2, peak
         if rank == 0:
             assert out is res and torch.equal(out, ref14), "bench pattern"
+        # bench.py's graph-replayed N>1 pattern: one batch per rank and step; rank 0's forward writes its own rows of
+        # the gathered output in place (the graph is captured on out[0:B]); the other ranks alternate two send
+        # buffers with PendingSends(limit=1), so a step never rewrites a buffer whose send may be in flight
+        B = 3
+        lo, hi = shard_range(B * world, world, rank)
+        blk = torch.randn(B, 2, 200, generator=torch.Generator().manual_seed(100 + rank))
+        res = torch.full((B * world, 4, 2, 200), float("nan")) if rank == 0 else None
+        bufs = [res[0:B]] if rank == 0 else [torch.empty(B, 4, 2, 200) for _ in range(2)]
+        pend = PendingSends(limit=1 if rank else 2)
+        calls = [0]
+
+        def ping_pong(wav, o, scale):
+            k = calls[0] % len(bufs)
+            calls[0] += 1
+            bufs[k].copy_(torch.stack([_fake_stem(wav * scale, si) for si in range(4)], dim=1))
+            return bufs[k]
+
+        for step in range(4):
+            out = separate_segments(None, blk, ["a", "b", "c", "d"], forward_fn=lambda w, o: ping_pong(w, o, step + 1),
+                                    max_batch=B, n_total=B * world, out=res, pending=pend)
+            assert len(pend.works) <= (1 if rank else 2)
+        pend.wait()
+        if rank == 0:
+            want = torch.cat([torch.randn(B, 2, 200, generator=torch.Generator().manual_seed(100 + r))
+                              for r in range(world)])
+            want = torch.stack([_fake_stem(want * 4, si) for si in range(4)], dim=1)
+            assert out is res and torch.equal(res, want), "graph ping-pong pattern"
+            assert calls[0] == 4
+        else:
+            assert calls[0] == 4
         if split_dir is not None:
             _dataset_checks(rank, world, split_dir, out_dir)
         # --- one track, windows sharded over ranks
