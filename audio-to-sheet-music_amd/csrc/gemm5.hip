@@ -29,6 +29,7 @@
 #include "gemm_epi.h"
 
 #include <climits>
+#include <type_traits>
 
 namespace athd {
 
@@ -65,7 +66,13 @@ __device__ __attribute__((aligned(64))) uint4 g_zero_page5[4];
 
 // PROBE (tools/kbench ablations only; the product instantiates 0): 1 = no LDS-DMA staging in the K-loop, 2 = no
 // fragment reads in the K-loop, 3 = no MFMAs, 4 = no section barriers in the K-loop (results are garbage).
-template <unsigned F, int PROBE = 0>
+// LIN: dense single-tap rows (linear / 1x1 layers: A row of output row m at m * a_ld, K == Kp == C_in).  Each lane's A
+// source is then a 32-bit byte offset fixed per tile, and a K-tile's address is a wave-uniform base + that offset
+// (global_load_lds with an SGPR base: no per-issue VALU), instead of the implicit-GEMM row / tap / bounds arithmetic
+// (~170 VALU instructions per K-tile and wave in the general form, against 64 MFMAs).  In both forms the
+// steady-state K-steps (u + 2 < nk) wait with a constant vmcnt(8) (every window of 4 consecutive load sections issues
+// 8 pieces) instead of the counted-history branch chain; the last two K-steps keep the history.
+template <unsigned F, int PROBE = 0, bool LIN = false>
 __global__ __launch_bounds__(512) void gemm5_kernel(const GemmDesc d) {
     constexpr bool PERSIST = (F & (F_RES | F_STATS)) == 0;
     constexpr int TM = 8, TN = 4;
@@ -96,6 +103,7 @@ __global__ __launch_bounds__(512) void gemm5_kernel(const GemmDesc d) {
     uint32_t a_base[2][2];
     int a_h0[2][2];
     uint32_t b_off[2];
+    const uint32_t a_ld2 = (uint32_t)d.a_ld * 2u;
     auto setup = [&](int t) {
         const int id = xcd_remap5(t, ntiles);
         m0 = (int64_t)(id / ntn) * 256;
@@ -108,6 +116,11 @@ __global__ __launch_bounds__(512) void gemm5_kernel(const GemmDesc d) {
                 const int r = (sr >> 6) * 128 + 64 * h + (sr & 63);
                 const uint32_t m = (uint32_t)(m0 + r);
                 const bool ok = m < (uint32_t)M;
+                if constexpr (LIN) {      // rows past M re-read row M - 1 (their outputs are never stored)
+                    a_base[h][q] = (ok ? m : (uint32_t)M - 1u) * a_ld2 + 16u * (uint32_t)chunk;
+                    if (h == 0) b_off[q] = (uint32_t)(((int64_t)(n0 + (sr >> 5) * 64 + (sr & 31)) * d.Kp + 8 * chunk) * 2);
+                    continue;
+                }
                 const uint32_t mm = ok ? m : 0u;
                 const uint32_t t2 = fdiv(mm, d.fd_w);
                 const uint32_t w = mm - t2 * (uint32_t)d.W;
@@ -124,6 +137,14 @@ __global__ __launch_bounds__(512) void gemm5_kernel(const GemmDesc d) {
     auto issueA = [&](int kt, int h) {
         if (PROBE == 1 && kt > 1) return;
         char* dst = smem + ((kt & 1) * 4 + h) * G5_SLOT;
+        if constexpr (LIN) {
+            const char* base = (const char*)d.A + (int64_t)kt * 128;      // wave-uniform
+#pragma unroll
+            for (int q = 0; q < 2; ++q)
+                __builtin_amdgcn_global_load_lds((gbl_void*)(base + a_base[h][q]), (lds_void*)(dst + (wave + NW * q) * 1024),
+                                                 16, 0, 0);
+            return;
+        }
         const int k = kt * 64 + 8 * chunk;
         const bool kok = k < d.K;
         const int tap = k / d.C_in, ci = k - tap * d.C_in;
@@ -247,11 +268,17 @@ __global__ __launch_bounds__(512) void gemm5_kernel(const GemmDesc d) {
 #pragma unroll
             for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
         if (wr == 1) section_barrier();           // the stagger: G1 runs one section behind G0
-        for (int u = 0; u < nk; ++u) {
+        // one K-tile u; STEADY (u + 2 < nk): n1 = n2 = true and the load waits are the constant vmcnt(8)
+        auto kstep = [&](int u, auto steady) {
+            constexpr bool ST = decltype(steady)::value;
             const int buf = u & 1;
-            const bool n1 = u + 1 < nk, n2 = u + 2 < nk;
+            const bool n1 = ST || u + 1 < nk, n2 = ST || u + 2 < nk;
+            auto lw = [&]() {
+                if constexpr (ST) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+                else load_wait();
+            };
             // ---- phase 0: (A0, B0)
-            load_wait();
+            lw();
             if (wr == 0 && n1) issueA(u + 1, 1);
             push(wr == 0 && n1 ? 2 : 0);
             readB(buf, 0, bf0);
@@ -260,7 +287,7 @@ __global__ __launch_bounds__(512) void gemm5_kernel(const GemmDesc d) {
             quad(0, 0, af, bf0);
             sbar();
             // ---- phase 1: (A0, B1)
-            load_wait();
+            lw();
             if (wr == 1 && n2) {
                 issueA(u + 2, 0);
                 issueB(u + 2, 0);
@@ -271,7 +298,7 @@ __global__ __launch_bounds__(512) void gemm5_kernel(const GemmDesc d) {
             quad(0, 1, af, bf1);
             sbar();
             // ---- phase 2: (A1, B1)
-            load_wait();
+            lw();
             if (n2) {
                 if (wr == 0) {
                     issueA(u + 2, 0);
@@ -286,7 +313,7 @@ __global__ __launch_bounds__(512) void gemm5_kernel(const GemmDesc d) {
             quad(1, 1, af, bf1);
             sbar();
             // ---- phase 3: (A1, B0)
-            load_wait();
+            lw();
             if (n2) {
                 if (wr == 0) issueB(u + 2, 1);
                 else issueA(u + 2, 1);
@@ -295,7 +322,12 @@ __global__ __launch_bounds__(512) void gemm5_kernel(const GemmDesc d) {
             sbar();
             quad(1, 0, af, bf0);
             sbar();
+        };
+        int u = 0;
+        if constexpr (PROBE == 0) {
+            for (; u + 2 < nk; ++u) kstep(u, std::true_type{});
         }
+        for (; u < nk; ++u) kstep(u, std::false_type{});
         if (wr == 0) section_barrier();           // G0 waits out G1's last MFMA section: equal barrier counts
         // every slot's last fragment reads have retired (lgkmcnt(0) before the barriers above)
         const int next = tile + (int)gridDim.x;
@@ -349,7 +381,7 @@ bool gemm5_supported(const GemmDesc& d) {
            d.col_split % 4 == 0 && (d.act != ACT_GLU || d.N % 32 == 0);
 }
 
-template <unsigned F, int PROBE = 0>
+template <unsigned F, int PROBE = 0, bool LIN = false>
 static void launch5f(const GemmDesc& d, hipStream_t s) {
     const int64_t M = (int64_t)d.nb * d.H_out * d.W;
     const int64_t tiles = ((M + 255) / 256) * ((d.N + 255) / 256);
@@ -360,7 +392,7 @@ static void launch5f(const GemmDesc& d, hipStream_t s) {
             int per_cu = 0, cus = 0, dev = 0;
             (void)hipGetDevice(&dev);
             (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-            (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, gemm5_kernel<F, PROBE>, 512, 0);
+            (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, gemm5_kernel<F, PROBE, LIN>, 512, 0);
             resident = per_cu > 0 && cus > 0 ? per_cu * cus / 8 * 8 : -1;
         }
         if (resident >= 8 && resident < tiles) grid = resident;
@@ -369,15 +401,27 @@ static void launch5f(const GemmDesc& d, hipStream_t s) {
     if (ks.on()) {
         double fl, by;
         gemm_work(d, 1, fl, by);
-        ks.begin(klabel("gemm5_kernel<%u,%d>", F, PROBE), fl, by);
+        ks.begin(klabel("gemm5_kernel<%u,%d,%s>", F, PROBE, LIN ? "true" : "false"), fl, by);
     }
-    hipLaunchKernelGGL((gemm5_kernel<F, PROBE>), dim3((unsigned)grid), dim3(512), 0, s, with_fastdiv(d));
+    hipLaunchKernelGGL((gemm5_kernel<F, PROBE, LIN>), dim3((unsigned)grid), dim3(512), 0, s, with_fastdiv(d));
 }
 
+// dense single-tap rows: the LIN fast path of gemm5_kernel applies
+static bool gemm5_lin(const GemmDesc& d) {
+    return d.ntaps == 1 && d.in_stride == 1 && d.in_off == 0 && d.H_out == d.H_in && d.a_hs < 0 &&
+           (d.a_bs < 0 || d.a_bs == (int64_t)d.H_in * d.W * d.a_ld) && d.C_in == d.K && d.K == d.Kp &&
+           d.a_cs == 1 && !d.k_blk && (int64_t)d.nb * d.H_in * d.W * d.a_ld * 2 < (1LL << 32);
+}
+
+#ifndef ATHD_G5_LIN
+#define ATHD_G5_LIN 1       // (0: every launch takes the general implicit-GEMM addressing; kbench A/B builds)
+#endif
+
 int gemm5_launch(const GemmDesc& d, hipStream_t s) {
+    const bool lin = ATHD_G5_LIN && gemm5_lin(d);
     switch (epi_flags(d)) {
 #define ATHD_CASE(FL) \
-    case (FL): launch5f<(FL)>(d, s); break;
+    case (FL): lin ? launch5f<(FL), 0, true>(d, s) : launch5f<(FL)>(d, s); break;
         ATHD_EPI_LIST(ATHD_CASE)
 #undef ATHD_CASE
         default: launch5f<F_ALL>(d, s); break;
