@@ -141,12 +141,14 @@ def test_test_inference_reference_signature(tmp_path, state_dict, text_table, or
     from athd.musdb import HQ_FILES, read_wav, write_wav
     from athd.synth import synthetic_mixture
     from athd.weights import STEMS
-    L = 2 * 260190 + 30000                               # 3 windows: 2 full + a 30000-sample tail
+    L = 520380 + 10000                                   # 3 windows: 2 full + a 10000-sample tail
     data = tmp_path / "quick_test"
     d = data / "Art's Band - A Song"
     d.mkdir(parents=True)
-    parts = [0.5 * synthetic_mixture(L, seed=500 + j) for j in range(4)]
-    for f, x in zip(HQ_FILES, [sum(parts)] + parts):
+    # the mixture of test_separate_track_matches_oracle_loop (its spectrum keeps away from the mask's singular bins,
+    # test_gpu_parity._phase_cond); the true stems are independent signals (only the SDR arithmetic reads them)
+    parts = [synthetic_mixture(L, seed=77)] + [0.5 * synthetic_mixture(L, seed=500 + j) for j in range(4)]
+    for f, x in zip(HQ_FILES, parts):
         write_wav(d / f"{f}.wav", x, 44100, "FLOAT")
     sd = {k: torch.as_tensor(np.asarray(v)) for k, v in state_dict.items()}
     ckpt = tmp_path / "best_model.pt"
