@@ -425,7 +425,18 @@ namespace {
 constexpr int F0_NT = 18;                 // m-tiles per row
 constexpr int F0_TP = 16 * F0_NT;         // positions per row (T <= 288)
 constexpr int F0_C = 48, F0_H = 6;
-constexpr int F0_XIN_P = 40, F0_XS_P = 56, F0_HS_P = 40;
+// LDS images (bf16 elements).  xs (the residual stream x, 2 halo rows each side): 160-B rows with the 16-B chunk
+// XOR-swizzled by (row >> 2) & 1; xin (conv input) and hs (DConv hidden) share one buffer of 64-B rows, chunk XOR
+// (row >> 1) & 3.  With these every fragment read (16 rows x 16 B per lane group; the conv3 taps shift rows by 0, +-1, +-2) and
+// every 8-B residual / hidden write is bank-conflict-free (round 3's padded pitches 56 / 40 cost 1.9 extra LDS cycles
+// per LDS instruction, SQ_LDS_BANK_CONFLICT).
+// (pitch 128 B with chunk XOR row & 7 is conflict-free too, but that layout made the compiler allocate 131 VGPRs:
+// two 6-wave workgroups per CU need <= 128)
+constexpr int F0_XIN_P = 32, F0_XS_P = 80, F0_HS_P = 32;
+ATHD_DEV int xs_off(int row, int col) { return row * F0_XS_P + (((col >> 3) ^ ((row >> 2) & 1)) << 3) + (col & 7); }
+ATHD_DEV int hs_off(int row, int col) { return row * F0_HS_P + (((col >> 3) ^ ((row >> 1) & 3)) << 3) + (col & 7); }
+// (both swizzles repeat every 8 rows, so an m-tile's image is the lane's offset at row l15 (+ halo, + tap shift) plus
+// mt * 16 rows: the per-tile part stays an immediate offset)
 
 ATHD_DEV float dpp_row_sum(float v) {     // every lane: the sum over its row of 16 lanes
     v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));   // quad_perm 1032
@@ -531,7 +542,7 @@ __global__ __launch_bounds__(FR_NT, 4) void fenc_row0_kernel(const FencRowDesc d
         uint4 v = make_uint4(pack2bf((a.x - sub) * rdv, (a.y - sub) * rdv), pack2bf((a.z - sub) * rdv, (a.w - sub) * rdv),
                              pack2bf((e.x - sub) * rdv, (e.y - sub) * rdv), pack2bf((e.z - sub) * rdv, (e.w - sub) * rdv));
         if (!ok) v = make_uint4(0u, 0u, 0u, 0u);
-        *reinterpret_cast<uint4*>(&xin[m * F0_XIN_P + q * 8]) = v;
+        *reinterpret_cast<uint4*>(&xin[hs_off(m, q * 8)]) = v;
     }
     __syncthreads();
 
@@ -541,7 +552,7 @@ __global__ __launch_bounds__(FR_NT, 4) void fenc_row0_kernel(const FencRowDesc d
     for (int i = 0; i < MTW; ++i) {
         const int mt = mg + 2 * i;
         if (i % 3 == 0) FR_SCHED();
-        xr[i] = mfma(wf, ldfrag(&xin[(mt * 16 + l15) * F0_XIN_P + 8 * l4]), f32x4_t{0.f, 0.f, 0.f, 0.f});
+        xr[i] = mfma(wf, ldfrag(&xin[hs_off(l15, 8 * l4) + mt * 16 * F0_XIN_P]), f32x4_t{0.f, 0.f, 0.f, 0.f});
     }
     {
         const float bcv[4] = {bc.x, bc.y, bc.z, bc.w};
@@ -556,13 +567,13 @@ __global__ __launch_bounds__(FR_NT, 4) void fenc_row0_kernel(const FencRowDesc d
 #pragma unroll
                 for (int q = 0; q < 4; ++q) xr[i][q] = m < T ? xr[i][q] : 0.f;
             }
-            st4bf(&xs[(FR_HALO + m) * F0_XS_P + cb], xr[i][0], xr[i][1], xr[i][2], xr[i][3]);
+            st4bf(&xs[xs_off(FR_HALO + l15, cb) + mt * 16 * F0_XS_P], xr[i][0], xr[i][1], xr[i][2], xr[i][3]);
         }
     }
     __syncthreads();
     // the conv input is dead: zero the hidden tile's K padding columns 16..31
     for (int i = tid; i < F0_TP * 2; i += FR_NT)
-        *reinterpret_cast<uint4*>(&hs[(i >> 1) * F0_HS_P + 16 + 8 * (i & 1)]) = make_uint4(0u, 0u, 0u, 0u);
+        *reinterpret_cast<uint4*>(&hs[hs_off(i >> 1, 16 + 8 * (i & 1))]) = make_uint4(0u, 0u, 0u, 0u);
 
     // ---- DConv: x += LayerScale(GLU(GN(1x1(GELU(GN(conv3(x)))))))
 #pragma unroll 1
@@ -583,7 +594,7 @@ __global__ __launch_bounds__(FR_NT, 4) void fenc_row0_kernel(const FencRowDesc d
 #pragma unroll
             for (int i = 0; i < 3; ++i) {
                 const int mt = wave + FR_NW * i;
-                bf16x8_t xf = ldfrag(&xs[(FR_HALO + mt * 16 + l15 + (kok ? (tap - 1) * dil : 0)) * F0_XS_P + (kok ? c0 : 0)]);
+                bf16x8_t xf = ldfrag(&xs[xs_off(FR_HALO + l15 + (kok ? (tap - 1) * dil : 0), kok ? c0 : 0) + mt * 16 * F0_XS_P]);
                 if (!kok) xf = bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
                 ha[i] = mfma(w3f, xf, ha[i]);
             }
@@ -628,7 +639,7 @@ __global__ __launch_bounds__(FR_NT, 4) void fenc_row0_kernel(const FencRowDesc d
                 const float v = gelu_fast((ha[i][q] + hb[q] - hm) * hr * g1w[q] + g1b[q]);
                 g[q] = 4 * l4 + q < H ? v : 0.f;
             }
-            *reinterpret_cast<uint2*>(&hs[(mt * 16 + l15) * F0_HS_P + 4 * l4]) =
+            *reinterpret_cast<uint2*>(&hs[hs_off(l15, 4 * l4) + mt * 16 * F0_HS_P]) =
                 make_uint2(pack2bf(g[0], g[1]), pack2bf(g[2], g[3]));
         }
         // (the hidden rows of this wave's positions were written by this wave: LDS order within a wave suffices)
@@ -636,7 +647,7 @@ __global__ __launch_bounds__(FR_NT, 4) void fenc_row0_kernel(const FencRowDesc d
         {
             const int mt = wave + FR_NW * l4;
             if (l4 < 3 && mt * 16 + l15 < T) {
-                const uint4 hq = *reinterpret_cast<const uint4*>(&hs[(mt * 16 + l15) * F0_HS_P]);
+                const uint4 hq = *reinterpret_cast<const uint4*>(&hs[hs_off(l15, 0) + mt * 16 * F0_HS_P]);
                 const float x[6] = {__uint_as_float(hq.x << 16), __uint_as_float(hq.x & 0xFFFF0000u),
                                     __uint_as_float(hq.y << 16), __uint_as_float(hq.y & 0xFFFF0000u),
                                     __uint_as_float(hq.z << 16), __uint_as_float(hq.z & 0xFFFF0000u)};
@@ -686,7 +697,7 @@ __global__ __launch_bounds__(FR_NT, 4) void fenc_row0_kernel(const FencRowDesc d
             const int mt = mg + 2 * i;
             const int m = mt * 16 + l15c;
             FR_SCHED();
-            const bf16x8_t hf = ldfrag(&hs[m * F0_HS_P + 8 * l4]);
+            const bf16x8_t hf = ldfrag(&hs[hs_off(l15c, 8 * l4) + mt * 16 * F0_HS_P]);
             const f32x4_t z = f32x4_t{0.f, 0.f, 0.f, 0.f};
             const f32x4_t ya = mfma(wa, hf, z), yg = mfma(wg, hf, z);
 #pragma unroll
@@ -699,7 +710,7 @@ __global__ __launch_bounds__(FR_NT, 4) void fenc_row0_kernel(const FencRowDesc d
 #pragma unroll
                 for (int q = 0; q < 4; ++q) xr[i][q] = m < T ? xr[i][q] : 0.f;
             }
-            st4bf(&xs[(FR_HALO + m) * F0_XS_P + cb], xr[i][0], xr[i][1], xr[i][2], xr[i][3]);
+            st4bf(&xs[xs_off(FR_HALO + l15c, cb) + mt * 16 * F0_XS_P], xr[i][0], xr[i][1], xr[i][2], xr[i][3]);
         }
         __syncthreads();
     }
@@ -731,7 +742,7 @@ __global__ __launch_bounds__(FR_NT, 4) void fenc_row0_kernel(const FencRowDesc d
 #pragma unroll
             for (int ks = 0; ks < 2; ++ks) {
                 const int k0 = ks * 32 + 8 * l4;
-                bf16x8_t xf = ldfrag(&xs[(FR_HALO + m) * F0_XS_P + (k0 < C ? k0 : 0)]);
+                bf16x8_t xf = ldfrag(&xs[xs_off(FR_HALO + l15, k0 < C ? k0 : 0) + (m - l15) * F0_XS_P]);
                 if (k0 >= C) xf = bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
                 za = mfma(wa[ks], xf, za);
                 zg = mfma(wg[ks], xf, zg);
