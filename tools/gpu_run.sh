@@ -8,7 +8,7 @@
 #   full                    bench.py with the CPU baseline (the driver's default line)
 #   sites:TAG               bench + per-call-site kernel times           -> gpurun_out/k_TAG.json / k_TAG_sites.json
 #   ab:A.so:B.so[:ROUNDS]   whole-model A/B of two library builds, alternating runs (tools/gpu_ab_lib.sh)
-#   kbench:MODE             tools/kbench.py MODE (kernel micro-benchmarks; tools/libkbench.so)
+#   kbench:MODE[:LIB]       tools/kbench.py MODE (kernel micro-benchmarks; tools/libkbench.so or tools/LIB)
 #   prof:TAG                rocprofv3 kernel trace of a short bench, both streams and serialised (ATHD_SERIAL=1)
 #   sq:TAG                  two SQ counter passes + summary                -> gpurun_out/pmc_sq_TAG.txt
 O=gpurun_out
@@ -37,7 +37,7 @@ for step in "$@"; do
     ab)
       timeout -k 10 900 bash tools/gpu_ab_lib.sh "$a1" "$a2" "${a3:-2}" || exit 1 ;;
     kbench)
-      timeout -k 10 600 python tools/kbench.py $a1 > $O/kbench_$n.log 2>&1; rc=$?
+      KB_LIB=${a2:-libkbench.so} timeout -k 10 600 python tools/kbench.py $a1 > $O/kbench_$n.log 2>&1; rc=$?
       grep -v amdgpu.ids $O/kbench_$n.log | cut -c1-300; [ $rc -ne 0 ] && exit $rc ;;
     prof)
       timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$a1 -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-extras > $O/prof_$a1.log 2>&1 || { tail -20 $O/prof_$a1.log; exit 1; }

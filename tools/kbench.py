@@ -168,6 +168,35 @@ def attn_case(B, N, variants=(1, 0, 2, 3)):
     print(f"ATTN B={B} N={N}: " + " | ".join(res) + f" | torch sdpa {ust:8.1f}us {flops / ust / 1e6:7.1f}TF", flush=True)
 
 
+def attn_acc(B, N, scales=(1.0, 4.0, 6.0), ramp=(0.0, 8.0)):
+    """Accuracy of the product attention kernel (v0) against torch SDPA in fp32 on bf16 inputs whose logit range forces
+    the rescale path: Q and K scaled (logits x scale^2) and a per-key ramp added along the key axis through an extra
+    channel pair (later keys score higher, so later tiles exceed the first tile's max)."""
+    st = torch.cuda.current_stream().cuda_stream
+    for sc in scales:
+        for rp in ramp:
+            g = torch.Generator(device="cuda").manual_seed(int(sc * 10 + rp))
+            qkv = torch.randn(B, N, 1536, device="cuda", generator=g)
+            qkv[..., :1024] *= sc
+            if rp:
+                # head dim 63 of q = 1, of k = ramp * key / N  (adds ramp * key / N to every logit of the key)
+                qkv.view(B, N, 3, 8, 64)[:, :, 0, :, 63] = 1.0
+                qkv.view(B, N, 3, 8, 64)[:, :, 1, :, 63] = (rp * 8.0 * torch.arange(N, device="cuda") / N)[None, :, None]
+            qkv = qkv.to(torch.bfloat16)
+            qkvp = qkv.clone()
+            qkvp[..., :512] = (qkv[..., :512].float() * (0.125 * 1.4426950408889634)).to(torch.bfloat16)
+            q, k, v = qkv.float().view(B, N, 3, 8, 64).permute(2, 0, 3, 1, 4)
+            ref = torch.nn.functional.scaled_dot_product_attention(q, k, v)
+            out = torch.zeros(B, N, 512, device="cuda", dtype=torch.bfloat16)
+            lib.kb_attn(0, 1, vp(qkvp.data_ptr()), B, N, vp(out.data_ptr()), vp(st))
+            torch.cuda.synchronize()
+            o = out.view(B, N, 8, 64).permute(0, 2, 1, 3).float()
+            err = (o - ref).abs().max().item()
+            sdr = 10 * torch.log10((ref ** 2).sum() / ((o - ref) ** 2).sum()).item()
+            print(f"ATTNACC B={B} N={N} scale={sc} ramp={rp}: maxerr={err:.2e} sdr={sdr:.2f} dB finite={bool(torch.isfinite(o).all())}",
+                  flush=True)
+
+
 def tr_probe():
     out = torch.zeros(64, 4, dtype=torch.int16, device="cuda")
     lib.kb_tr(vp(out.data_ptr()))
@@ -313,6 +342,10 @@ if __name__ == "__main__":
             gemm_case(M, 512, 512)
             gemm_case(4096, 4096, 4096)
             gemm_case(256 * 32 * 259, 768, 192)
+        sys.exit(0)
+    if "attnacc" in sys.argv[1:]:
+        attn_acc(8, 2072)
+        attn_acc(8, 1034)
         sys.exit(0)
     if "g4" in sys.argv[1:]:
         gemm_case(M, 1536, 512)
