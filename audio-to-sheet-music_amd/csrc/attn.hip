@@ -257,12 +257,6 @@ typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
 
 // defer-max threshold of the bf16 kernel's online softmax (log2 units): P <= 2^8 before the final 1/l
 constexpr float ATTN_RESCALE = 8.0f;
-// attn32_kernel: a lane's 32 probabilities of a tile summing past this (2^16) send the wave through the rescale path
-// (kbench builds override it: 0.5 forces the rescale path on every tile, for the threshold-sweep check)
-#ifndef ATHD_ATTN_SUM_TRIGGER
-#define ATHD_ATTN_SUM_TRIGGER 65536.0f
-#endif
-constexpr float ATTN_SUM_TRIGGER = ATHD_ATTN_SUM_TRIGGER;
 
 #ifdef ATHD_KBENCH      // round-1 16x16x32 kernel: tools/kbench A/B builds only
 __global__ __launch_bounds__(256, 3) void attn_bf16_kernel(const AttnDesc d) {
@@ -467,8 +461,8 @@ __global__ __launch_bounds__(256, 3) void attn_bf16_kernel(const AttnDesc d) {
 // Per wave 32 queries, per tile 64 keys.  S^T = K Q^T as two 32x32 blocks (keys x queries): lane l holds query
 // r = l & 31 and keys (reg & 3) + 8 (reg >> 2) + 4 (l >> 5) of each block, so the online softmax is in-lane plus one
 // exchange between the two 32-lane halves.  The accumulators start at -m (the running max) instead of 0, so the MFMA
-// itself subtracts the max: p = exp2(S) is one v_exp_f32 per score.  Only the first tile takes a max; later tiles form
-// P against the running max and move it only when a lane's tile sum passes ATTN_SUM_TRIGGER (the rescale path).
+// itself subtracts the max: p = exp2(S) is one v_exp_f32 per score.  The max moves only when a tile's scores exceed it
+// by more than ATTN_RESCALE (defer-max; the rescale runs before any of the tile's P is formed).
 //
 // O^T += V^T P^T: for PV k-step kk (16 keys of key block kk >> 1) lane (r, h) feeds its own registers
 // 8 (kk & 1) .. +7 as the B operand, i.e. keys 4h + {0..3} and 4h + 8 + {0..3} of the 16 - the k order inside the step
@@ -647,63 +641,42 @@ __global__ __launch_bounds__(256, MINW) void attn32_kernel(const AttnDesc d) {
             ATHD_A32_QK(-mrun);
             A32_PRIO(0);
             // ---- online softmax (log2 units) ----
-            // The first tile sets the running max from its scores.  Later tiles take no max at all: p = 2^(s - m) is
-            // formed against the current running max and the row sums double as the check - a lane whose 32 p sum past
-            // ATTN_SUM_TRIGGER (any p > 2^16, or an overflow to inf) sends the wave through the rescale path, which
-            // takes the tile max, moves m, rescales O and l and forms P again.  Below the trigger every p <= 2^16: far
-            // inside f32 / bf16 range, and the result is the same softmax (the max is only a range shift).  This drops
-            // the per-tile max reduction (16 v_max3 + a lane exchange per tile and wave) and its dependency between
-            // the QK^T MFMAs and the exponentials.
-            auto tile_max = [&]() {
-                float mxk[NKB];
+            float mxk[NKB];
 #pragma unroll
-                for (int kb = 0; kb < NKB; ++kb) {                 // independent chains, one per key block
-                    float m = vmax3(sc[kb][0], sc[kb][1], sc[kb][2]);
+            for (int kb = 0; kb < NKB; ++kb) {                     // independent chains, one per key block
+                float m = vmax3(sc[kb][0], sc[kb][1], sc[kb][2]);
 #pragma unroll
-                    for (int i = 3; i < 15; i += 2) m = vmax3(m, sc[kb][i], sc[kb][i + 1]);
-                    mxk[kb] = vmax3(m, sc[kb][15], sc[kb][15]);
+                for (int i = 3; i < 15; i += 2) m = vmax3(m, sc[kb][i], sc[kb][i + 1]);
+                mxk[kb] = vmax3(m, sc[kb][15], sc[kb][15]);
+            }
+            float mx = mxk[0];
+#pragma unroll
+            for (int kb = 1; kb < NKB; ++kb) mx = vmax3(mx, mxk[kb], mxk[kb]);
+            mx = half_swap_max(mx);
+            // first tile: the max is set; later tiles: it moves only past ATTN_RESCALE.  A move rescales O and l
+            // and recomputes the tile's scores against the new max (S is never modified in place, which keeps the
+            // accumulators in place across the branch)
+            const bool jump = t == 0 || mx > ATTN_RESCALE;
+            if (__any(jump)) {
+                const float dm = jump ? mx : 0.f;
+                const float alpha = t == 0 ? 0.f : __builtin_amdgcn_exp2f(-dm);
+                mrun += dm;
+                lrun *= alpha;
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    o0[i] *= alpha;
+                    o1[i] *= alpha;
                 }
-                float mx = mxk[0];
-#pragma unroll
-                for (int kb = 1; kb < NKB; ++kb) mx = vmax3(mx, mxk[kb], mxk[kb]);
-                return half_swap_max(mx);
-            };
-            auto exp_sum = [&](float (&ls)[NKB]) {
-#pragma unroll
-                for (int kb = 0; kb < NKB; ++kb) {
-                    ls[kb] = 0.f;
-#pragma unroll
-                    for (int i = 0; i < 16; ++i) {
-                        sc[kb][i] = __builtin_amdgcn_exp2f(sc[kb][i]);
-                        ls[kb] += sc[kb][i];
-                    }
-                }
-            };
-            float ls[NKB];
-            if (t == 0) {                                          // (wave-uniform)
-                const float mx = tile_max();
-                mrun += mx;                                        // O and l are still 0: nothing to rescale
                 ATHD_A32_QK(-mrun);
-                exp_sum(ls);
-            } else {
-                exp_sum(ls);
-                float lt = ls[0];
+            }
+            float ls[NKB];
 #pragma unroll
-                for (int kb = 1; kb < NKB; ++kb) lt += ls[kb];
-                if (__any(!(lt <= ATTN_SUM_TRIGGER))) {            // rare: this tile's scores far above the max
-                    ATHD_A32_QK(-mrun);
-                    const float mx = tile_max();
-                    const float dm = mx > 0.f ? mx : 0.f;
-                    const float alpha = __builtin_amdgcn_exp2f(-dm);
-                    mrun += dm;
-                    lrun *= alpha;
+            for (int kb = 0; kb < NKB; ++kb) {
+                ls[kb] = 0.f;
 #pragma unroll
-                    for (int i = 0; i < 16; ++i) {
-                        o0[i] *= alpha;
-                        o1[i] *= alpha;
-                    }
-                    ATHD_A32_QK(-mrun);
-                    exp_sum(ls);
+                for (int i = 0; i < 16; ++i) {
+                    sc[kb][i] = __builtin_amdgcn_exp2f(sc[kb][i]);
+                    ls[kb] += sc[kb][i];
                 }
             }
 #pragma unroll

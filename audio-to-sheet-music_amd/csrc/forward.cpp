@@ -493,19 +493,30 @@ void encode(Run& r, const Dims& d, const Bufs& b, const float* wav) {
     }
     struct Pending { const double* st = nullptr; const float* w = nullptr; const float* b = nullptr; };
     Pending pf, pt;
+    // bf16 mode: the LayerNorm pass that consumes a pending GroupNorm applies it in registers only, without writing
+    // X / XT back; the branch's next out_proj applies the same GroupNorm to its residual read (GemmDesc::res_gn_*), the
+    // only other reader of those raw rows (the cross layers' second norm of the same rows runs inside the same pass).
+    // Saves the 271 MB (freq) / 136 MB (time) write-back per layer.  f32 mode keeps the write-back.
+    const bool lazy_gn = r.actbf;
+    Pending rf, rt;                              // consumed by the last LayerNorm, due on the next out_proj residual
     auto ln2 = [&](float* x, int64_t N, const float* w, const float* bb, Pending* pend, void* out, const float* w2,
-                   const float* b2, void* out2) {
+                   const float* b2, void* out2, Pending* resgn) {
         LnDesc l;
         l.x = x; l.nb = (int)B; l.N = N; l.C = 512; l.w = w; l.b = bb; l.out = out; l.out_bf16 = ab;
-        if (pend && pend->st) { l.gn_stats = pend->st; l.gn_w = pend->w; l.gn_b = pend->b; *pend = Pending(); }
+        if (pend && pend->st) {
+            l.gn_stats = pend->st; l.gn_w = pend->w; l.gn_b = pend->b;
+            if (lazy_gn && resgn) { l.gn_writeback = 0; *resgn = *pend; }
+            *pend = Pending();
+        }
         l.w2 = w2; l.b2 = b2; l.out2 = out2;
         layernorm_launch(l, r.s);
     };
-    auto ln = [&](float* x, int64_t N, const float* w, const float* bb, Pending* pend, void* out) {
-        ln2(x, N, w, bb, pend, out, nullptr, nullptr, nullptr);
+    auto ln = [&](float* x, int64_t N, const float* w, const float* bb, Pending* pend, void* out, Pending* resgn) {
+        ln2(x, N, w, bb, pend, out, nullptr, nullptr, nullptr, resgn);
     };
     // attention + FFN of one branch given LN'ed query rows Hq and key/value source (projected inside)
-    auto block = [&](const TLayerW& L, float* X, int64_t N, void* Hq, void* Hkv, int64_t Nk, Pending* pend, bool tb) {
+    auto block = [&](const TLayerW& L, float* X, int64_t N, void* Hq, void* Hkv, int64_t Nk, Pending* pend, bool tb,
+                     Pending* resgn) {
         void* const sQKV = tb ? b.QKVt : b.QKV;
         void* const sO = tb ? b.Ot : b.O;
         void* const sF1 = tb ? b.F1t : b.F1;
@@ -536,8 +547,12 @@ void encode(Run& r, const Dims& d, const Bufs& b, const float* wav) {
         r.check(attn_launch(a, r.mode, r.s), "attention");
         GemmDesc go = r.lin(L.out, sO, ab, (int)B, N, 512);
         go.C = X; go.res = X; go.res_scale = L.g1;
+        if (resgn->st) {
+            go.res_gn_stats = resgn->st; go.res_gn_count = N * 512; go.res_gn_w = resgn->w; go.res_gn_b = resgn->b;
+            *resgn = Pending();
+        }
         r.gemm(go, "out_proj");
-        ln(X, N, L.cross ? L.n3w : L.n2w, L.cross ? L.n3b : L.n2b, nullptr, Hq);
+        ln(X, N, L.cross ? L.n3w : L.n2w, L.cross ? L.n3b : L.n2b, nullptr, Hq, nullptr);
         GemmDesc g1 = r.lin(L.l1, Hq, ab, (int)B, N, 512);
         g1.C = sF1; g1.c_bf16 = ab; g1.act = ACT_GELU;
         r.gemm(g1, "linear1");
@@ -569,26 +584,26 @@ void encode(Run& r, const Dims& d, const Bufs& b, const float* wav) {
         const TLayerW& Lt = c->Lt[idx];
         if (!Lf.cross) {
             r.s = s_f;
-            ln(b.X, d.Nf, Lf.n1w, Lf.n1b, &pf, b.H[0]);
-            block(Lf, b.X, d.Nf, b.H[0], nullptr, d.Nf, &pf, false);
+            ln(b.X, d.Nf, Lf.n1w, Lf.n1b, &pf, b.H[0], &rf);
+            block(Lf, b.X, d.Nf, b.H[0], nullptr, d.Nf, &pf, false, &rf);
             r.s = s_t;
-            ln(b.XT, d.Nt, Lt.n1w, Lt.n1b, &pt, b.H[2]);
-            block(Lt, b.XT, d.Nt, b.H[2], nullptr, d.Nt, &pt, true);
+            ln(b.XT, d.Nt, Lt.n1w, Lt.n1b, &pt, b.H[2], &rt);
+            block(Lt, b.XT, d.Nt, b.H[2], nullptr, d.Nt, &pt, true, &rt);
         } else {
             join();
             // all four norms read the pre-layer X / XT (time branch attends to old_x, demucs transformer.py)
             // (bf16 mode: each pair is one pass over X / XT with two affines, layernorm_launch's out2)
             r.s = s_f;
-            ln2(b.X, d.Nf, Lf.n1w, Lf.n1b, &pf, b.H[0], Lt.n2w, Lt.n2b, b.H[1]);   // pending GN applied to X; norm1(x) and
+            ln2(b.X, d.Nf, Lf.n1w, Lf.n1b, &pf, b.H[0], Lt.n2w, Lt.n2b, b.H[1], &rf);   // pending GN applied to X; norm1(x) and
                                                                                 // the time branch's kv = norm2_t(old_x)
             r.s = s_t;
-            ln2(b.XT, d.Nt, Lt.n1w, Lt.n1b, &pt, b.H[2], Lf.n2w, Lf.n2b, b.H[3]);  // norm1_t(xt) and the freq branch's kv
+            ln2(b.XT, d.Nt, Lt.n1w, Lt.n1b, &pt, b.H[2], Lf.n2w, Lf.n2b, b.H[3], &rt);  // norm1_t(xt) and the freq branch's kv
                                                                                 // = norm2(xt)
             join();
             r.s = s_f;
-            block(Lf, b.X, d.Nf, b.H[0], b.H[3], d.Nt, &pf, false);
+            block(Lf, b.X, d.Nf, b.H[0], b.H[3], d.Nt, &pf, false, &rf);
             r.s = s_t;
-            block(Lt, b.XT, d.Nt, b.H[2], b.H[1], d.Nf, &pt, true);
+            block(Lt, b.XT, d.Nt, b.H[2], b.H[1], d.Nf, &pt, true, &rt);
         }
     }
     // the last layer's pending GroupNorm: in the bf16 mode applied by the downsamplers' A load (gemm2 a_gn; X / XT

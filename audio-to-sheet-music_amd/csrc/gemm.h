@@ -80,6 +80,14 @@ struct GemmDesc {
     const void* res = nullptr;        // residual (same layout as C; f32, or bf16 with res_bf16); out = res + rs[n]*v
     int res_bf16 = 0;
     const float* res_scale = nullptr;
+    // optional GroupNorm(1) on the f32 residual as it is read (epilogue flag F_RGN, gemm5's residual epilogue): the
+    // residual stream's pending GroupNorm, which the LayerNorm pass before this GEMM applied in registers only
+    // (LnDesc::gn_writeback = 0): res' = (res - mean[b]) * rstd[b] * res_gn_w[n] + res_gn_b[n], statistics {sum, sumsq}
+    // over res_gn_count elements per batch
+    const double* res_gn_stats = nullptr;
+    int64_t res_gn_count = 0;
+    const float* res_gn_w = nullptr;
+    const float* res_gn_b = nullptr;
     const float* row_add = nullptr;   // out += row_add[ho][n]   (freq embedding after encoder level 0)
     double* stats = nullptr;          // per-batch {sum, sumsq} of the final output value
     const double* gn_stats = nullptr; // GroupNorm(1) applied to v (after bias, before act) with per-batch

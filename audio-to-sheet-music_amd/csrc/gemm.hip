@@ -293,6 +293,8 @@ int gemm_launch(const GemmDesc& d0, int mode, hipStream_t s) {
     // the GroupNorm folded into the A load (a_gn_*, the transformer's last pending GroupNorm): gemm2 only; refuse
     // rather than silently skip it on another kernel
     if (d.a_gn_stats) return mode == 1 && gemm2_supported(d) ? gemm2_launch(d, s) : -2;
+    // the residual's GroupNorm (res_gn_*): gemm5's residual epilogue only
+    if (d.res_gn_stats && !(mode == 1 && gemm5_supported(d) && d.N % 256 == 0 && epi_res_fast_ok(d))) return -2;
     // bf16 activations, N a multiple of 256: 256x256 tile, staggered two-group K-loop (gemm5.hip; it replaced round
     // 2's gemm4.hip, which tools/kbench still builds as the A/B baseline: kbench +6..16 % on the transformer shapes,
     // equal at K = 2048).  (Measured on N = 192 / 384: slower than gemm3's 256x192 tiles, which waste no columns.)

@@ -348,9 +348,23 @@ __global__ __launch_bounds__(512) void gemm5_kernel(const GemmDesc d) {
             for (int j = 0; j < TN; ++j) bias4[j] = *reinterpret_cast<const float4*>(bl + 16 * j);
         }
         bool fast = false;
-        if constexpr ((F & F_RES) != 0 && (F & ~(F_RES | F_STATS)) == 0) {
+        if constexpr ((F & F_RES) != 0 && (F & ~(F_RES | F_STATS | F_RGN)) == 0) {
             if (epi_res_fast_ok(d)) {
-                gemm_epilogue_res<TM, TN, F>(d, acc, m0_done, n0_done, wm0, wn0, lane, st_lds, 256, bias4);
+                float* gn_lds = nullptr;
+                if constexpr ((F & F_RGN) != 0) {
+                    // the residual GroupNorm affine of the tile's 256 columns -> staging slot 0 (free: not persistent, so
+                    // no next-tile prologue; every wave's last fragment reads retired before the loop's last barrier)
+                    static_assert(!PERSIST, "F_RGN stages through a ring slot");
+                    gn_lds = reinterpret_cast<float*>(smem);
+                    if (tid < 256) {
+                        const int n = n0_done + tid < d.N ? n0_done + tid : d.N - 1;
+                        gn_lds[tid] = d.res_gn_w[n];
+                        gn_lds[256 + tid] = d.res_gn_b[n];
+                        gn_lds[512 + tid] = d.res_scale ? d.res_scale[n] : 1.f;
+                    }
+                    __syncthreads();
+                }
+                gemm_epilogue_res<TM, TN, F>(d, acc, m0_done, n0_done, wm0, wn0, lane, st_lds, 256, bias4, gn_lds);
                 fast = true;
             }
         }

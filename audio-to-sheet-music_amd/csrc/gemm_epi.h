@@ -19,7 +19,7 @@ constexpr int EPI_MAXG = 32;   // GroupNorm groups tracked per block in LDS
 
 enum EpiFlag : unsigned {
     F_GELU = 1u, F_GLU = 2u, F_RES = 4u, F_STATS = 8u, F_GN = 16u, F_ROWADD = 32u, F_SPLIT = 64u, F_CBF16 = 128u,
-    F_NOSTORE = 256u, F_PB = 512u, F_LN = 1024u, F_ALL = 0xFFFFu
+    F_NOSTORE = 256u, F_PB = 512u, F_LN = 1024u, F_RGN = 2048u, F_ALL = 0xFFFFu
 };
 
 inline unsigned epi_flags(const GemmDesc& d) {
@@ -35,6 +35,7 @@ inline unsigned epi_flags(const GemmDesc& d) {
     if (!d.store) f |= F_NOSTORE;
     if (d.pbias) f |= F_PB;
     if (d.ln_w) f |= F_LN;
+    if (d.res_gn_stats) f |= F_RGN;
     return f;
 }
 
@@ -43,7 +44,7 @@ inline unsigned epi_flags(const GemmDesc& d) {
     X(0u) X(F_CBF16) X(F_GELU) X(F_GELU | F_CBF16) X(F_RES) X(F_RES | F_STATS) X(F_GLU) X(F_GLU | F_ROWADD)    \
     X(F_STATS | F_NOSTORE) X(F_GN | F_GLU | F_RES) X(F_STATS) X(F_SPLIT | F_STATS) X(F_SPLIT)                  \
     X(F_SPLIT | F_STATS | F_CBF16) X(F_SPLIT | F_CBF16) X(F_GLU | F_CBF16) X(F_GLU | F_ROWADD | F_CBF16)         \
-    X(F_GN | F_GLU | F_RES | F_CBF16) X(F_GELU | F_CBF16 | F_PB) X(F_GELU | F_PB) X(F_RES | F_PB)
+    X(F_GN | F_GLU | F_RES | F_CBF16) X(F_GELU | F_CBF16 | F_PB) X(F_GELU | F_PB) X(F_RES | F_PB) X(F_RES | F_RGN)
 
 // Publishes the LDS statistics partials before the per-block flush: the LDS atomics retired (lgkmcnt) + s_barrier.
 // Not __syncthreads(): that also waits vmcnt(0), i.e. for every output store of the tile to be acknowledged,
@@ -414,13 +415,18 @@ __device__ __attribute__((weak)) float4 g_epi_sink[64];
 
 ATHD_HD bool epi_res_fast_ok(const GemmDesc& d) {
     return d.res && !d.res_bf16 && !d.c_bf16 && d.store && d.act == ACT_NONE && !d.gn_stats && !d.row_add && !d.pbias &&
-           !d.col_split && d.o_stride == 1 && d.o_off == 0 && d.H_out_total == d.H_out && d.c_bs < 0 && d.N % 4 == 0;
+           !d.col_split && d.o_stride == 1 && d.o_off == 0 && d.H_out_total == d.H_out && d.c_bs < 0 && d.N % 4 == 0 &&
+           (!d.res_gn_stats || (d.res_gn_w && d.res_gn_b && d.res_gn_count > 0 && d.col_off == 0 &&
+                                 (int64_t)d.H_out * d.W >= 256));
 }
 
+// F_RGN: gn_lds holds the residual GroupNorm affine of the tile's columns, w at [n - n0], b at [256 + n - n0], and
+// the residual scale at [512 + n - n0] (staged by the kernel; registers for them would spill the residual ring)
 template <int TM, int TN, unsigned F>
 ATHD_DEV void gemm_epilogue_res(const GemmDesc& d, const f32x4_t (&acc)[TM][TN], int64_t m0, int n0, int wm0, int wn0,
-                                int lane, double* st_lds, int BM, const float4* bj) {
+                                int lane, double* st_lds, int BM, const float4* bj, const float* gn_lds = nullptr) {
     constexpr bool f_stats = (F & F_STATS) != 0;
+    constexpr bool f_rgn = (F & F_RGN) != 0;
     const int fr = lane & 15, fg = lane >> 4;
     const uint32_t M = (uint32_t)d.nb * d.H_out * d.W;
     const uint32_t g0 = fdiv((uint32_t)m0, d.fd_hw);
@@ -434,7 +440,8 @@ ATHD_DEV void gemm_epilogue_res(const GemmDesc& d, const f32x4_t (&acc)[TM][TN],
         ncol[j] = n0 + wn0 + 16 * j + 4 * fg;
         const int nc = ncol[j] < d.N ? ncol[j] : d.N - 4;
         ncol[j] = nc;
-        sc[j] = d.res_scale ? *reinterpret_cast<const float4*>(d.res_scale + nc) : make_float4(1.f, 1.f, 1.f, 1.f);
+        if constexpr (!f_rgn)   // (F_RGN: the scale is read from gn_lds per fragment, its registers go to the affine)
+            sc[j] = d.res_scale ? *reinterpret_cast<const float4*>(d.res_scale + nc) : make_float4(1.f, 1.f, 1.f, 1.f);
     }
     bool colok[TN];
 #pragma unroll
@@ -447,6 +454,14 @@ ATHD_DEV void gemm_epilogue_res(const GemmDesc& d, const f32x4_t (&acc)[TM][TN],
         ok[i] = m < M;
         rb[i] = (int64_t)(ok[i] ? m : M - 1) * d.ldo + d.col_off;
     }
+    // F_RGN: (mean, rstd) of the tile's first batch g0 and of g0 + 1 (a BM-row tile spans at most two batches: every
+    // caller has H_out * W >= BM rows per batch, epi_res_fast_ok)
+    float rgn[4] = {0.f, 1.f, 0.f, 1.f};
+    if constexpr (f_rgn) {
+        const uint32_t glast = fdiv(M - 1, d.fd_hw);
+        gn_params(d.res_gn_stats, g0, d.res_gn_count, rgn[0], rgn[1]);
+        gn_params(d.res_gn_stats, g0 + 1 <= glast ? g0 + 1 : glast, d.res_gn_count, rgn[2], rgn[3]);
+    }
     const float* res = (const float*)d.res;
     float* C = (float*)d.C;
     float* sink = reinterpret_cast<float*>(g_epi_sink + lane);
@@ -457,7 +472,8 @@ ATHD_DEV void gemm_epilogue_res(const GemmDesc& d, const f32x4_t (&acc)[TM][TN],
 #ifndef ATHD_RES_RD
 #define ATHD_RES_RD 3      // 3: two fragments ahead (244-246 VGPRs; 4 spills in the K-loop kernels)
 #endif
-    constexpr int RD = TM < ATHD_RES_RD ? TM : ATHD_RES_RD;
+    constexpr int RD0 = f_rgn ? 2 : ATHD_RES_RD;     // (F_RGN: its per-fragment affine needs the ring's registers)
+    constexpr int RD = TM < RD0 ? TM : RD0;
     float4 rr[RD][TN];
 #pragma unroll
     for (int i = 0; i + 1 < RD; ++i)
@@ -472,9 +488,26 @@ ATHD_DEV void gemm_epilogue_res(const GemmDesc& d, const f32x4_t (&acc)[TM][TN],
                 rr[(i + RD - 1) % RD][j] = *reinterpret_cast<const float4*>(res + rb[i + RD - 1] + ncol[j]);
         }
         float s1 = 0.f, s2 = 0.f;
+        float rgm = 0.f, rgr = 1.f;            // F_RGN: the residual row's GroupNorm (mean, rstd)
+        if constexpr (f_rgn) {
+            const uint32_t m = (uint32_t)m0 + wm0 + 16 * i + fr;
+            const bool second = fdiv(ok[i] ? m : M - 1, d.fd_hw) != g0;
+            rgm = second ? rgn[2] : rgn[0];
+            rgr = second ? rgn[3] : rgn[1];
+        }
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
-            const float4 rc = rr[i % RD][j];
+            float4 rc = rr[i % RD][j];
+            if constexpr (f_rgn) {
+                const int cl = ncol[j] - n0;
+                const float4 gw = *reinterpret_cast<const float4*>(gn_lds + cl);
+                const float4 gb = *reinterpret_cast<const float4*>(gn_lds + 256 + cl);
+                sc[j] = *reinterpret_cast<const float4*>(gn_lds + 512 + cl);
+                rc.x = (rc.x - rgm) * rgr * gw.x + gb.x;
+                rc.y = (rc.y - rgm) * rgr * gw.y + gb.y;
+                rc.z = (rc.z - rgm) * rgr * gw.z + gb.z;
+                rc.w = (rc.w - rgm) * rgr * gw.w + gb.w;
+            }
             const float4 o = make_float4(rc.x + sc[j].x * (acc[i][j][0] + bj[j].x), rc.y + sc[j].y * (acc[i][j][1] + bj[j].y),
                                          rc.z + sc[j].z * (acc[i][j][2] + bj[j].z), rc.w + sc[j].w * (acc[i][j][3] + bj[j].w));
             const bool st = ok[i] && colok[j];

@@ -60,6 +60,8 @@ struct LnDesc {
     float* x = nullptr; int nb = 1; int64_t N = 0; int C = 512;
     const float* w = nullptr; const float* b = nullptr;
     const double* gn_stats = nullptr; const float* gn_w = nullptr; const float* gn_b = nullptr;
+    int gn_writeback = 1;    // 0: the pending GroupNorm is applied in registers only (x keeps its raw values; the next
+                             // reader of x as a residual applies it again: GemmDesc::res_gn_*, bf16 mode)
     const float* pos = nullptr;
     void* out = nullptr; int out_bf16 = 0;
     // optional second affine of the same normalised rows -> out2 (C = 512, bf16, no pos): the cross layers' two

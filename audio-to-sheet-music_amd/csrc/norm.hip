@@ -525,9 +525,11 @@ __global__ __launch_bounds__(256) void layernorm_rows_kernel(const LnDesc d) {
             gn_params(d.gn_stats, row / d.N, d.N * (int64_t)C, gm, gr);
 #pragma unroll
             for (int j = 0; j < 8; ++j) v[r][j] = (v[r][j] - gm) * gr * gw[j] + gb[j];
-            float4* xo = reinterpret_cast<float4*>(d.x + row * C + 8 * lane);
-            xo[0] = make_float4(v[r][0], v[r][1], v[r][2], v[r][3]);
-            xo[1] = make_float4(v[r][4], v[r][5], v[r][6], v[r][7]);
+            if (d.gn_writeback) {
+                float4* xo = reinterpret_cast<float4*>(d.x + row * C + 8 * lane);
+                xo[0] = make_float4(v[r][0], v[r][1], v[r][2], v[r][3]);
+                xo[1] = make_float4(v[r][4], v[r][5], v[r][6], v[r][7]);
+            }
         }
     }
 #pragma unroll
@@ -584,7 +586,8 @@ void layernorm_launch(const LnDesc& d0, hipStream_t s) {
         const dim3 grid((unsigned)((rows + 4 * LN_RW - 1) / (4 * LN_RW)));
         KScope ks(s);
         if (ks.on()) {
-            double by = (double)rows * d.C * (4 + (d.out_bf16 ? 2 : 4)) + (d.gn_stats ? (double)rows * d.C * 4 : 0.0);
+            double by = (double)rows * d.C * (4 + (d.out_bf16 ? 2 : 4)) +
+                        (d.gn_stats && d.gn_writeback ? (double)rows * d.C * 4 : 0.0);
             if (d.pos) by += (double)d.N * d.C * 4;
             if (d.out2) by += (double)rows * d.C * 2;
             ks.begin(klabel("layernorm_rows_kernel<%d>", LN_RW), 0.0, by);
