@@ -505,7 +505,8 @@ void encode(Run& r, const Dims& d, const Bufs& b, const float* wav) {
         l.x = x; l.nb = (int)B; l.N = N; l.C = 512; l.w = w; l.b = bb; l.out = out; l.out_bf16 = ab;
         if (pend && pend->st) {
             l.gn_stats = pend->st; l.gn_w = pend->w; l.gn_b = pend->b;
-            if (lazy_gn && resgn) { l.gn_writeback = 0; *resgn = *pend; }
+            // (the residual epilogue takes it when a 256-row tile spans at most two batches: N >= 256 tokens)
+            if (lazy_gn && resgn && N >= 256) { l.gn_writeback = 0; *resgn = *pend; }
             *pend = Pending();
         }
         l.w2 = w2; l.b2 = b2; l.out2 = out2;
