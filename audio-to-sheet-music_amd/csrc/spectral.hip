@@ -149,8 +149,17 @@ __global__ __launch_bounds__(256) void stft_kernel(const float* __restrict__ wav
                                                    const TW* __restrict__ tw, const float* __restrict__ win,
                                                    float* __restrict__ specT, double* __restrict__ st) {
     __shared__ cpx buf[FPAD];
-    const int t = blockIdx.x;
-    const int64_t b = blockIdx.y;
+    // 1-D grid over (b, t), each XCD a contiguous range (workgroup i runs on XCD i % 8): the 4 frames that share each
+    // hop of samples run on one XCD and read them from HBM once (a frame-fastest 2-D grid put neighbouring frames on
+    // different XCDs: 1.6x the waveform bytes, PMC)
+    int t;
+    int64_t b;
+    {
+        const int n = (int)gridDim.x, q = n / 8, r = n % 8, x = (int)blockIdx.x % 8;
+        const int id = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (int)blockIdx.x / 8;
+        t = id % Tspec;
+        b = id / Tspec;
+    }
     const float* xl = wav + b * 2 * T;
     const float* xr = xl + T;
     const int64_t p0 = (int64_t)t * HOP;     // kept frame t = stft frame t+2, starts at 1024 t in the pad1d'ed signal
@@ -196,11 +205,12 @@ void stft_launch(const float* wav, int nb, int64_t T, const PadPlan& pp, int Tsp
                  const double2* tw64, const float* win, float* specT, double* stats, hipStream_t s) {
     KScope ks(s);
     if (ks.on()) ks.begin(tw64 ? "stft_kernel<double,HIP_vector_type<double,2>>" : "stft_kernel<float,HIP_vector_type<float,2>>", 0.0, (double)nb * 2 * T * 4 + (double)nb * 2048 * Tspec * 4 * 4);
+    // 1-D grid of Tspec * nb workgroups (the kernel maps each to its (b, t) XCD-contiguously)
     if (tw64)
-        hipLaunchKernelGGL((stft_kernel<double, double2>), dim3(Tspec, nb), dim3(256), 0, s, wav, T, pp, Tspec, tw64, win,
-                           specT, stats);
+        hipLaunchKernelGGL((stft_kernel<double, double2>), dim3(Tspec * nb, 1), dim3(256), 0, s, wav, T, pp, Tspec, tw64,
+                           win, specT, stats);
     else
-        hipLaunchKernelGGL((stft_kernel<float, float2>), dim3(Tspec, nb), dim3(256), 0, s, wav, T, pp, Tspec, tw, win,
+        hipLaunchKernelGGL((stft_kernel<float, float2>), dim3(Tspec * nb, 1), dim3(256), 0, s, wav, T, pp, Tspec, tw, win,
                            specT, stats);
 }
 
