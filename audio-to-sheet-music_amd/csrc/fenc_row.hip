@@ -489,6 +489,15 @@ ATHD_DEV int opaque_lane() {
 
 }  // namespace
 
+#ifdef ATHD_FR_STAMP
+// measurement build only (-DATHD_FR_STAMP, tools/fr_stamps.py): s_memtime at the phase boundaries of
+// fenc_row0_kernel, wave 0 of every workgroup -> g_fr_stamp[block][16]; read back with athd_fr_stamps
+__device__ uint64_t g_fr_stamp[65536 * 16];
+#define FR_STAMP(k) do { if (threadIdx.x == 0) g_fr_stamp[(size_t)blockIdx.x * 16 + (k)] = __builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define FR_STAMP(k) do { } while (0)
+#endif
+
 __global__ __launch_bounds__(FR_NT, 4) void fenc_row0_kernel(const FencRowDesc d) {
     constexpr int C = F0_C, H = F0_H, NCT = 3, MTW = 9;
     __shared__ __attribute__((aligned(16))) bf16_t xin[F0_TP * F0_XIN_P];    // conv input, then the hidden tile
@@ -497,6 +506,7 @@ __global__ __launch_bounds__(FR_NT, 4) void fenc_row0_kernel(const FencRowDesc d
     __shared__ float red[4][2 * FR_NW];
     __shared__ float gsh[2][52];                 // the 1x1 convs' moments (50 floats per layer)
 
+    FR_STAMP(0);
     const int R = d.B * d.Fout;
     const int per = (R + 7) / 8;
     const int r = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
@@ -545,6 +555,7 @@ __global__ __launch_bounds__(FR_NT, 4) void fenc_row0_kernel(const FencRowDesc d
         *reinterpret_cast<uint4*>(&xin[hs_off(m, q * 8)]) = v;
     }
     __syncthreads();
+    FR_STAMP(1);
 
     // ---- conv (8,1)/(4,1)/(2,0): one K-step of 32 + bias + GELU; residual stream xr in registers
     f32x4_t xr[MTW];
@@ -571,6 +582,7 @@ __global__ __launch_bounds__(FR_NT, 4) void fenc_row0_kernel(const FencRowDesc d
         }
     }
     __syncthreads();
+    FR_STAMP(2);
     // the conv input is dead: zero the hidden tile's K padding columns 16..31
     for (int i = tid; i < F0_TP * 2; i += FR_NT)
         *reinterpret_cast<uint4*>(&hs[hs_off(i >> 1, 16 + 8 * (i & 1))]) = make_uint4(0u, 0u, 0u, 0u);
@@ -620,7 +632,9 @@ __global__ __launch_bounds__(FR_NT, 4) void fenc_row0_kernel(const FencRowDesc d
             g1w[q] = d.g1w[dd][min(4 * l4 + q, H - 1)];
             g1b[q] = d.g1b[dd][min(4 * l4 + q, H - 1)];
         }
+        FR_STAMP(3 + 4 * dd);
         block_sum2_dpp(s1, s2, red[2 * dd]);
+        FR_STAMP(4 + 4 * dd);
         float hm, hr;
         gn_from_sums(s1, s2, (float)(H * T), hm, hr);
         // GELU(GN(h)) -> hs (bf16); then the 1x1 output's GroupNorm statistics from the moments of the 1x1 conv
@@ -674,6 +688,7 @@ __global__ __launch_bounds__(FR_NT, 4) void fenc_row0_kernel(const FencRowDesc d
         const float4 gwg = ld4f(d.g2w[dd] + pa + 16), gbg = ld4f(d.g2b[dd] + pa + 16);
         const float4 sc4 = ld4f(d.scale[dd] + cb);
         block_sum2_dpp(s1, s2, red[2 * dd + 1]);
+        FR_STAMP(5 + 4 * dd);
         float ym, yr;
         gn_from_sums(s1, s2, (float)(2 * C * T), ym, yr);
         // (y + b - mean) * rstd * w + beta  as  y * wa + ca  (wa = rstd w, ca = (b - mean) wa + beta); the 'a' half
@@ -713,6 +728,7 @@ __global__ __launch_bounds__(FR_NT, 4) void fenc_row0_kernel(const FencRowDesc d
             st4bf(&xs[xs_off(FR_HALO + l15c, cb) + mt * 16 * F0_XS_P], xr[i][0], xr[i][1], xr[i][2], xr[i][3]);
         }
         __syncthreads();
+        FR_STAMP(6 + 4 * dd);
     }
 
     // ---- rewrite 1x1 (C -> 2C) + GLU + freq embedding
@@ -753,6 +769,7 @@ __global__ __launch_bounds__(FR_NT, 4) void fenc_row0_kernel(const FencRowDesc d
                 o[q] = (za[q] + bav[q]) * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(zg[q] * -1.4426950408889634f + bgv[q])) + rav[q];
             ov[i] = make_uint2(pack2bf(o[0], o[1]), pack2bf(o[2], o[3]));
         }
+        FR_STAMP(11);
         __syncthreads();         // every wave has read xs: stage the output row [T][C] there
         bf16_t* ob = xs;
 #pragma unroll
@@ -768,12 +785,19 @@ __global__ __launch_bounds__(FR_NT, 4) void fenc_row0_kernel(const FencRowDesc d
             uint2* d4 = reinterpret_cast<uint2*>(d.out4 + ((int64_t)b * d.Fout + f) * (int64_t)T * 4);
             for (int m = tid; m < T; m += FR_NT) d4[m] = *reinterpret_cast<const uint2*>(&ob[m * C]);
         }
+        FR_STAMP(12);
     }
 }
 
 bool fenc_row_supported(int cin, int c, int T) {
     return ((cin == 4 && c == 48) || (cin == 48 && c == 96)) && T >= 1 && T <= 16 * FR_MT_MAX;
 }
+
+#ifdef ATHD_FR_STAMP
+extern "C" int athd_fr_stamps(void* host, int blocks) {
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_fr_stamp), (size_t)blocks * 16 * 8, 0, hipMemcpyDeviceToHost);
+}
+#endif
 
 int fenc_row_launch(const FencRowDesc& d, int cin, int c, hipStream_t s) {
     // (the 1x1 convs' GroupNorm statistics come from their moments, d.gram)
