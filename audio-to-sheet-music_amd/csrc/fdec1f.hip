@@ -1,0 +1,382 @@
+// FreqDecoder level 1, GroupNorm statistics as a quadratic form (bf16 mode; ATHTDemucs_v2.py:90-103 for i = 1, the
+// re-association of fdec_lr.hip).
+//
+// fdec_lr.hip writes Z = S @ [W_0 .. W_7] (3.3 GB of bf16 at the bench size) and sweeps it twice: once for the
+// GroupNorm(1) {sum, sumsq} of the level-1 ConvT output Y, once to merge.  The merge pass only reads taps 0, 3, 4, 7
+// (rows 4d+1, 4d+2), so Z is needed in full only for the statistics - and those need no sweep at all.  Every ConvT
+// output row r = 4v + rho involves ONE tap class q = (rho + 2) % 4, i.e. taps {q, q+4}:
+//   y_r[w][c] = b_c + c_r . x_q[w][c],   x_q = (Z_q[0..31], Z_{q+4}[0..31], Zs_q[0..7], Zs_{q+4}[0..7])   (80 values)
+// with c_r the resize-lerp coefficients of the row (2 per tap, 0.1 on the Zs rows).  Over the Hd rows of a class:
+//   sum   y   = Hd W sum_c b_c    + c1_q . u_q                   c1_q = sum_r c_r,      u_q  = sum_wc x_q
+//   sum   y^2 = Hd W sum_c b_c^2  + 2 c1_q . ub_q + <Q_q, G_q>   Q_q = sum_r c_r c_r^T, ub_q = sum_wc b_c x_q,
+//                                                                                       G_q  = sum_wc x_q x_q^T
+// Q_q / c1_q depend only on (Hd, Hs, Hk) (fdec1_gram_q_kernel, double); G_q and the per-channel sums of x_q are a
+// Gram matrix over (w, c): matrix-core work on the Z tile while it is in LDS.  So this pass computes Z tile by tile
+// (MFMA, into LDS, never to HBM), accumulates the 4 classes' 80 x 80 Gram blocks in MFMA accumulators across the
+// tiles of an item, flushes them per item with fp32 atomics, and fdec1_gram_final_kernel forms {sum, sumsq}.  It
+// replaces the 8-tap Z store + fdec_lr_stats3_kernel's sweep (VALU-bound); the merge pass reads a 4-tap Z.
+//
+// Tile = (item n, 8 consecutive w columns, channel group of 16), all 32 rows j of S:
+//   Z GEMM   rows R = 8 j + wl (256; A = S[n][j][w0 + wl][0..191]), cols t * 16 + c (8 taps x 16 channels, K = 192);
+//            wave wv: rows 32 wv .. +31, all 128 columns (v_mfma_f32_16x16x32_bf16, weights as the A operand)
+//   LDS      ZT [t * 32 + j][wl * 16 + c] (bf16; the Gram's X rows), Zs [q * 16 + (t >> 2) * 8 + m][wl * 16 + c]
+//   Gram     per class q: X row blocks R0..R3 (Z, 16 rows each) and R4 (Zs), K = (wl, c) = 128; blocks (ri <= ci)
+//            of X X^T plus X times a one-hot channel matrix (the per-channel sums); wave wv: class wv >> 1, half
+//            wv & 1 of the class's 20 blocks (9 / 11), accumulated across the item's tiles.
+// Each persistent workgroup owns one channel group (its 128 weight rows stay in LDS, 48 KB) and walks a contiguous
+// run of (item, w block) tiles.  LDS chunks (16 B) of every [row][256 B] array are XOR-swizzled by (row & 15):
+// the MFMA-layout stores (ds_write_b64, 32 lanes) and the operand reads (ds_read_b128, 16 rows) both cover the 64
+// banks once.
+#include <type_traits>
+
+#include "common.h"
+#include "kernels.h"
+#include "prof.h"
+
+namespace athd {
+
+namespace {
+
+constexpr int G_CI = 192, G_CO = 96, G_HS = 32, G_HK = 8;
+constexpr int G_WB = 8;                       // w columns per tile
+constexpr int G_CG = 16;                      // channels per group
+constexpr int G_NG = G_CO / G_CG;             // 6 groups
+constexpr int G_THREADS = 512;
+constexpr int G_B_BYTES = 128 * 384;          // weights [128 cols][192 K]
+constexpr int G_ZT_BYTES = 256 * 256;         // ZT [(t, j)][(wl, c)]
+constexpr int G_ZS_BYTES = 64 * 256;          // Zs [(q, t >> 2, m)][(wl, c)]
+constexpr int G_LDS = G_B_BYTES + G_ZT_BYTES + G_ZS_BYTES;   // 128 KB
+constexpr int G_NX = 80;                      // x_q entries
+constexpr int G_NB = G_NX + G_CO;             // Gram row: 80 data columns + 96 per-channel sums
+constexpr int G_ITEM = 4 * G_NX * G_NB;       // floats per item
+
+ATHD_DEV int swz(int row, int chunk) { return row * 256 + ((chunk ^ (row & 15)) << 4); }
+
+ATHD_DEV int g_xcd_remap(int i, int n) {
+    const int q = n / 8, r = n % 8, x = i % 8;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i / 8;
+}
+
+// the Gram blocks of a wave: half 0 of a class takes rows R0 (columns 0..5) and R3 (3..5), half 1 rows R1 (1..5),
+// R2 (2..5), R4 (4, 5); column 5 = the one-hot channel matrix
+constexpr int G_NBLK = 11;
+ATHD_HD constexpr int blk_r(int h, int b) {
+    return h == 0 ? (b < 6 ? 0 : b < 9 ? 3 : -1) : (b < 5 ? 1 : b < 9 ? 2 : 4);
+}
+ATHD_HD constexpr int blk_c(int h, int b) {
+    return h == 0 ? (b < 6 ? b : b < 9 ? b - 3 : -1) : (b < 5 ? b + 1 : b < 9 ? b - 3 : b - 5);
+}
+
+// resize-lerp coefficient of x_q entry a in ConvT output row 4v + rho (rho = (q + 2) % 4): the row is
+// T_v[rho + 2] + (rho < 2 ? T_{v-1}[rho + 6] : T_{v+1}[rho - 2]) (fdec_lr.hip), T_s = lerp of the Z rows + 0.1 lerp
+// of the Zs rows at step s (zero outside 0 <= s < Hd)
+ATHD_HD double g_coef(int q, int v, int a, int Hd) {
+    const int rho = (q + 2) & 3;
+    const int t_main = rho < 2 ? q : q + 4;
+    const int v_oth = rho < 2 ? v - 1 : v + 1;
+    const bool zs = a >= 64;
+    const int idx = zs ? (a - 64) & 7 : a & 31;
+    const int tap = zs ? (a < 72 ? q : q + 4) : (a < 32 ? q : q + 4);
+    const int s = tap == t_main ? v : v_oth;
+    if (s < 0 || s >= Hd) return 0.0;
+    const LinIdx li = lin_index(s, zs ? G_HK : G_HS, Hd);
+    const double cf = (idx == li.i0 ? 1.0 - (double)li.l1 : 0.0) + (idx == li.i1 ? (double)li.l1 : 0.0);
+    return zs ? cf * (double)0.1f : cf;
+}
+
+}  // namespace
+
+// Q_q [4][80][80] and c1_q [4][80] (double, per class q: 6400 + 80 entries): one thread per entry
+__global__ __launch_bounds__(256) void fdec1_gram_q_kernel(double* gq, int Hd) {
+    const int e = blockIdx.x * 256 + threadIdx.x;
+    const int per = G_NX * G_NX + G_NX;
+    if (e >= 4 * per) return;
+    const int q = e / per, k = e % per;
+    double s = 0.0;
+    if (k < G_NX * G_NX) {
+        const int a = k / G_NX, b = k % G_NX;
+        for (int v = 0; v < Hd; ++v) {
+            const double ca = g_coef(q, v, a, Hd);
+            if (ca != 0.0) s += ca * g_coef(q, v, b, Hd);
+        }
+    } else {
+        const int a = k - G_NX * G_NX;
+        for (int v = 0; v < Hd; ++v) s += g_coef(q, v, a, Hd);
+    }
+    gq[e] = s;
+}
+
+__global__ __launch_bounds__(G_THREADS, 1) void fdec1_gram_kernel(const LowRankDesc d, float* gram) {
+    __shared__ __attribute__((aligned(16))) char smem[G_LDS];
+    char* const bl = smem;                                    // weights
+    char* const zt = smem + G_B_BYTES;                        // ZT
+    char* const zsl = zt + G_ZT_BYTES;                        // Zs
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int nblk = (int)gridDim.x;
+    const int L = g_xcd_remap((int)blockIdx.x, nblk);
+    const int g = L % G_NG, qi = L / G_NG, Qg = (nblk - 1 - g) / G_NG + 1;
+    const int c0 = g * G_CG;
+    const int W = d.W;
+    const int NWB = (W + G_WB - 1) / G_WB;
+    const int64_t T = (int64_t)d.NI * NWB;
+    const int64_t t_beg = T * qi / Qg, t_end = T * (qi + 1) / Qg;
+    const bf16_t* const S = (const bf16_t*)d.S;
+    const bf16_t* const Wt = (const bf16_t*)d.Wt;
+    const bf16_t* const Zs = (const bf16_t*)d.Zs;
+
+    // ---- weights of this channel group -> LDS (column t * 16 + c = weight row t * 96 + c0 + c) ----
+    for (int idx = tid; idx < 128 * 24; idx += G_THREADS) {
+        const int col = idx / 24, qq = idx % 24;
+        const int wrow = (col >> 4) * G_CO + c0 + (col & 15);
+        const uint4 v = *reinterpret_cast<const uint4*>(Wt + (int64_t)wrow * d.w_ld + qq * 8);
+        *reinterpret_cast<uint4*>(bl + col * 384 + ((qq ^ ((col >> 1) & 7)) << 4)) = v;
+    }
+
+    // ---- Z GEMM operands: this wave's tile rows 32 wv .. +31 ----
+    bf16x8_t sf[2][6];
+    auto load_s = [&](int64_t t) {
+        const int n = (int)(t / NWB), w0 = (int)(t % NWB) * G_WB;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int R = (2 * wv + i) * 16 + (lane & 15);
+            const int j = R >> 3, w = min(w0 + (R & 7), W - 1);
+            const bf16_t* p = S + (((int64_t)n * G_HS + j) * W + w) * G_CI + 8 * (lane >> 4);
+#pragma unroll
+            for (int ks = 0; ks < 6; ++ks) sf[i][ks] = *reinterpret_cast<const bf16x8_t*>(p + ks * 32);
+        }
+    };
+    // Zs rows of a tile: 1024 pieces of 16 B (t, m, wl, half), two per thread
+    uint4 zsr[2];
+    auto load_zs = [&](int64_t t) {
+        const int n = (int)(t / NWB), w0 = (int)(t % NWB) * G_WB, seg = n / d.P;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int p = tid * 2 + h;
+            const int tm = p >> 4, wl = (p >> 1) & 7, hf = p & 1;
+            const int tp = tm >> 3, m = tm & 7;
+            const int w = min(w0 + wl, W - 1);
+            zsr[h] = *reinterpret_cast<const uint4*>(Zs + (((int64_t)seg * G_HK + m) * W + w) * (8 * G_CO) + tp * G_CO +
+                                                     c0 + hf * 8);
+        }
+    };
+
+    // ---- Gram roles ----
+    const int gq = wv >> 1, gh = wv & 1;
+    const int nb = gh == 0 ? 9 : 11;
+    // one-hot channel matrix as the B operand: lane n = lane & 15 (channel), k = 8 (lane >> 4) + e is channel
+    // 8 ((lane >> 4) & 1) + e of the K index (wl, c)
+    bf16x8_t onehot;
+    {
+        const int e = (lane & 15) - 8 * ((lane >> 4) & 1);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) onehot[i] = (short)(i == e ? 0x3F80 : 0);
+    }
+    f32x4_t gacc[G_NBLK];
+#pragma unroll
+    for (int b = 0; b < G_NBLK; ++b) gacc[b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    auto flush = [&](int n) {
+        float* const gb = gram + ((int64_t)n * 4 + gq) * G_NX * G_NB;
+#pragma unroll
+        for (int b = 0; b < G_NBLK; ++b) {
+            if (b < nb) {
+                const int ri = blk_r(gh, b), ci = blk_c(gh, b);
+                const int col = ci < 5 ? ci * 16 + (lane & 15) : G_NX + c0 + (lane & 15);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int a = ri * 16 + 4 * (lane >> 4) + i;
+                    atomicAdd(gb + a * G_NB + col, gacc[b][i]);
+                }
+            }
+            gacc[b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+        }
+    };
+
+    int n_cur = -1;
+    if (t_beg < t_end) {
+        load_s(t_beg);
+        load_zs(t_beg);
+    }
+    __syncthreads();                               // weights visible
+
+    for (int64_t t = t_beg; t < t_end; ++t) {
+        const int n = (int)(t / NWB), w0 = (int)(t % NWB) * G_WB;
+        if (n != n_cur) {
+            if (n_cur >= 0) flush(n_cur);
+            n_cur = n;
+        }
+        // 1. Z tile (fp32 accumulators)
+        f32x4_t acc[2][8];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int cb = 0; cb < 8; ++cb) acc[i][cb] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < 6; ++ks) {
+#pragma unroll
+            for (int cb = 0; cb < 8; ++cb) {
+                const int col = cb * 16 + (lane & 15);
+                const int qq = ks * 4 + (lane >> 4);
+                const bf16x8_t wf = *reinterpret_cast<const bf16x8_t*>(bl + col * 384 + ((qq ^ ((col >> 1) & 7)) << 4));
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+                    acc[i][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, sf[i][ks], acc[i][cb], 0, 0, 0);
+            }
+        }
+        // 2. -> LDS as bf16 (the rounding of the stored Z of the unfused path), columns w >= W as zeros, once the
+        //    previous tile's Gram reads are done
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int R = (2 * wv + i) * 16 + (lane & 15);
+            const int j = R >> 3, wl = R & 7;
+            const uint32_t keep = w0 + wl < W ? ~0u : 0u;       // (a mask, not a branch per store)
+            const int c = 4 * (lane >> 4);
+#pragma unroll
+            for (int cb = 0; cb < 8; ++cb) {
+                uint2 v;
+                v.x = pack2bf(acc[i][cb][0], acc[i][cb][1]) & keep;
+                v.y = pack2bf(acc[i][cb][2], acc[i][cb][3]) & keep;
+                *reinterpret_cast<uint2*>(zt + swz(cb * 32 + j, wl * 2 + (c >> 3)) + ((c >> 2) & 1) * 8) = v;
+            }
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int p = tid * 2 + h;
+            const int tm = p >> 4, wl = (p >> 1) & 7, hf = p & 1;
+            const int tp = tm >> 3, m = tm & 7;
+            const uint32_t keep = w0 + wl < W ? ~0u : 0u;
+            const uint4 v = {zsr[h].x & keep, zsr[h].y & keep, zsr[h].z & keep, zsr[h].w & keep};
+            *reinterpret_cast<uint4*>(zsl + swz((tp & 3) * 16 + (tp >> 2) * 8 + m, wl * 2 + hf)) = v;
+        }
+        __syncthreads();
+        if (t + 1 < t_end) {
+            load_s(t + 1);
+            load_zs(t + 1);
+        }
+        // 3. Gram blocks of class gq over this tile's K = (wl, c): X row block ri = 16 consecutive LDS rows starting
+        //    at a multiple of 16, so the swizzle key of its row l & 15 is l & 15
+        auto gram_tile = [&](auto H) {             // H: this wave's half of the class blocks (compile time)
+            constexpr int h = decltype(H)::value;
+            constexpr int nbh = h == 0 ? 9 : 11;
+#pragma unroll 1
+            for (int ks = 0; ks < 4; ++ks) {
+                const int chunk = ks * 4 + (lane >> 4), row = lane & 15;
+                bf16x8_t xf[5];
+#pragma unroll
+                for (int ri = 0; ri < 5; ++ri) {
+                    const char* base =
+                        ri < 4 ? zt + ((ri < 2 ? gq : gq + 4) * 32 + (ri & 1) * 16) * 256 : zsl + gq * 16 * 256;
+                    xf[ri] = *reinterpret_cast<const bf16x8_t*>(base + row * 256 + ((chunk ^ row) << 4));
+                }
+#pragma unroll
+                for (int b = 0; b < nbh; ++b) {
+                    const int ri = blk_r(h, b), ci = blk_c(h, b);
+                    gacc[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[ri], ci < 5 ? xf[ci] : onehot, gacc[b], 0, 0, 0);
+                }
+            }
+        };
+        if (gh == 0) gram_tile(std::integral_constant<int, 0>{});
+        else gram_tile(std::integral_constant<int, 1>{});
+    }
+    if (n_cur >= 0) flush(n_cur);
+}
+
+// {sum, sumsq} of item n from its Gram blocks: one 256-thread block per item
+__global__ __launch_bounds__(256) void fdec1_gram_final_kernel(const float* gram, const double* gq, const float* bias,
+                                                               double* stats, int Hd, int W) {
+    const int n = blockIdx.x, tid = threadIdx.x;
+    const float* const gi = gram + (int64_t)n * G_ITEM;
+    const int per = G_NX * G_NX + G_NX;
+    double s1 = 0.0, s2 = 0.0;
+    // <Q_q, G_q> over the upper block triangle (off-diagonal blocks twice)
+    for (int e = tid; e < 4 * G_NX * G_NX; e += 256) {
+        const int q = e / (G_NX * G_NX), k = e % (G_NX * G_NX), a = k / G_NX, b = k % G_NX;
+        const int ra = a >> 4, rb = b >> 4;
+        if (ra <= rb) s2 += (ra == rb ? 1.0 : 2.0) * gq[q * per + k] * (double)gi[(q * G_NX + a) * G_NB + b];
+    }
+    // c1 . u and 2 c1 . ub from the per-channel sums
+    for (int e = tid; e < 4 * G_NX; e += 256) {
+        const int q = e / G_NX, a = e % G_NX;
+        const float* row = gi + (q * G_NX + a) * G_NB + G_NX;
+        double u = 0.0, ub = 0.0;
+        for (int c = 0; c < G_CO; ++c) {
+            u += (double)row[c];
+            ub += (double)bias[c] * (double)row[c];
+        }
+        const double c1 = gq[q * per + G_NX * G_NX + a];
+        s1 += c1 * u;
+        s2 += 2.0 * c1 * ub;
+    }
+    if (tid < G_CO) {
+        const double b = bias[tid], rows = 4.0 * Hd * W;
+        s1 += rows * b;
+        s2 += rows * b * b;
+    }
+    s1 = wave_sum_d(s1);
+    s2 = wave_sum_d(s2);
+    __shared__ double sh[2][4];
+    if ((tid & 63) == 0) { sh[0][tid >> 6] = s1; sh[1][tid >> 6] = s2; }
+    __syncthreads();
+    if (tid == 0) {
+        stats[2 * n] = sh[0][0] + sh[0][1] + sh[0][2] + sh[0][3];
+        stats[2 * n + 1] = sh[1][0] + sh[1][1] + sh[1][2] + sh[1][3];
+    }
+}
+
+bool fdec1_gram_supported(const LowRankDesc& d) {
+    return d.S && d.Wt && d.w_ld >= G_CI && d.w_ld % 8 == 0 && d.Ci == G_CI && d.Co == G_CO && d.Hs == G_HS &&
+           d.Hk == G_HK && d.z_bf16 && d.Zs && d.bias && d.stats && d.W >= 1 && d.P >= 1 && d.NI >= 1 &&
+           d.NI % d.P == 0 && d.Hd > G_HS && d.Hd < 65536;
+}
+
+int64_t fdec1_gram_floats(int64_t NI) { return NI * G_ITEM; }
+int64_t fdec1_gram_q_doubles() { return 4 * (G_NX * G_NX + G_NX); }
+
+static int g_blocks() {
+    static int n = 0;
+    if (n == 0) {
+        int dev = 0, cus = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < G_NG)
+            cus = 256;
+        n = cus;                                   // one workgroup per CU
+    }
+    return n;
+}
+
+int fdec1_gram_launch(const LowRankDesc& d, float* gram, double* gq, hipStream_t s) {
+    if (!fdec1_gram_supported(d) || !gram || !gq) return -1;
+    HIP_CHECK_RET(hipMemsetAsync(gram, 0, (size_t)fdec1_gram_floats(d.NI) * sizeof(float), s));
+    {
+        KScope ks(s);
+        if (ks.on()) ks.begin("fdec1_gram_q_kernel", 0.0, (double)fdec1_gram_q_doubles() * 8.0);
+        const int ne = (int)fdec1_gram_q_doubles();
+        hipLaunchKernelGGL(fdec1_gram_q_kernel, dim3((ne + 255) / 256), dim3(256), 0, s, gq, d.Hd);
+        HIP_CHECK_RET(hipGetLastError());
+    }
+    {
+        KScope ks(s);
+        if (ks.on()) {
+            // algorithmic: S (read once), Zs (once per segment), the Gram rows (written once per item); flops: the
+            // 8-tap Z GEMM + the Gram blocks (20 per class)
+            const double rows = (double)d.NI * G_HS * d.W;
+            const double by = rows * G_CI * 2.0 + (double)(d.NI / d.P) * G_HK * d.W * 8.0 * G_CO * 2.0 +
+                              (double)d.NI * G_ITEM * 4.0;
+            const double fl = 2.0 * rows * G_CI * 8 * G_CO + 2.0 * (double)d.NI * d.W * G_CO * 4 * 20 * 256;
+            ks.begin("fdec1_gram_kernel", fl, by);
+        }
+        hipLaunchKernelGGL(fdec1_gram_kernel, dim3(g_blocks()), dim3(G_THREADS), 0, s, d, gram);
+        HIP_CHECK_RET(hipGetLastError());
+    }
+    {
+        KScope ks(s);
+        if (ks.on()) ks.begin("fdec1_gram_final_kernel", 0.0, (double)d.NI * G_ITEM * 4.0);
+        hipLaunchKernelGGL(fdec1_gram_final_kernel, dim3(d.NI), dim3(256), 0, s, gram, gq, d.bias, d.stats, d.Hd, d.W);
+        HIP_CHECK_RET(hipGetLastError());
+    }
+    return 0;
+}
+
+}  // namespace athd

@@ -357,9 +357,10 @@ __global__ __launch_bounds__(256) void fdec_lr_merge3_kernel(const LowRankDesc d
     const LrThread th = lr_thread(d);
     if (!th.active) return;
     constexpr int NT = 4;
-    const int N8 = 8 * d.Co;
-    const int64_t rp = (int64_t)d.W * N8;
-    const bf16_t* zb = (const bf16_t*)d.Z + (int64_t)th.item * d.Hs * rp + (int64_t)th.w * N8 + th.c;
+    const int N8 = 8 * d.Co, NZ = d.z_taps * d.Co;      // Zs rows: 8 taps; Z rows: 8 taps or taps 0, 3, 4, 7 only
+    const int64_t rp = (int64_t)d.W * N8, rpz = (int64_t)d.W * NZ;
+    const bool z4 = d.z_taps == 4;
+    const bf16_t* zb = (const bf16_t*)d.Z + (int64_t)th.item * d.Hs * rpz + (int64_t)th.w * NZ + th.c;
     const bf16_t* sb = (const bf16_t*)d.Zs + (int64_t)th.seg * d.Hk * rp + (int64_t)th.w * N8 + th.c;
     float mean, rstd;
     gn_params(d.stats, th.item, 4LL * d.Hd * d.W * d.Co, mean, rstd);
@@ -371,9 +372,11 @@ __global__ __launch_bounds__(256) void fdec_lr_merge3_kernel(const LowRankDesc d
     bf2_t* op = (bf2_t*)((bf16_t*)d.out + (int64_t)th.item * d.Hd * d.W * d.Co + (int64_t)th.w * d.Co + th.c);
     const int64_t ostep = (int64_t)d.W * d.Co / 2;        // bf2 elements between output rows
 
-    auto ldrow = [&](const bf16_t* p, int row, uint32_t (&r)[NT]) {
+    auto ldrow = [&](const bf16_t* p, int row, uint32_t (&r)[NT], bool compact) {
 #pragma unroll
-        for (int t = 0; t < NT; ++t) r[t] = *reinterpret_cast<const uint32_t*>(p + (int64_t)row * rp + tap_of<NT>(t) * d.Co);
+        for (int t = 0; t < NT; ++t)
+            r[t] = *reinterpret_cast<const uint32_t*>(p + (int64_t)row * (compact ? rpz : rp) +
+                                                      (compact ? t : tap_of<NT>(t)) * d.Co);
     };
     f2 zhi[NT], zdr[NT], shi[NT], sdr[NT], base[NT];
     uint32_t zpf[NT], spf[NT];
@@ -381,10 +384,10 @@ __global__ __launch_bounds__(256) void fdec_lr_merge3_kernel(const LowRankDesc d
     int zr = (s0.zk >> 8) & 0xFF, kr = s0.zk >> 24;
     {
         uint32_t za[NT], ka[NT];
-        ldrow(zb, s0.zk & 0xFF, za);
-        ldrow(zb, zr, zpf);
-        ldrow(sb, (s0.zk >> 16) & 0xFF, ka);
-        ldrow(sb, kr, spf);
+        ldrow(zb, s0.zk & 0xFF, za, z4);
+        ldrow(zb, zr, zpf, z4);
+        ldrow(sb, (s0.zk >> 16) & 0xFF, ka, false);
+        ldrow(sb, kr, spf, false);
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
             const f2 a = bf2u(za[t]), b = bf2u(zpf[t]);
@@ -396,8 +399,8 @@ __global__ __launch_bounds__(256) void fdec_lr_merge3_kernel(const LowRankDesc d
             base[t] = a + ka2 + ((t == 1 || t == 2) ? bias : f2{});
         }
     }
-    ldrow(zb, min(zr + 1, d.Hs - 1), zpf);
-    ldrow(sb, min(kr + 1, d.Hk - 1), spf);
+    ldrow(zb, min(zr + 1, d.Hs - 1), zpf, z4);
+    ldrow(sb, min(kr + 1, d.Hk - 1), spf, false);
     // skip2 rows of output row 0 (step 1's entry), then the next one prefetched
     const LrStep s1e = lr_step(d.steps, 1);
     int jr = (int)(s1e.jj >> 16);
@@ -421,7 +424,7 @@ __global__ __launch_bounds__(256) void fdec_lr_merge3_kernel(const LowRankDesc d
                 zhi[t] = nb;
             }
             zr = min(zr + 1, d.Hs - 1);
-            ldrow(zb, min(zr + 1, d.Hs - 1), zpf);
+            ldrow(zb, min(zr + 1, d.Hs - 1), zpf, z4);
         }
         if (st.flags & 2u) {
 #pragma unroll
@@ -432,7 +435,7 @@ __global__ __launch_bounds__(256) void fdec_lr_merge3_kernel(const LowRankDesc d
                 shi[t] = nb;
             }
             kr = min(kr + 1, d.Hk - 1);
-            ldrow(sb, min(kr + 1, d.Hk - 1), spf);
+            ldrow(sb, min(kr + 1, d.Hk - 1), spf, false);
         }
 #pragma unroll
         for (int t = 0; t < NT; ++t) T[t] = pfma(splat(st.lz), zdr[t], pfma(splat(st.lk), sdr[t], base[t]));
@@ -573,7 +576,7 @@ static bool lr_ok(const LowRankDesc& d) {
 }
 
 int fdec_lr_stats_launch(const LowRankDesc& d, hipStream_t s) {
-    if (!lr_ok(d)) return -1;
+    if (!lr_ok(d) || d.z_taps != 8) return -1;
     const dim3 grid((unsigned)((d.W * (d.Co / 2) + 255) / 256), (unsigned)d.NI);
     KScope ks(s);
     if (ks.on()) {
@@ -599,7 +602,7 @@ static bool merge3(const LowRankDesc& d) {
 
 int fdec_lr_merge_launch(const LowRankDesc& d, hipStream_t s) {
     if (!lr_ok(d) || !d.gn_w || !d.gn_b || !d.skip || !d.out || d.C_skip < d.Co || d.C_skip % 2 != 0 ||
-        d.H_skip <= 0)
+        d.H_skip <= 0 || (d.z_taps != 8 && !(d.z_taps == 4 && merge3(d))))
         return -1;
     const dim3 grid((unsigned)((d.W * (d.Co / 2) + 255) / 256), (unsigned)d.NI);
     KScope ks(s);

@@ -87,6 +87,8 @@ struct Bufs {
                                       // chunk c + 1's decoder writes the other one
     float* ola_part;    // boundary partial sums of the fused iSTFT (spectral.hip)
     LrStep* lrsteps;    // level-1 low-rank decoder step table (fdec_lr.hip)
+    float* gram;        // level-1 statistics Gram blocks / quadratic forms (fdec1f.hip, bf16 mode)
+    double* gramq;
     void *S, *Z, *Zs;   // freq level 1 re-associated (fdec_lr.hip): per-tap products of the 32 / 8 source rows
     mutable float* xt2 = nullptr;   // time_out(time decoder) of the last decode chunk: D (fused tail) or G (ragged T)
 };
@@ -178,6 +180,8 @@ size_t plan(Arena& ar, const Dims& d, Bufs& b, bool actbf) {
     if (d.chunks > 1) b.FO2 = ar.take<float>(NI * Ts * Ts * 2);
     b.ola_part = ar.take<float>(istft_ola_part_floats(NI, (int)Ts));
     b.lrsteps = ar.take<LrStep>(Ts + 1);
+    b.gram = actbf ? ar.take<float>(fdec1_gram_floats(NI)) : nullptr;
+    b.gramq = actbf ? ar.take<double>(fdec1_gram_q_doubles()) : nullptr;
     return ar.off;
 }
 
@@ -244,6 +248,13 @@ bool serial_branches(const Run& r) {
         env = (e && *e && *e != '0') ? 1 : 0;
     }
     return env == 1 || r.c->prof != nullptr;
+}
+
+// ATHD_FDEC1_FUSED=0: the unfused level-1 frequency decoder (Z stored by a GEMM, fdec_lr.hip's two passes) instead
+// of fdec1f.hip; read at every forward (A/B and parity runs switch it between calls)
+bool fdec1_fused_enabled() {
+    const char* e = std::getenv("ATHD_FDEC1_FUSED");
+    return !(e && *e == '0');
 }
 
 // (created by athd_finalize: a forward creates no HIP objects, so it can be graph-captured from the first call)
@@ -753,20 +764,30 @@ void decode_chunk(Run& r, const Dims& d, const Bufs& b, int64_t s0, int64_t Bc, 
         gz.A = r.actbf ? b.S : (const void*)b.G; gz.a_bf16 = ab; gz.nb = NI; gz.H_in = 32; gz.W = (int)Ts; gz.C_in = w1.cin; gz.a_ld = w1.cin;
         gz.H_out = 32; gz.Wp = w1.taps.w; gz.N = w1.taps.N; gz.K = w1.taps.K; gz.Kp = w1.taps.Kp;
         gz.C = b.Z; gz.c_bf16 = ab; gz.H_out_total = 32; gz.ldo = w1.taps.N;
-        r.gemm(gz, "fdec1.z");
-        GemmDesc gs = gz;
-        gs.A = sv[3]; gs.a_bf16 = ab; gs.nb = (int)Bc; gs.H_in = 8; gs.H_out = 8; gs.H_out_total = 8; gs.a_ld = 384;
-        gs.C = b.Zs;
-        r.gemm(gs, "fdec1.zs");
         LowRankDesc lr;
-        r.check(fdec_lr_steps_launch(b.lrsteps, (int)Ts, 32, 8, 32, r.s), "fdec_lr_steps");
         lr.steps = b.lrsteps;
         lr.Z = b.Z; lr.Zs = b.Zs; lr.z_bf16 = ab; lr.Hs = 32; lr.Hk = 8; lr.Hd = (int)Ts; lr.W = (int)Ts;
         lr.Co = w1.cout; lr.P = P; lr.NI = NI; lr.bias = w1.bias; lr.stats = r.stats(NI);
         lr.gn_w = w1.gnw; lr.gn_b = w1.gnb; lr.fast_gelu = ab;
         lr.skip = sv[2]; lr.skip_bf16 = ab; lr.H_skip = 32; lr.C_skip = 192;
         lr.out = b.D; lr.out_bf16 = ab;
-        r.check(fdec_lr_stats_launch(lr, r.s), "fdec_lr_stats");
+        lr.S = gz.A; lr.Wt = w1.taps.w; lr.w_ld = w1.taps.Kp; lr.Ci = w1.cin;
+        // bf16 mode: the statistics from Gram matrices of Z tiles computed in LDS (fdec1f.hip), so the stored Z is
+        // only the merge pass's taps 0, 3, 4, 7
+        const bool gram = fdec1_fused_enabled() && b.gram && w1.taps4.w && fdec1_gram_supported(lr);
+        if (gram) {
+            gz.Wp = w1.taps4.w; gz.N = w1.taps4.N; gz.K = w1.taps4.K; gz.Kp = w1.taps4.Kp; gz.ldo = w1.taps4.N;
+            lr.z_taps = 4;
+        }
+        r.gemm(gz, gram ? "fdec1.z4" : "fdec1.z");
+        GemmDesc gs = gz;
+        gs.A = sv[3]; gs.a_bf16 = ab; gs.nb = (int)Bc; gs.H_in = 8; gs.H_out = 8; gs.H_out_total = 8; gs.a_ld = 384;
+        gs.Wp = w1.taps.w; gs.N = w1.taps.N; gs.K = w1.taps.K; gs.Kp = w1.taps.Kp; gs.ldo = w1.taps.N;
+        gs.C = b.Zs;
+        r.gemm(gs, "fdec1.zs");
+        r.check(fdec_lr_steps_launch(b.lrsteps, (int)Ts, 32, 8, 32, r.s), "fdec_lr_steps");
+        if (gram) r.check(fdec1_gram_launch(lr, b.gram, b.gramq, r.s), "fdec1_gram");
+        else r.check(fdec_lr_stats_launch(lr, r.s), "fdec_lr_stats");
         r.check(fdec_lr_merge_launch(lr, r.s), "fdec_lr_merge");
         // levels 1..3: Tspec -> 4 Tspec rows; the /4 bilinear resize reads only rows 4d+1, 4d+2
         const int skH[3] = {32, 128, 512};

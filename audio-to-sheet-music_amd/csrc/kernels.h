@@ -102,16 +102,27 @@ struct LrStep {
 struct LowRankDesc {
     const LrStep* steps = nullptr;                // Hd + 1 entries (fdec_lr_steps_launch)
     const void* Z = nullptr; const void* Zs = nullptr; int z_bf16 = 0;
+    int z_taps = 8;                               // Z row layout: all 8 taps, or 4 = taps 0, 3, 4, 7 (merge pass only)
     int Hs = 32, Hk = 8, Hd = 0, W = 0, Co = 0, P = 1, NI = 0;
     const float* bias = nullptr;                  // ConvT bias [Co]
     double* stats = nullptr;                      // per item {sum, sumsq} over the 4*Hd ConvT rows
     const float* gn_w = nullptr; const float* gn_b = nullptr; int fast_gelu = 0;
     const void* skip = nullptr; int skip_bf16 = 0; int H_skip = 0; int C_skip = 0;
     void* out = nullptr; int out_bf16 = 0;        // [NI][Hd][W][Co]
+    // fused passes (fdec1f.hip): the GEMM operands of Z instead of Z itself
+    const void* S = nullptr;                      // bf16 [NI][Hs][W][Ci]
+    const void* Wt = nullptr; int w_ld = 0;       // bf16 tap weights [8 Co][w_ld] (row k Co + c)
+    int Ci = 0;
 };
 int fdec_lr_steps_launch(LrStep* steps, int Hd, int Hs, int Hk, int H_skip, hipStream_t s);
 int fdec_lr_stats_launch(const LowRankDesc& d, hipStream_t s);
 int fdec_lr_merge_launch(const LowRankDesc& d, hipStream_t s);
+// fdec1f.hip: the statistics pass as Gram matrices of Z tiles computed in LDS (bf16 mode, Co = 96, Ci = 192, Hs = 32,
+// Hk = 8, Hd > 32); gram: fdec1_gram_floats(NI) floats, gq: fdec1_gram_q_doubles() doubles of workspace
+bool fdec1_gram_supported(const LowRankDesc& d);
+int64_t fdec1_gram_floats(int64_t NI);
+int64_t fdec1_gram_q_doubles();
+int fdec1_gram_launch(const LowRankDesc& d, float* gram, double* gq, hipStream_t s);
 // fenc_row.hip: a whole narrow frequency-encoder level (conv + GELU + DConv + rewrite GLU) per (b, f) row, bf16 mode
 constexpr int FR_MT_MAX = 17;        // T <= 272 positions (16-position tiles)
 struct FencRowDesc {

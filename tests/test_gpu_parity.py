@@ -188,6 +188,29 @@ def test_forward_prompts_matches_forward(models):
                 assert sdr_db(single.cpu().numpy(), multi[:, p].cpu().numpy()) >= 40.0, name
 
 
+@pytest.mark.parametrize("T", [264600, 33297, 50000])
+def test_fdec1_fused_matches_unfused(models, monkeypatch, T):
+    """The level-1 frequency decoder's GroupNorm statistics as quadratic forms of per-item Gram matrices of Z
+    (fdec1f.hip: Z tiles computed on the matrix cores into LDS, never stored; the merge pass reads a 4-tap Z) ==
+    the unfused path (8-tap Z stored by a GEMM, fdec_lr_stats3_kernel's sweep; ATHD_FDEC1_FUSED=0), bf16 model,
+    3 segments x 4 prompts (segment / prompt item mapping of the skip-projection rows).  T = 264600: Tspec = 259,
+    the bench shape (33 w blocks of 8, the last one 3 columns wide); 33297: Tspec = 33, the smallest Tspec the
+    Gram pass takes; 50000: Tspec = 49.  The two differ in the MFMA accumulation order of Z (a bf16 rounding of Z
+    may flip) and in how {sum, sumsq} are accumulated (fp32 Gram blocks vs fp32 row sums, both folded in fp64)."""
+    from athd.synth import synthetic_batch
+    wav = torch.as_tensor(synthetic_batch(3, T, seed0=31)).cuda()
+    prompts = ["drums", "bass", "other", "vocals"]
+    m = models["bf16"]
+    monkeypatch.setenv("ATHD_FDEC1_FUSED", "0")
+    ref = m.forward_prompts(wav, prompts).cpu().numpy()
+    monkeypatch.setenv("ATHD_FDEC1_FUSED", "1")
+    out = m.forward_prompts(wav, prompts).cpu().numpy()
+    assert np.isfinite(out).all()
+    s = min(sdr_db(ref[b, p], out[b, p]) for b in range(3) for p in range(4))
+    _report(f"fdec1_fused_T{T}", {"sdr_db_min_vs_unfused": s})
+    assert s >= 60.0, s
+
+
 def test_batch_independence(models):
     """Each segment of a batch is computed independently (per-sample normalisation, no cross-sample state)."""
     from athd.synth import synthetic_batch
