@@ -426,12 +426,6 @@ int athd_finalize(athd_ctx* c) {
                         for (int ci = 0; ci < dw.cin; ++ci)
                             tk[((size_t)k * dw.cout + co) * dw.cin + ci] = w[((size_t)ci * dw.cout + co) * 8 + k];
                 dw.taps = c->up_gemm(tk, 8 * dw.cout, dw.cin, {});
-                std::vector<float> tk4((size_t)4 * dw.cout * dw.cin);
-                static const int K4[4] = {0, 3, 4, 7};
-                for (int t = 0; t < 4; ++t)
-                    std::copy_n(tk.begin() + (size_t)K4[t] * dw.cout * dw.cin, (size_t)dw.cout * dw.cin,
-                                tk4.begin() + (size_t)t * dw.cout * dw.cin);
-                dw.taps4 = c->up_gemm(tk4, 4 * dw.cout, dw.cin, {});
                 dw.bias = c->up_f32(b);
             }
             if (i < 3) {

@@ -57,7 +57,6 @@ struct DecW {
     uint16_t* ct4w = nullptr;   // level 2, bf16 mode: [rho * cout + co][2 cin] = the residue pair's two rows (convt4.hip)
     float* ct4b = nullptr;      //   and the bias [cout]
     GemmW taps;             // freq level 1 only: every tap as its own column block, N = 8*cout, K = cin (fdec_lr.hip)
-    GemmW taps4;            // ... taps 0, 3, 4, 7 only (N = 4*cout): the merge pass's Z when fdec1f.hip takes the statistics
     float* bias = nullptr;  // freq level 1 only: ConvT bias [cout]
     float *gnw = nullptr, *gnb = nullptr;
 };

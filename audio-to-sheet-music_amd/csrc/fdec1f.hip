@@ -14,7 +14,8 @@
 // Gram matrix over (w, c): matrix-core work on the Z tile while it is in LDS.  So this pass computes Z tile by tile
 // (MFMA, into LDS, never to HBM), accumulates the 4 classes' 80 x 80 Gram blocks in MFMA accumulators across the
 // tiles of an item, flushes them per item with fp32 atomics, and fdec1_gram_final_kernel forms {sum, sumsq}.  It
-// replaces the 8-tap Z store + fdec_lr_stats3_kernel's sweep (VALU-bound); the merge pass reads a 4-tap Z.
+// replaces the 8-tap Z GEMM + fdec_lr_stats3_kernel's sweep (VALU-bound); it also stores the 4-tap Z (taps 0, 3, 4, 7)
+// the merge pass reads, from the same LDS tiles.
 //
 // Tile = (item n, 8 consecutive w columns, channel group of 16), all 32 rows j of S:
 //   Z GEMM   rows R = 8 j + wl (256; A = S[n][j][w0 + wl][0..191]), cols t * 16 + c (8 taps x 16 channels, K = 192);
@@ -125,6 +126,7 @@ __global__ __launch_bounds__(G_THREADS, 1) void fdec1_gram_kernel(const LowRankD
     const bf16_t* const S = (const bf16_t*)d.S;
     const bf16_t* const Wt = (const bf16_t*)d.Wt;
     const bf16_t* const Zs = (const bf16_t*)d.Zs;
+    bf16_t* const z4 = (bf16_t*)d.z4;
 
     // ---- weights of this channel group -> LDS (column t * 16 + c = weight row t * 96 + c0 + c) ----
     for (int idx = tid; idx < 128 * 24; idx += G_THREADS) {
@@ -255,6 +257,20 @@ __global__ __launch_bounds__(G_THREADS, 1) void fdec1_gram_kernel(const LowRankD
             load_s(t + 1);
             load_zs(t + 1);
         }
+        // the merge pass's Z (taps 0, 3, 4, 7) from the tile in LDS, [n][j][w][4][96] (after the prefetch loads, so
+        // that waiting for those does not wait for these stores): 2048 pieces of 16 B, four per thread
+        if (z4) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int p = tid + k * G_THREADS;
+                const int ti = p >> 9, j = (p >> 4) & 31, wl = (p >> 1) & 7, hf = p & 1;
+                const int tp = ti == 0 ? 0 : ti == 1 ? 3 : ti == 2 ? 4 : 7;
+                if (w0 + wl < W) {
+                    const uint4 v = *reinterpret_cast<const uint4*>(zt + swz(tp * 32 + j, wl * 2 + hf));
+                    *reinterpret_cast<uint4*>(z4 + ((((int64_t)n * G_HS + j) * W + w0 + wl) * 4 + ti) * G_CO + c0 + hf * 8) = v;
+                }
+            }
+        }
         // 3. Gram blocks of class gq over this tile's K = (wl, c): X row block ri = 16 consecutive LDS rows starting
         //    at a multiple of 16, so the swizzle key of its row l & 15 is l & 15
         auto gram_tile = [&](auto H) {             // H: this wave's half of the class blocks (compile time)
@@ -363,7 +379,7 @@ int fdec1_gram_launch(const LowRankDesc& d, float* gram, double* gq, hipStream_t
             // 8-tap Z GEMM + the Gram blocks (20 per class)
             const double rows = (double)d.NI * G_HS * d.W;
             const double by = rows * G_CI * 2.0 + (double)(d.NI / d.P) * G_HK * d.W * 8.0 * G_CO * 2.0 +
-                              (double)d.NI * G_ITEM * 4.0;
+                              (double)d.NI * G_ITEM * 4.0 + (d.z4 ? rows * 4.0 * G_CO * 2.0 : 0.0);
             const double fl = 2.0 * rows * G_CI * 8 * G_CO + 2.0 * (double)d.NI * d.W * G_CO * 4 * 20 * 256;
             ks.begin("fdec1_gram_kernel", fl, by);
         }

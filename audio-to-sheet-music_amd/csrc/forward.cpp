@@ -772,14 +772,15 @@ void decode_chunk(Run& r, const Dims& d, const Bufs& b, int64_t s0, int64_t Bc, 
         lr.skip = sv[2]; lr.skip_bf16 = ab; lr.H_skip = 32; lr.C_skip = 192;
         lr.out = b.D; lr.out_bf16 = ab;
         lr.S = gz.A; lr.Wt = w1.taps.w; lr.w_ld = w1.taps.Kp; lr.Ci = w1.cin;
-        // bf16 mode: the statistics from Gram matrices of Z tiles computed in LDS (fdec1f.hip), so the stored Z is
-        // only the merge pass's taps 0, 3, 4, 7
-        const bool gram = fdec1_fused_enabled() && b.gram && w1.taps4.w && fdec1_gram_supported(lr);
+        // bf16 mode: the statistics from Gram matrices of Z tiles computed in LDS (fdec1f.hip), which also stores
+        // the merge pass's taps 0, 3, 4, 7 of Z (no Z GEMM)
+        const bool gram = fdec1_fused_enabled() && b.gram && fdec1_gram_supported(lr);
         if (gram) {
-            gz.Wp = w1.taps4.w; gz.N = w1.taps4.N; gz.K = w1.taps4.K; gz.Kp = w1.taps4.Kp; gz.ldo = w1.taps4.N;
             lr.z_taps = 4;
+            lr.z4 = b.Z;                            // written by fdec1_gram_kernel
+        } else {
+            r.gemm(gz, "fdec1.z");
         }
-        r.gemm(gz, gram ? "fdec1.z4" : "fdec1.z");
         GemmDesc gs = gz;
         gs.A = sv[3]; gs.a_bf16 = ab; gs.nb = (int)Bc; gs.H_in = 8; gs.H_out = 8; gs.H_out_total = 8; gs.a_ld = 384;
         gs.Wp = w1.taps.w; gs.N = w1.taps.N; gs.K = w1.taps.K; gs.Kp = w1.taps.Kp; gs.ldo = w1.taps.N;

@@ -113,6 +113,7 @@ struct LowRankDesc {
     const void* S = nullptr;                      // bf16 [NI][Hs][W][Ci]
     const void* Wt = nullptr; int w_ld = 0;       // bf16 tap weights [8 Co][w_ld] (row k Co + c)
     int Ci = 0;
+    void* z4 = nullptr;                           // fdec1_gram_kernel also writes the merge pass's 4-tap Z here (bf16)
 };
 int fdec_lr_steps_launch(LrStep* steps, int Hd, int Hs, int Hk, int H_skip, hipStream_t s);
 int fdec_lr_stats_launch(const LowRankDesc& d, hipStream_t s);
