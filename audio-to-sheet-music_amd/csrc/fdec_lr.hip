@@ -360,7 +360,9 @@ __global__ __launch_bounds__(256) void fdec_lr_merge3_kernel(const LowRankDesc d
     const int N8 = 8 * d.Co, NZ = d.z_taps * d.Co;      // Zs rows: 8 taps; Z rows: 8 taps or taps 0, 3, 4, 7 only
     const int64_t rp = (int64_t)d.W * N8, rpz = (int64_t)d.W * NZ;
     const bool z4 = d.z_taps == 4;
-    const bf16_t* zb = (const bf16_t*)d.Z + (int64_t)th.item * d.Hs * rpz + (int64_t)th.w * NZ + th.c;
+    // 4-tap Z (fdec1f.hip): [item][j][w][channel group of 16][tap][16]: 128 B per (w, group) for the Gram pass's stores
+    const bf16_t* zb = (const bf16_t*)d.Z + (int64_t)th.item * d.Hs * rpz + (int64_t)th.w * NZ +
+                       (z4 ? (th.c >> 4) * 64 + (th.c & 15) : th.c);
     const bf16_t* sb = (const bf16_t*)d.Zs + (int64_t)th.seg * d.Hk * rp + (int64_t)th.w * N8 + th.c;
     float mean, rstd;
     gn_params(d.stats, th.item, 4LL * d.Hd * d.W * d.Co, mean, rstd);
@@ -376,7 +378,7 @@ __global__ __launch_bounds__(256) void fdec_lr_merge3_kernel(const LowRankDesc d
 #pragma unroll
         for (int t = 0; t < NT; ++t)
             r[t] = *reinterpret_cast<const uint32_t*>(p + (int64_t)row * (compact ? rpz : rp) +
-                                                      (compact ? t : tap_of<NT>(t)) * d.Co);
+                                                      (compact ? t * 16 : tap_of<NT>(t) * d.Co));
     };
     f2 zhi[NT], zdr[NT], shi[NT], sdr[NT], base[NT];
     uint32_t zpf[NT], spf[NT];

@@ -102,7 +102,8 @@ struct LrStep {
 struct LowRankDesc {
     const LrStep* steps = nullptr;                // Hd + 1 entries (fdec_lr_steps_launch)
     const void* Z = nullptr; const void* Zs = nullptr; int z_bf16 = 0;
-    int z_taps = 8;                               // Z row layout: all 8 taps, or 4 = taps 0, 3, 4, 7 (merge pass only)
+    int z_taps = 8;                               // Z rows: [w][8 taps][Co], or 4 = taps 0, 3, 4, 7 as [w][Co / 16][4][16]
+                                                  // (merge pass only; written by fdec1_gram_kernel)
     int Hs = 32, Hk = 8, Hd = 0, W = 0, Co = 0, P = 1, NI = 0;
     const float* bias = nullptr;                  // ConvT bias [Co]
     double* stats = nullptr;                      // per item {sum, sumsq} over the 4*Hd ConvT rows
