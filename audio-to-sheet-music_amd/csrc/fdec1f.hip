@@ -138,16 +138,11 @@ __global__ __launch_bounds__(G_THREADS, 1) void fdec1_gram_kernel(const LowRankD
 
     // ---- Z GEMM operands: this wave's tile rows 32 wv .. +31 ----
     bf16x8_t sf[2][6];
-    auto load_s = [&](int64_t t) {
+    auto s_row = [&](int64_t t, int i) {          // this lane's S row of row block i of tile t
         const int n = (int)(t / NWB), w0 = (int)(t % NWB) * G_WB;
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int R = (2 * wv + i) * 16 + (lane & 15);
-            const int j = R >> 3, w = min(w0 + (R & 7), W - 1);
-            const bf16_t* p = S + (((int64_t)n * G_HS + j) * W + w) * G_CI + 8 * (lane >> 4);
-#pragma unroll
-            for (int ks = 0; ks < 6; ++ks) sf[i][ks] = *reinterpret_cast<const bf16x8_t*>(p + ks * 32);
-        }
+        const int R = (2 * wv + i) * 16 + (lane & 15);
+        const int j = R >> 3, w = min(w0 + (R & 7), W - 1);
+        return S + (((int64_t)n * G_HS + j) * W + w) * G_CI + 8 * (lane >> 4);
     };
     // Zs rows of a tile: 1024 pieces of 16 B (t, m, wl, half), two per thread
     uint4 zsr[2];
@@ -197,7 +192,12 @@ __global__ __launch_bounds__(G_THREADS, 1) void fdec1_gram_kernel(const LowRankD
 
     int n_cur = -1;
     if (t_beg < t_end) {
-        load_s(t_beg);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const bf16_t* p = s_row(t_beg, i);
+#pragma unroll
+            for (int ks = 0; ks < 6; ++ks) sf[i][ks] = *reinterpret_cast<const bf16x8_t*>(p + ks * 32);
+        }
         load_zs(t_beg);
     }
     __syncthreads();                               // weights visible
@@ -208,7 +208,11 @@ __global__ __launch_bounds__(G_THREADS, 1) void fdec1_gram_kernel(const LowRankD
             if (n_cur >= 0) flush(n_cur);
             n_cur = n;
         }
-        // 1. Z tile (fp32 accumulators)
+        // 1. Z tile (fp32 accumulators).  Each K-step's S fragments are reloaded with the NEXT tile's as soon as its
+        //    MFMAs have issued, so those loads have the rest of this tile (barriers, LDS stores, Gram) to arrive
+        //    without a second register set (the last tile reloads its own rows: harmless)
+        const bf16_t* const pn0 = s_row(t + 1 < t_end ? t + 1 : t, 0);
+        const bf16_t* const pn1 = s_row(t + 1 < t_end ? t + 1 : t, 1);
         f32x4_t acc[2][8];
 #pragma unroll
         for (int i = 0; i < 2; ++i)
@@ -225,6 +229,8 @@ __global__ __launch_bounds__(G_THREADS, 1) void fdec1_gram_kernel(const LowRankD
                 for (int i = 0; i < 2; ++i)
                     acc[i][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, sf[i][ks], acc[i][cb], 0, 0, 0);
             }
+            sf[0][ks] = *reinterpret_cast<const bf16x8_t*>(pn0 + ks * 32);
+            sf[1][ks] = *reinterpret_cast<const bf16x8_t*>(pn1 + ks * 32);
         }
         // 2. -> LDS as bf16 (the rounding of the stored Z of the unfused path), columns w >= W as zeros, once the
         //    previous tile's Gram reads are done
@@ -253,10 +259,7 @@ __global__ __launch_bounds__(G_THREADS, 1) void fdec1_gram_kernel(const LowRankD
             *reinterpret_cast<uint4*>(zsl + swz((tp & 3) * 16 + (tp >> 2) * 8 + m, wl * 2 + hf)) = v;
         }
         __syncthreads();
-        if (t + 1 < t_end) {
-            load_s(t + 1);
-            load_zs(t + 1);
-        }
+        if (t + 1 < t_end) load_zs(t + 1);
         // the merge pass's Z (taps 0, 3, 4, 7) from the tile in LDS as [n][j][w][group][4][16] (128 B per (j, w) of
         // this group: eight threads (tap, half) write one line), after the prefetch loads so that waiting for those
         // does not wait for these stores: 2048 pieces of 16 B, four per thread
