@@ -362,7 +362,10 @@ static int g_blocks() {
         if (hipGetDevice(&dev) != hipSuccess ||
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < G_NG)
             cus = 256;
-        n = cus;                                   // one workgroup per CU
+        // one workgroup per CU, a multiple of the 6 channel groups: the six workgroups L = 6q .. 6q + 5 (one XCD)
+        // then walk the same tile range together and read each S row from HBM once (with 256 the groups' ranges
+        // drifted apart: 1.72x the algorithmic bytes, PMC)
+        n = cus / G_NG * G_NG;
     }
     return n;
 }

@@ -1,6 +1,7 @@
 #!/bin/bash
 # Full GPU pass: parity tests, bench (with CPU baseline), kernel-trace profile at the bench config, HBM traffic from
 # two PMC passes, and a final bench line carrying the measured traffic.  Usage: tools/gpu_round.sh <tag>
+# (SKIP_PYTEST=1: no tests / default bench; SKIP_TRACE=1: no kernel traces - e.g. when tools/gpu_run.sh prof:<tag> ran)
 TAG=${1:-r01}
 O=gpurun_out
 mkdir -p $O
@@ -15,6 +16,7 @@ step bench
 timeout -k 10 600 python bench.py > $O/bench_full.log 2>&1 || { tail -20 $O/bench_full.log; exit 1; }
 tail -1 $O/bench_full.log
 fi
+if [ -z "$SKIP_TRACE" ]; then
 step kernel-trace
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$TAG -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-extras > $O/prof_$TAG.log 2>&1 || { tail -20 $O/prof_$TAG.log; exit 1; }
 tail -1 $O/prof_$TAG.log
@@ -22,6 +24,7 @@ python tools/timeline.py $O/prof_$TAG --last-steps 2 > $O/timeline_$TAG.txt 2>&1
 step kernel-trace-serial
 ATHD_SERIAL=1 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_${TAG}_serial -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-extras > $O/prof_${TAG}_serial.log 2>&1 || { tail -20 $O/prof_${TAG}_serial.log; exit 1; }
 tail -1 $O/prof_${TAG}_serial.log | cut -c1-200
+fi
 step pmc-fetch
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch_$TAG -o run -- python bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-extras > $O/pmc_fetch_$TAG.log 2>&1 || { tail -20 $O/pmc_fetch_$TAG.log; exit 1; }
 step pmc-write
