@@ -261,13 +261,14 @@ __global__ __launch_bounds__(G_THREADS, 1) void fdec1_gram_kernel(const LowRankD
         __syncthreads();
         if (t + 1 < t_end) load_zs(t + 1);
         // the merge pass's Z (taps 0, 3, 4, 7) from the tile in LDS as [n][j][w][group][4][16] (128 B per (j, w) of
-        // this group: eight threads (tap, half) write one line), after the prefetch loads so that waiting for those
-        // does not wait for these stores: 2048 pieces of 16 B, four per thread
+        // this group, its 8 pieces in one store instruction; each 16-lane LDS read phase takes 16 chunks of one ZT
+        // row), after the prefetch loads so that waiting for those does not wait for these stores: 2048 pieces of
+        // 16 B, four per thread
         if (z4) {
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 const int p = tid + k * G_THREADS;
-                const int hf = p & 1, ti = (p >> 1) & 3, wl = (p >> 3) & 7, j = p >> 6;
+                const int hf = p & 1, wl = (p >> 1) & 7, ti = (p >> 4) & 3, j = p >> 6;   // 16 lanes: one row
                 const int tp = ti == 0 ? 0 : ti == 1 ? 3 : ti == 2 ? 4 : 7;
                 if (w0 + wl < W) {
                     const uint4 v = *reinterpret_cast<const uint4*>(zt + swz(tp * 32 + j, wl * 2 + hf));
