@@ -57,6 +57,20 @@ ATHD_DEV athd_f2v gelu_fast_pk(athd_f2v x) {
     const athd_f2v den = (athd_f2v){__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)} + (athd_f2v){1.0f, 1.0f};
     return x * (athd_f2v){__builtin_amdgcn_rcpf(den.x), __builtin_amdgcn_rcpf(den.y)};
 }
+// wa * gelu_fast(a) + wb * gelu_fast(b) on pairs with ONE reciprocal per element instead of two (the decoder merges
+// only need the resize's weighted sum of two rows' GELUs): (wa a (1 + eb) + wb b (1 + ea)) / ((1 + ea)(1 + eb)).  The
+// exp2 argument is clamped at 60 so that the product of the denominators stays finite (there the term is x 2^-60).
+ATHD_DEV athd_f2v gelu_fast_wsum_pk(athd_f2v wa, athd_f2v a, athd_f2v wb, athd_f2v b) {
+    constexpr float K0 = -1.5957691216057308f * 1.4426950408889634f, K1 = K0 * 0.044715f;
+    const athd_f2v lim = {60.0f, 60.0f}, one = {1.0f, 1.0f};
+    const athd_f2v ta = __builtin_elementwise_min(a * __builtin_elementwise_fma((athd_f2v){K1, K1}, a * a, (athd_f2v){K0, K0}), lim);
+    const athd_f2v tb = __builtin_elementwise_min(b * __builtin_elementwise_fma((athd_f2v){K1, K1}, b * b, (athd_f2v){K0, K0}), lim);
+    const athd_f2v da = (athd_f2v){__builtin_amdgcn_exp2f(ta.x), __builtin_amdgcn_exp2f(ta.y)} + one;
+    const athd_f2v db = (athd_f2v){__builtin_amdgcn_exp2f(tb.x), __builtin_amdgcn_exp2f(tb.y)} + one;
+    const athd_f2v den = da * db;
+    return __builtin_elementwise_fma(wa * a, db, wb * b * da) *
+           (athd_f2v){__builtin_amdgcn_rcpf(den.x), __builtin_amdgcn_rcpf(den.y)};
+}
 ATHD_DEV float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
 // bf16-mode sigmoid: v_exp_f32 + v_rcp_f32 (~1 ulp each; 4 instructions vs ~25 for expf and an IEEE divide).  The
 // f32 parity mode keeps sigmoidf_.

@@ -406,11 +406,10 @@ __global__ __launch_bounds__(256) void fdec_tail_kernel(const DecLastDesc d, int
             const athd_f2v l0 = {li.l0, li.l0}, l1 = {li.l1, li.l1}, k0 = {lj.l0, lj.l0}, k1 = {lj.l1, lj.l1};
 #pragma unroll
             for (int sp = 0; sp < 6; ++sp) {
-                const athd_f2v va = gelu_fast_pk(__builtin_elementwise_fma(r.get2(0, sp), ga2[sp], gc2[sp]));
-                const athd_f2v vb = gelu_fast_pk(__builtin_elementwise_fma(r.get2(1, sp), ga2[sp], gc2[sp]));
                 const athd_f2v sv = __builtin_elementwise_fma(k0, r.get2(2, sp), k1 * r.get2(3, sp)) *
                                     (athd_f2v){0.1f, 0.1f};
-                const athd_f2v x = __builtin_elementwise_fma(l0, va, l1 * vb) + sv;
+                const athd_f2v x = gelu_fast_wsum_pk(l0, __builtin_elementwise_fma(r.get2(0, sp), ga2[sp], gc2[sp]), l1,
+                                                     __builtin_elementwise_fma(r.get2(1, sp), ga2[sp], gc2[sp])) + sv;
                 acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wA[2 * sp], x.x, acc, 0, 0, 0);
                 acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wA[2 * sp + 1], x.y, acc, 0, 0, 0);
             }

@@ -60,23 +60,6 @@ ATHD_DEV f2 gelu2_pk(f2 x) {
     return x * (f2){__builtin_amdgcn_rcpf(den.x), __builtin_amdgcn_rcpf(den.y)};
 }
 
-// GELU(a) + GELU(b) on packed pairs with ONE reciprocal per element instead of two (the merge only needs the sum of
-// its two rows' GELUs): a / (1 + ea) + b / (1 + eb) = (a (1 + eb) + b (1 + ea)) / ((1 + ea)(1 + eb)), ea = exp2(ta).
-// The exponent is clamped at 60 so that the product of the denominators stays finite (at 2^60 the term is
-// x * 2^-60: the tanh-form GELU's own value there is below fp32 resolution of any other term).
-ATHD_DEV f2 gelu2_sum_pk(f2 a, f2 b) {
-    const f2 ta = __builtin_elementwise_min(a * pfma(splat(0.044715f * 1.5957691216057308f), a * a,
-                                                     splat(1.5957691216057308f)) * splat(-1.4426950408889634f),
-                                            splat(60.0f));
-    const f2 tb = __builtin_elementwise_min(b * pfma(splat(0.044715f * 1.5957691216057308f), b * b,
-                                                     splat(1.5957691216057308f)) * splat(-1.4426950408889634f),
-                                            splat(60.0f));
-    const f2 da = (f2){__builtin_amdgcn_exp2f(ta.x), __builtin_amdgcn_exp2f(ta.y)} + splat(1.0f);
-    const f2 db = (f2){__builtin_amdgcn_exp2f(tb.x), __builtin_amdgcn_exp2f(tb.y)} + splat(1.0f);
-    const f2 den = da * db;
-    return pfma(a, db, b * da) * (f2){__builtin_amdgcn_rcpf(den.x), __builtin_amdgcn_rcpf(den.y)};
-}
-
 // rows i0, i1 of a [H][W][8 Co] tap matrix at the thread's (w, channel pair): r0 = scale row[i0], dr = scale (row[i1] -
 // row[i0]) for the NT tap slots (tap_of); i0 / i1 are wave-uniform (scalar offsets)
 template <typename ZT, int NT>
@@ -469,8 +452,9 @@ __global__ __launch_bounds__(256) void fdec_lr_merge3_kernel(const LowRankDesc d
             jr = min(jr + 1, d.H_skip - 1);
             jpf = *reinterpret_cast<const uint32_t*>(kbp + (int64_t)min(jr + 1, d.H_skip - 1) * kp);
         }
-        const f2 gs = gelu2_sum_pk(pfma(y1, gsc, gb), pfma(y2, gsc, gb));
-        const f2 o = pfma(gs, splat(0.5f), pfma(splat(st.lj), kdr, kbase));
+        // the exact /4 resize: 0.5 GELU(y1) + 0.5 GELU(y2) with one reciprocal per element (common.h)
+        const f2 gs = gelu_fast_wsum_pk(splat(0.5f), pfma(y1, gsc, gb), splat(0.5f), pfma(y2, gsc, gb));
+        const f2 o = gs + pfma(splat(st.lj), kdr, kbase);
         op[(int64_t)dd * ostep] = __builtin_convertvector(o, bf2_t);
     };
     f2 cur3, cur4, cur7, prev7 = {};
