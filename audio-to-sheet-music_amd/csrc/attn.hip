@@ -669,18 +669,21 @@ __global__ __launch_bounds__(256, MINW) void attn32_kernel(const AttnDesc d) {
                 }
                 ATHD_A32_QK(-mrun);
             }
-            float ls[NKB];
+            // row sums on packed adds: 8 v_pk_add_f32 per key block instead of 16 adds
+            athd_f2v ls2[NKB];                                     // one chain per key block
 #pragma unroll
             for (int kb = 0; kb < NKB; ++kb) {
-                ls[kb] = 0.f;
+                ls2[kb] = (athd_f2v){0.f, 0.f};
 #pragma unroll
-                for (int i = 0; i < 16; ++i) {
+                for (int i = 0; i < 16; i += 2) {
                     sc[kb][i] = __builtin_amdgcn_exp2f(sc[kb][i]);
-                    ls[kb] += sc[kb][i];
+                    sc[kb][i + 1] = __builtin_amdgcn_exp2f(sc[kb][i + 1]);
+                    ls2[kb] += (athd_f2v){sc[kb][i], sc[kb][i + 1]};
                 }
             }
 #pragma unroll
-            for (int kb = 0; kb < NKB; ++kb) lrun += ls[kb];
+            for (int kb = 1; kb < NKB; ++kb) ls2[0] += ls2[kb];
+            lrun += ls2[0].x + ls2[0].y;
             // ---- O^T += V^T P^T ----
             A32_PRIO(1);
 #pragma unroll
