@@ -107,6 +107,17 @@ __global__ __launch_bounds__(256) void fdec1_gram_q_kernel(double* gq, int Hd) {
     gq[e] = s;
 }
 
+#ifdef ATHD_GR_STAMP
+// measurement build only (-DATHD_GR_STAMP): per wave, s_memtime cycles summed over its tiles per phase (0 flush + Z
+// MFMA + the previous tile's 4-tap stores, 1 first barrier, 2 ZT / Zs stores + second barrier, 3 Zs prefetch, 4 Gram),
+// tile count, span ->
+// g_gr_stamp[block][wave][8]; read back with athd_gr_stamps
+__device__ uint64_t g_gr_stamp[1024 * 8 * 8];
+#define GR_MARK(k) do { const uint64_t now_ = __builtin_amdgcn_s_memtime(); ph_[k] += now_ - tp_; tp_ = now_; } while (0)
+#else
+#define GR_MARK(k) do { } while (0)
+#endif
+
 __global__ __launch_bounds__(G_THREADS, 1) void fdec1_gram_kernel(const LowRankDesc d, float* gram) {
     __shared__ __attribute__((aligned(16))) char smem[G_LDS];
     char* const bl = smem;                                    // weights
@@ -121,8 +132,8 @@ __global__ __launch_bounds__(G_THREADS, 1) void fdec1_gram_kernel(const LowRankD
     const int c0 = g * G_CG;
     const int W = d.W;
     const int NWB = (W + G_WB - 1) / G_WB;
-    const int64_t T = (int64_t)d.NI * NWB;
-    const int64_t t_beg = T * qi / Qg, t_end = T * (qi + 1) / Qg;
+    const int T = d.NI * NWB;                      // (< 2^31: fdec1_gram_supported)
+    const int t_beg = (int)((int64_t)T * qi / Qg), t_end = (int)((int64_t)T * (qi + 1) / Qg);
     const bf16_t* const S = (const bf16_t*)d.S;
     const bf16_t* const Wt = (const bf16_t*)d.Wt;
     const bf16_t* const Zs = (const bf16_t*)d.Zs;
@@ -138,16 +149,16 @@ __global__ __launch_bounds__(G_THREADS, 1) void fdec1_gram_kernel(const LowRankD
 
     // ---- Z GEMM operands: this wave's tile rows 32 wv .. +31 ----
     bf16x8_t sf[2][6];
-    auto s_row = [&](int64_t t, int i) {          // this lane's S row of row block i of tile t
-        const int n = (int)(t / NWB), w0 = (int)(t % NWB) * G_WB;
+    auto s_row = [&](int t, int i) {              // this lane's S row of row block i of tile t
+        const int n = t / NWB, w0 = (t % NWB) * G_WB;
         const int R = (2 * wv + i) * 16 + (lane & 15);
         const int j = R >> 3, w = min(w0 + (R & 7), W - 1);
         return S + (((int64_t)n * G_HS + j) * W + w) * G_CI + 8 * (lane >> 4);
     };
     // Zs rows of a tile: 1024 pieces of 16 B (t, m, wl, half), two per thread
     uint4 zsr[2];
-    auto load_zs = [&](int64_t t) {
-        const int n = (int)(t / NWB), w0 = (int)(t % NWB) * G_WB, seg = n / d.P;
+    auto load_zs = [&](int t) {
+        const int n = t / NWB, w0 = (t % NWB) * G_WB, seg = n / d.P;
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             const int p = tid * 2 + h;
@@ -201,9 +212,14 @@ __global__ __launch_bounds__(G_THREADS, 1) void fdec1_gram_kernel(const LowRankD
         load_zs(t_beg);
     }
     __syncthreads();                               // weights visible
+#ifdef ATHD_GR_STAMP
+    uint64_t ph_[5] = {0, 0, 0, 0, 0};
+    const uint64_t t0_ = __builtin_amdgcn_s_memtime();
+    uint64_t tp_ = t0_;
+#endif
 
-    for (int64_t t = t_beg; t < t_end; ++t) {
-        const int n = (int)(t / NWB), w0 = (int)(t % NWB) * G_WB;
+    for (int t = t_beg; t < t_end; ++t) {
+        const int n = t / NWB, w0 = (t % NWB) * G_WB;
         if (n != n_cur) {
             if (n_cur >= 0) flush(n_cur);
             n_cur = n;
@@ -234,7 +250,9 @@ __global__ __launch_bounds__(G_THREADS, 1) void fdec1_gram_kernel(const LowRankD
         }
         // 2. -> LDS as bf16 (the rounding of the stored Z of the unfused path), columns w >= W as zeros, once the
         //    previous tile's Gram reads are done
+        GR_MARK(0);
         __syncthreads();
+        GR_MARK(1);
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
             const int R = (2 * wv + i) * 16 + (lane & 15);
@@ -259,24 +277,9 @@ __global__ __launch_bounds__(G_THREADS, 1) void fdec1_gram_kernel(const LowRankD
             *reinterpret_cast<uint4*>(zsl + swz((tp & 3) * 16 + (tp >> 2) * 8 + m, wl * 2 + hf)) = v;
         }
         __syncthreads();
+        GR_MARK(2);
         if (t + 1 < t_end) load_zs(t + 1);
-        // the merge pass's Z (taps 0, 3, 4, 7) from the tile in LDS as [n][j][w][group][4][16] (128 B per (j, w) of
-        // this group, its 8 pieces in one store instruction; each 16-lane LDS read phase takes 16 chunks of one ZT
-        // row), after the prefetch loads so that waiting for those does not wait for these stores: 2048 pieces of
-        // 16 B, four per thread
-        if (z4) {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const int p = tid + k * G_THREADS;
-                const int hf = p & 1, wl = (p >> 1) & 7, ti = (p >> 4) & 3, j = p >> 6;   // 16 lanes: one row
-                const int tp = ti == 0 ? 0 : ti == 1 ? 3 : ti == 2 ? 4 : 7;
-                if (w0 + wl < W) {
-                    const uint4 v = *reinterpret_cast<const uint4*>(zt + swz(tp * 32 + j, wl * 2 + hf));
-                    *reinterpret_cast<uint4*>(z4 + (((int64_t)n * G_HS + j) * W + w0 + wl) * (4 * G_CO) + g * 64 + ti * 16 +
-                                              hf * 8) = v;
-                }
-            }
-        }
+        GR_MARK(3);
         // 3. Gram blocks of class gq over this tile's K = (wl, c): X row block ri = 16 consecutive LDS rows starting
         //    at a multiple of 16, so the swizzle key of its row l & 15 is l & 15
         auto gram_tile = [&](auto H) {             // H: this wave's half of the class blocks (compile time)
@@ -301,8 +304,36 @@ __global__ __launch_bounds__(G_THREADS, 1) void fdec1_gram_kernel(const LowRankD
         };
         if (gh == 0) gram_tile(std::integral_constant<int, 0>{});
         else gram_tile(std::integral_constant<int, 1>{});
+        GR_MARK(4);
+        // the merge pass's Z (taps 0, 3, 4, 7) from the tile in LDS as [n][j][w][group][4][16] (128 B per (j, w) of
+        // this group, its 8 pieces in one store instruction; each 16-lane LDS read phase takes 16 chunks of one ZT
+        // row), after the Gram MFMAs (issued earlier they queue behind the S / Zs prefetch loads and hold the Gram
+        // back) and after those loads, so that waiting for them does not wait for these stores: 2048 pieces of 16 B,
+        // four per thread
+        if (z4) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int p = tid + k * G_THREADS;
+                const int hf = p & 1, wl = (p >> 1) & 7, ti = (p >> 4) & 3, j = p >> 6;   // 16 lanes: one row
+                const int tp = ti == 0 ? 0 : ti == 1 ? 3 : ti == 2 ? 4 : 7;
+                if (w0 + wl < W) {
+                    const uint4 v = *reinterpret_cast<const uint4*>(zt + swz(tp * 32 + j, wl * 2 + hf));
+                    *reinterpret_cast<uint4*>(z4 + (((int64_t)n * G_HS + j) * W + w0 + wl) * (4 * G_CO) + g * 64 + ti * 16 +
+                                              hf * 8) = v;
+                }
+            }
+        }
     }
     if (n_cur >= 0) flush(n_cur);
+#ifdef ATHD_GR_STAMP
+    if (lane == 0) {
+        uint64_t* o = g_gr_stamp + ((size_t)blockIdx.x * 8 + wv) * 8;
+        for (int k = 0; k < 5; ++k) o[k] = ph_[k];
+        o[5] = (uint64_t)(t_end - t_beg);
+        o[6] = tp_ - t0_;
+        o[7] = 1;
+    }
+#endif
 }
 
 // {sum, sumsq} of item n from its Gram blocks: one 256-thread block per item
@@ -347,10 +378,17 @@ __global__ __launch_bounds__(256) void fdec1_gram_final_kernel(const float* gram
     }
 }
 
+#ifdef ATHD_GR_STAMP
+extern "C" int athd_gr_stamps(void* host) {
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_gr_stamp), sizeof(uint64_t) * 1024 * 64, 0, hipMemcpyDeviceToHost);
+}
+#endif
+
 bool fdec1_gram_supported(const LowRankDesc& d) {
     return d.S && d.Wt && d.w_ld >= G_CI && d.w_ld % 8 == 0 && d.Ci == G_CI && d.Co == G_CO && d.Hs == G_HS &&
            d.Hk == G_HK && d.z_bf16 && d.Zs && d.bias && d.stats && d.W >= 1 && d.P >= 1 && d.NI >= 1 &&
-           d.NI % d.P == 0 && d.Hd > G_HS && d.Hd < 65536;
+           d.NI % d.P == 0 && d.Hd > G_HS && d.Hd < 65536 &&
+           (int64_t)d.NI * ((d.W + G_WB - 1) / G_WB) < (1LL << 31);
 }
 
 int64_t fdec1_gram_floats(int64_t NI) { return NI * G_ITEM; }
