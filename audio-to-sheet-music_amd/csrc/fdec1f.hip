@@ -149,25 +149,27 @@ __global__ __launch_bounds__(G_THREADS, 1) void fdec1_gram_kernel(const LowRankD
 
     // ---- Z GEMM operands: this wave's tile rows 32 wv .. +31 ----
     bf16x8_t sf[2][6];
+    // a tile's first column: the last tile of an item is shifted left to end at W (W >= G_WB), so that every load and
+    // store of a tile is in range and unconditional (no per-lane branches: the wait counters stay exact across the
+    // loop); its columns the previous tile already covered are masked out of the Gram operands and their Z stored
+    // again (the same values)
+    auto w_first = [&](int t) { return min((t % NWB) * G_WB, W - G_WB); };
     auto s_row = [&](int t, int i) {              // this lane's S row of row block i of tile t
-        const int n = t / NWB, w0 = (t % NWB) * G_WB;
+        const int n = t / NWB, w0 = w_first(t);
         const int R = (2 * wv + i) * 16 + (lane & 15);
-        const int j = R >> 3, w = min(w0 + (R & 7), W - 1);
+        const int j = R >> 3, w = w0 + (R & 7);
         return S + (((int64_t)n * G_HS + j) * W + w) * G_CI + 8 * (lane >> 4);
     };
-    // Zs rows of a tile: 1024 pieces of 16 B (t, m, wl, half), two per thread
-    uint4 zsr[2];
+    // Zs rows of a tile: 1024 pieces of 16 B (t, m, wl, half), two per thread (adjacent halves: the second is the
+    // first + 16 B).  Two named registers, not an array: a private array is promoted to LDS by the compiler
+    uint4 zsr0, zsr1;
+    const int zs_tm = tid >> 3, zs_wl = tid & 7;
     auto load_zs = [&](int t) {
-        const int n = t / NWB, w0 = (t % NWB) * G_WB, seg = n / d.P;
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const int p = tid * 2 + h;
-            const int tm = p >> 4, wl = (p >> 1) & 7, hf = p & 1;
-            const int tp = tm >> 3, m = tm & 7;
-            const int w = min(w0 + wl, W - 1);
-            zsr[h] = *reinterpret_cast<const uint4*>(Zs + (((int64_t)seg * G_HK + m) * W + w) * (8 * G_CO) + tp * G_CO +
-                                                     c0 + hf * 8);
-        }
+        const int n = t / NWB, w = w_first(t) + zs_wl, seg = n / d.P;
+        const int tp = zs_tm >> 3, m = zs_tm & 7;
+        const bf16_t* p = Zs + (((int64_t)seg * G_HK + m) * W + w) * (8 * G_CO) + tp * G_CO + c0;
+        zsr0 = *reinterpret_cast<const uint4*>(p);
+        zsr1 = *reinterpret_cast<const uint4*>(p + 8);
     };
 
     // ---- Gram roles ----
@@ -210,6 +212,12 @@ __global__ __launch_bounds__(G_THREADS, 1) void fdec1_gram_kernel(const LowRankD
             for (int ks = 0; ks < 6; ++ks) sf[i][ks] = *reinterpret_cast<const bf16x8_t*>(p + ks * 32);
         }
         load_zs(t_beg);
+        // four stores of zeros to a scratch slot after the Gram rows, in the place of the loop's four 4-tap stores:
+        // the compiler's wait counts at the loop head are the minimum over its entry and back edge, so without them
+        // every tile's first S fragments wait for two of the previous tile's stores to complete
+        f32x4_t* const pad = reinterpret_cast<f32x4_t*>(gram + (int64_t)d.NI * G_ITEM) + tid;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) pad[k * G_THREADS] = f32x4_t{0.f, 0.f, 0.f, 0.f};
     }
     __syncthreads();                               // weights visible
 #ifdef ATHD_GR_STAMP
@@ -219,7 +227,7 @@ __global__ __launch_bounds__(G_THREADS, 1) void fdec1_gram_kernel(const LowRankD
 #endif
 
     for (int t = t_beg; t < t_end; ++t) {
-        const int n = t / NWB, w0 = (t % NWB) * G_WB;
+        const int n = t / NWB, w0 = w_first(t), skip = (t % NWB) * G_WB - w0;   // skip: columns already covered
         if (n != n_cur) {
             if (n_cur >= 0) flush(n_cur);
             n_cur = n;
@@ -248,8 +256,8 @@ __global__ __launch_bounds__(G_THREADS, 1) void fdec1_gram_kernel(const LowRankD
             sf[0][ks] = *reinterpret_cast<const bf16x8_t*>(pn0 + ks * 32);
             sf[1][ks] = *reinterpret_cast<const bf16x8_t*>(pn1 + ks * 32);
         }
-        // 2. -> LDS as bf16 (the rounding of the stored Z of the unfused path), columns w >= W as zeros, once the
-        //    previous tile's Gram reads are done
+        // 2. -> LDS as bf16 (the rounding of the stored Z of the unfused path), once the previous tile's Gram reads
+        //    are done
         GR_MARK(0);
         __syncthreads();
         GR_MARK(1);
@@ -257,28 +265,23 @@ __global__ __launch_bounds__(G_THREADS, 1) void fdec1_gram_kernel(const LowRankD
         for (int i = 0; i < 2; ++i) {
             const int R = (2 * wv + i) * 16 + (lane & 15);
             const int j = R >> 3, wl = R & 7;
-            const uint32_t keep = w0 + wl < W ? ~0u : 0u;       // (a mask, not a branch per store)
             const int c = 4 * (lane >> 4);
 #pragma unroll
             for (int cb = 0; cb < 8; ++cb) {
                 uint2 v;
-                v.x = pack2bf(acc[i][cb][0], acc[i][cb][1]) & keep;
-                v.y = pack2bf(acc[i][cb][2], acc[i][cb][3]) & keep;
+                v.x = pack2bf(acc[i][cb][0], acc[i][cb][1]);
+                v.y = pack2bf(acc[i][cb][2], acc[i][cb][3]);
                 *reinterpret_cast<uint2*>(zt + swz(cb * 32 + j, wl * 2 + (c >> 3)) + ((c >> 2) & 1) * 8) = v;
             }
         }
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const int p = tid * 2 + h;
-            const int tm = p >> 4, wl = (p >> 1) & 7, hf = p & 1;
-            const int tp = tm >> 3, m = tm & 7;
-            const uint32_t keep = w0 + wl < W ? ~0u : 0u;
-            const uint4 v = {zsr[h].x & keep, zsr[h].y & keep, zsr[h].z & keep, zsr[h].w & keep};
-            *reinterpret_cast<uint4*>(zsl + swz((tp & 3) * 16 + (tp >> 2) * 8 + m, wl * 2 + hf)) = v;
+        {
+            const int tp = zs_tm >> 3, m = zs_tm & 7, row = (tp & 3) * 16 + (tp >> 2) * 8 + m;
+            *reinterpret_cast<uint4*>(zsl + swz(row, zs_wl * 2)) = zsr0;
+            *reinterpret_cast<uint4*>(zsl + swz(row, zs_wl * 2 + 1)) = zsr1;
         }
         __syncthreads();
         GR_MARK(2);
-        if (t + 1 < t_end) load_zs(t + 1);
+        load_zs(t + 1 < t_end ? t + 1 : t);
         GR_MARK(3);
         // 3. Gram blocks of class gq over this tile's K = (wl, c): X row block ri = 16 consecutive LDS rows starting
         //    at a multiple of 16, so the swizzle key of its row l & 15 is l & 15
@@ -288,12 +291,14 @@ __global__ __launch_bounds__(G_THREADS, 1) void fdec1_gram_kernel(const LowRankD
 #pragma unroll 1
             for (int ks = 0; ks < 4; ++ks) {
                 const int chunk = ks * 4 + (lane >> 4), row = lane & 15;
+                const bool kill = (chunk >> 1) < skip;            // K = (wl, c): a column the previous tile covered
                 bf16x8_t xf[5];
 #pragma unroll
                 for (int ri = 0; ri < 5; ++ri) {
                     const char* base =
                         ri < 4 ? zt + ((ri < 2 ? gq : gq + 4) * 32 + (ri & 1) * 16) * 256 : zsl + gq * 16 * 256;
                     xf[ri] = *reinterpret_cast<const bf16x8_t*>(base + row * 256 + ((chunk ^ row) << 4));
+                    if (kill) xf[ri] = bf16x8_t{};
                 }
 #pragma unroll
                 for (int b = 0; b < nbh; ++b) {
@@ -310,18 +315,14 @@ __global__ __launch_bounds__(G_THREADS, 1) void fdec1_gram_kernel(const LowRankD
         // row), after the Gram MFMAs (issued earlier they queue behind the S / Zs prefetch loads and hold the Gram
         // back) and after those loads, so that waiting for them does not wait for these stores: 2048 pieces of 16 B,
         // four per thread
-        if (z4) {
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const int p = tid + k * G_THREADS;
-                const int hf = p & 1, wl = (p >> 1) & 7, ti = (p >> 4) & 3, j = p >> 6;   // 16 lanes: one row
-                const int tp = ti == 0 ? 0 : ti == 1 ? 3 : ti == 2 ? 4 : 7;
-                if (w0 + wl < W) {
-                    const uint4 v = *reinterpret_cast<const uint4*>(zt + swz(tp * 32 + j, wl * 2 + hf));
-                    *reinterpret_cast<uint4*>(z4 + (((int64_t)n * G_HS + j) * W + w0 + wl) * (4 * G_CO) + g * 64 + ti * 16 +
-                                              hf * 8) = v;
-                }
-            }
+        for (int k = 0; k < 4; ++k) {
+            const int p = tid + k * G_THREADS;
+            const int hf = p & 1, wl = (p >> 1) & 7, ti = (p >> 4) & 3, j = p >> 6;   // 16 lanes: one row
+            const int tp = (ti >> 1) * 4 + (ti & 1) * 3;                                // taps 0, 3, 4, 7
+            const uint4 v = *reinterpret_cast<const uint4*>(zt + swz(tp * 32 + j, wl * 2 + hf));
+            *reinterpret_cast<uint4*>(z4 + (((int64_t)n * G_HS + j) * W + w0 + wl) * (4 * G_CO) + g * 64 + ti * 16 +
+                                      hf * 8) = v;
         }
     }
     if (n_cur >= 0) flush(n_cur);
@@ -387,11 +388,11 @@ extern "C" int athd_gr_stamps(void* host) {
 bool fdec1_gram_supported(const LowRankDesc& d) {
     return d.S && d.Wt && d.w_ld >= G_CI && d.w_ld % 8 == 0 && d.Ci == G_CI && d.Co == G_CO && d.Hs == G_HS &&
            d.Hk == G_HK && d.z_bf16 && d.Zs && d.bias && d.stats && d.W >= 1 && d.P >= 1 && d.NI >= 1 &&
-           d.NI % d.P == 0 && d.Hd > G_HS && d.Hd < 65536 &&
+           d.NI % d.P == 0 && d.Hd > G_HS && d.Hd < 65536 && d.W >= G_WB &&
            (int64_t)d.NI * ((d.W + G_WB - 1) / G_WB) < (1LL << 31);
 }
 
-int64_t fdec1_gram_floats(int64_t NI) { return NI * G_ITEM; }
+int64_t fdec1_gram_floats(int64_t NI) { return NI * G_ITEM + G_THREADS * 16; }   // + the prologue's scratch slot
 int64_t fdec1_gram_q_doubles() { return 4 * (G_NX * G_NX + G_NX); }
 
 static int g_blocks() {
@@ -410,7 +411,7 @@ static int g_blocks() {
 }
 
 int fdec1_gram_launch(const LowRankDesc& d, float* gram, double* gq, hipStream_t s) {
-    if (!fdec1_gram_supported(d) || !gram || !gq) return -1;
+    if (!fdec1_gram_supported(d) || !gram || !gq || !d.z4 || d.z_taps != 4) return -1;
     HIP_CHECK_RET(hipMemsetAsync(gram, 0, (size_t)fdec1_gram_floats(d.NI) * sizeof(float), s));
     {
         KScope ks(s);
