@@ -24,7 +24,7 @@ for step in "$@"; do
       K=(); [ -n "$a1" ] && K=(-k "$a1")
       timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -rA -p no:cacheprovider --timeout 120 --timeout-method thread "${K[@]}" > $O/pytest_$n.log 2>&1
       rc=$?; grep -E "passed|failed" $O/pytest_$n.log | tail -2
-      [ $rc -ne 0 ] && { grep -E "Error|assert|FAILED" $O/pytest_$n.log | head -20; exit $rc; } ;;
+      if [ $rc -ne 0 ]; then grep -E "Error|assert|FAILED" $O/pytest_$n.log | head -20; exit $rc; fi ;;
     bench)
       timeout -k 10 400 python bench.py --no-cpu-baseline ${a1//,/ } > $O/bench_$n.log 2>&1 || { tail -20 $O/bench_$n.log; exit 1; }
       tail -2 $O/bench_$n.log | cut -c1-700 ;;
@@ -38,7 +38,7 @@ for step in "$@"; do
       timeout -k 10 900 bash tools/gpu_ab_lib.sh "$a1" "$a2" "${a3:-2}" || exit 1 ;;
     kbench)
       KB_LIB=${a2:-libkbench.so} timeout -k 10 600 python tools/kbench.py $a1 > $O/kbench_$n.log 2>&1; rc=$?
-      grep -v amdgpu.ids $O/kbench_$n.log | cut -c1-300; [ $rc -ne 0 ] && exit $rc ;;
+      grep -v amdgpu.ids $O/kbench_$n.log | cut -c1-300; if [ $rc -ne 0 ]; then exit $rc; fi ;;
     prof)
       timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$a1 -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-extras > $O/prof_$a1.log 2>&1 || { tail -20 $O/prof_$a1.log; exit 1; }
       python tools/timeline.py $O/prof_$a1 --last-steps 2 > $O/timeline_$a1.txt 2>&1; head -20 $O/timeline_$a1.txt
@@ -52,3 +52,4 @@ for step in "$@"; do
     *) echo "unknown step $name"; exit 2 ;;
   esac
 done
+exit 0
