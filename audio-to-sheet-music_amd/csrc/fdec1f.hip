@@ -23,7 +23,7 @@
 //   LDS      ZT [t * 32 + j][wl * 16 + c] (bf16; the Gram's X rows), Zs [q * 16 + (t >> 2) * 8 + m][wl * 16 + c]
 //   Gram     per class q: X row blocks R0..R3 (Z, 16 rows each) and R4 (Zs), K = (wl, c) = 128; blocks (ri <= ci)
 //            of X X^T plus X times a one-hot channel matrix (the per-channel sums); wave wv: class wv >> 1, half
-//            wv & 1 of the class's 20 blocks (9 / 11), accumulated across the item's tiles.
+//            wv & 1 of the class's 20 blocks (10 each), accumulated across the item's tiles.
 // Each persistent workgroup owns one channel group (its 128 weight rows stay in LDS, 48 KB) and walks a contiguous
 // run of (item, w block) tiles.  LDS chunks (16 B) of every [row][256 B] array are XOR-swizzled by (row & 15):
 // the MFMA-layout stores (ds_write_b64, 32 lanes) and the operand reads (ds_read_b128, 16 rows) both cover the 64
@@ -58,14 +58,14 @@ ATHD_DEV int g_xcd_remap(int i, int n) {
     return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i / 8;
 }
 
-// the Gram blocks of a wave: half 0 of a class takes rows R0 (columns 0..5) and R3 (3..5), half 1 rows R1 (1..5),
-// R2 (2..5), R4 (4, 5); column 5 = the one-hot channel matrix
-constexpr int G_NBLK = 11;
+// the Gram blocks of a wave (10 each): half 0 of a class takes rows R0 (columns 0..5), R3 (3..5) and R4 (5), half 1
+// rows R1 (1..5), R2 (2..5) and R4 (4); column 5 = the one-hot channel matrix
+constexpr int G_NBLK = 10;
 ATHD_HD constexpr int blk_r(int h, int b) {
-    return h == 0 ? (b < 6 ? 0 : b < 9 ? 3 : -1) : (b < 5 ? 1 : b < 9 ? 2 : 4);
+    return h == 0 ? (b < 6 ? 0 : b < 9 ? 3 : 4) : (b < 5 ? 1 : b < 9 ? 2 : 4);
 }
 ATHD_HD constexpr int blk_c(int h, int b) {
-    return h == 0 ? (b < 6 ? b : b < 9 ? b - 3 : -1) : (b < 5 ? b + 1 : b < 9 ? b - 3 : b - 5);
+    return h == 0 ? (b < 6 ? b : b < 9 ? b - 3 : 5) : (b < 5 ? b + 1 : b < 9 ? b - 3 : 4);
 }
 
 // resize-lerp coefficient of x_q entry a in ConvT output row 4v + rho (rho = (q + 2) % 4): the row is
@@ -174,7 +174,6 @@ __global__ __launch_bounds__(G_THREADS, 1) void fdec1_gram_kernel(const LowRankD
 
     // ---- Gram roles ----
     const int gq = wv >> 1, gh = wv & 1;
-    const int nb = gh == 0 ? 9 : 11;
     // one-hot channel matrix as the B operand: lane n = lane & 15 (channel), k = 8 (lane >> 4) + e is channel
     // 8 ((lane >> 4) & 1) + e of the K index (wl, c)
     bf16x8_t onehot;
@@ -190,7 +189,7 @@ __global__ __launch_bounds__(G_THREADS, 1) void fdec1_gram_kernel(const LowRankD
         float* const gb = gram + ((int64_t)n * 4 + gq) * G_NX * G_NB;
 #pragma unroll
         for (int b = 0; b < G_NBLK; ++b) {
-            if (b < nb) {
+            {
                 const int ri = blk_r(gh, b), ci = blk_c(gh, b);
                 const int col = ci < 5 ? ci * 16 + (lane & 15) : G_NX + c0 + (lane & 15);
 #pragma unroll
@@ -287,7 +286,7 @@ __global__ __launch_bounds__(G_THREADS, 1) void fdec1_gram_kernel(const LowRankD
         //    at a multiple of 16, so the swizzle key of its row l & 15 is l & 15
         auto gram_tile = [&](auto H) {             // H: this wave's half of the class blocks (compile time)
             constexpr int h = decltype(H)::value;
-            constexpr int nbh = h == 0 ? 9 : 11;
+            constexpr int nbh = G_NBLK;
 #pragma unroll 1
             for (int ks = 0; ks < 4; ++ks) {
                 const int chunk = ks * 4 + (lane >> 4), row = lane & 15;
