@@ -17,9 +17,10 @@ separated waveforms to rank `dst`:
         track bit for bit;
       - "benchmark" (benchmark.py:155-204, weighted OLA, athd_overlap_add_weighted): the partial spans carry the
         unnormalised sum and the weight sum, added in rank order the same way, then normalised once on `dst`.
-  * `separate_dataset`: a whole MUSDB18 split (athd.musdb.MusDBTracks): every window of every track is a unit of
-    `separate_segments`; `dst` reassembles each track from its rows (weighted overlap-add), scores it against the
-    reference stems and writes evaluation_results.json (benchmark.py:742-781, :853-888).
+  * `separate_dataset`: a whole MUSDB18 split (athd.musdb.MusDBTracks) in track-aligned groups of a bounded number
+    of windows: every window of a group is a unit of `separate_segments`; `dst` gathers the group into one reused
+    buffer, reassembles each track from its rows (weighted overlap-add), scores it against the reference stems and
+    writes evaluation_results.json (benchmark.py:742-781, :853-888).
 Block, batch and span sizes follow from (N, W) or the window plan, so no size exchange is needed.  Before its first
 exchange each runner makes one barrier per process group, so a lazily created NCCL communicator (no `device_id`
 in init_process_group) exists on every rank even when some rank's block is empty.
@@ -175,68 +176,102 @@ def dataset_windows(tracks, units: Sequence[Tuple[int, int]], chunk_len: int, ov
     return out.pin_memory() if torch.cuda.is_available() else out
 
 
+def dataset_groups(lengths: Sequence[int], chunk_len: int, overlap_frames: int, cap: int) -> List[Tuple[int, int]]:
+    """Track-aligned gather groups of a split: consecutive track ranges [t0, t1) whose windows total <= cap (a track
+    with more than `cap` windows forms a group of its own).  Every rank derives the same list from the lengths."""
+    hop = chunk_len - overlap_frames
+    groups, t0, n = [], 0, 0
+    for ti, L in enumerate(lengths):
+        w = -(-int(L) // hop)
+        if ti > t0 and n + w > cap:
+            groups.append((t0, ti))
+            t0, n = ti, 0
+        n += w
+    if len(lengths) > t0:
+        groups.append((t0, len(lengths)))
+    return groups
+
+
 @torch.no_grad()
 def separate_dataset(model, tracks, stems: Sequence[str] = STEMS, segment_seconds: float = 6.0,
                      overlap: float = 1.5, sample_rate: int = 44100, dst: int = 0, group=None, max_batch: int = 64,
                      output_dir=None, forward_fn: Optional[Callable] = None, ola_fn: Optional[Callable] = None,
                      metric_fn: Optional[Callable] = None, model_name: str = "AudioTextHTDemucs (Ours)",
-                     keep_estimates: bool = False, log: Optional[Callable[[str], None]] = print):
+                     keep_estimates: bool = False, log: Optional[Callable[[str], None]] = print,
+                     group_windows: Optional[int] = None, stats: Optional[dict] = None):
     """A whole MUSDB18 split through the sharded runner -> per-track stems and metrics on rank `dst`.
 
     The reference evaluates a split track by track, one 6 s window and one stem at a time
     (test_inference.py:75-88 -> dataloader.py:56-84 -> benchmark.py:742-781, OurModel._chunked_inference
-    :155-204).  Here every window of every track is one unit of `separate_segments`: the units are sharded in
-    contiguous blocks over the ranks (each rank reads only the tracks its block touches), each rank separates its
-    block into all stems (encode once, decode len(stems) times, batches of `max_batch` windows spanning tracks) and
-    the separated windows are gathered point to point into one (N, S, 2, chunk) tensor on `dst`.  `dst` then
-    reassembles every track from its rows with the weighted overlap-add of benchmark.py:177-202
-    (athd_overlap_add_weighted), computes SDR / SI-SDR per stem against the track's reference stems
-    (benchmark.py:655-688) and, with `output_dir`, writes `evaluation_results.json` (save_results,
-    benchmark.py:853-888).
+    :155-204).  Here the split is cut into track-aligned groups of at most `group_windows` windows (dataset_groups;
+    default 4 x world x max_batch, at least the longest track's windows).  Per group, every window is one unit of
+    `separate_segments`: the units are sharded in contiguous blocks over the ranks (each rank reads only the tracks
+    its block touches), each rank separates its block into all stems (encode once, decode len(stems) times, batches
+    of `max_batch` windows spanning tracks) and the separated windows are gathered point to point into ONE reused
+    (group_windows, S, 2, chunk) buffer on `dst`.  `dst` then reassembles every track of the group from its rows with
+    the weighted overlap-add of benchmark.py:177-202 (athd_overlap_add_weighted), computes SDR / SI-SDR per stem
+    against the track's reference stems (benchmark.py:655-688) before the buffer is reused, and, with `output_dir`,
+    writes `evaluation_results.json` (save_results, benchmark.py:853-888).  So the gather buffer on `dst` (8.47 MB
+    per window at 4 stems x 6 s) and each rank's pinned host block are bounded by `group_windows`, whatever the
+    split's size (configs[3]: ~6k windows would otherwise be ~51 GB on dst).
 
     overlap=1.5 is benchmark.py's protocol (OurModel's default, the one behind eval_results/*.json); overlap=0
     separates the dataloader's non-overlapping segments (dataloader.py:67,104-121) and concatenates them.
     Returns (results, estimates) on dst - estimates {track name: (S, 2, L)} only with keep_estimates - and None
     elsewhere.  forward_fn / ola_fn(win, L, chunk, ov) / metric_fn(est, ref) -> (sdr, sisdr) default to the native
-    path; tests substitute CPU stand-ins to run the exchange on gloo."""
+    path; tests substitute CPU stand-ins to run the exchange on gloo.  `stats` (optional dict) receives
+    {"groups", "buffer_rows"}."""
     from .benchmark import track_result, log_track, save_results
     if sorted(stems) != sorted(STEMS):
         raise ValueError(f"the evaluation needs every stem of {STEMS}, got {list(stems)}")
     world, rank = _world(group)
     chunk_len = int(sample_rate * segment_seconds)
     ov = int(overlap * sample_rate)
+    hop = chunk_len - ov
     lengths = tracks.lengths()
-    units = dataset_plan(lengths, chunk_len, ov)
-    N = len(units)
-    lo, hi = shard_range(N, world, rank)
-    block = dataset_windows(tracks, units[lo:hi], chunk_len, ov)
-    if forward_fn is None:
-        block_dev = model.device
-    else:
-        block_dev = block.device
-    out = None
-    if rank == dst:
-        out = torch.empty((N, len(stems), 2, chunk_len), dtype=torch.float32, device=block_dev)
-    out = separate_segments(model, block, stems, dst=dst, group=group, max_batch=max_batch, forward_fn=forward_fn,
-                            n_total=N, out=out)
-    if rank != dst:
-        return None
-    if ola_fn is None:
+    longest = max((-(-int(L) // hop) for L in lengths), default=0)
+    cap = max(group_windows if group_windows is not None else 4 * world * max_batch, longest)
+    groups = dataset_groups(lengths, chunk_len, ov, cap)
+    if ola_fn is None and rank == dst:
         from .benchmark import overlap_add_weighted
         ola_fn = lambda win, L, c, o: overlap_add_weighted(win, L, c, o)      # noqa: E731
+    buf = None
     results, estimates = [], {}
-    row = 0
-    for ti, L in enumerate(lengths):
-        n = -(-int(L) // (chunk_len - ov))                                     # this track's rows of `out`
-        est = ola_fn(out[row:row + n], int(L), chunk_len, ov)                  # (S, 2, L)
-        row += n
-        name, _, refs = tracks.track(ti)
-        r = track_result(name, model_name, {s: est[i] for i, s in enumerate(stems)}, refs, metric_fn)
-        results.append(r)
-        if keep_estimates:
-            estimates[name] = est
-        if log:
-            log_track(r, log)
+    for t0, t1 in groups:
+        units = dataset_plan(lengths[t0:t1], chunk_len, ov)
+        units = [(t0 + ti, k) for ti, k in units]
+        N = len(units)
+        lo, hi = shard_range(N, world, rank)
+        block = dataset_windows(tracks, units[lo:hi], chunk_len, ov)
+        out = None
+        if rank == dst:
+            if buf is None:
+                dev = model.device if forward_fn is None else block.device
+                rows = min(cap, sum(-(-int(L) // hop) for L in lengths))
+                buf = torch.empty((rows, len(stems), 2, chunk_len), dtype=torch.float32, device=dev)
+            out = buf[:N]
+        out = separate_segments(model, block, stems, dst=dst, group=group, max_batch=max_batch,
+                                forward_fn=forward_fn, n_total=N, out=out)
+        del block
+        if rank != dst:
+            continue
+        row = 0
+        for ti in range(t0, t1):
+            L = int(lengths[ti])
+            n = -(-L // hop)                                                    # this track's rows of the group
+            est = ola_fn(out[row:row + n], L, chunk_len, ov)                    # (S, 2, L)
+            row += n
+            name, _, refs = tracks.track(ti)
+            r = track_result(name, model_name, {s: est[i] for i, s in enumerate(stems)}, refs, metric_fn)
+            results.append(r)
+            if keep_estimates:
+                estimates[name] = est
+            if log:
+                log_track(r, log)
+    if stats is not None:
+        stats.update(groups=len(groups), buffer_rows=0 if buf is None else buf.shape[0])
+    if rank != dst:
+        return None
     if output_dir is not None:
         save_results({model_name: results}, output_dir)
     return results, estimates

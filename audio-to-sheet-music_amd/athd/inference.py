@@ -23,6 +23,7 @@ import torch
 
 from . import native
 from .model import AudioTextHTDemucs
+from .text import load_clap
 from .weights import STEMS
 
 
@@ -32,11 +33,19 @@ def load_model(checkpoint_path: str, device: str = "cuda", dtype: str = "bf16",
     code); `checkpoint["model_state_dict"]` is loaded non-strictly.  The pretrained htdemucs object of the reference
     is not needed: every `htdemucs.*` key the hot path uses is in the checkpoint, as the reference's own
     `load_state_dict` overwrites the pretrained values with them.  Prompt embeddings: `text_table` or `clap`/`tokenizer`
-    (see athd/text.py)."""
+    (see athd/text.py).  With neither given, CLAP and its tokenizer are built from `laion/clap-htsat-unfused` in the
+    local Hugging Face cache as the reference does (`:26-28`, `text.load_clap`, `local_files_only=True`), the
+    checkpoint's `clap.*` keys are loaded into it (`:34-35`), and the embeddings of the 4 stem prompts are computed
+    once and cached (the CLAP tower is frozen: its output depends on the prompt string only)."""
+    default_clap = text_table is None and clap is None
+    if default_clap:
+        clap, tokenizer = load_clap()
     ckpt = torch.load(checkpoint_path, map_location="cpu", weights_only=True)
     sd = ckpt["model_state_dict"] if isinstance(ckpt, dict) and "model_state_dict" in ckpt else ckpt
     model = AudioTextHTDemucs(None, clap, tokenizer, dtype=dtype, text_table=text_table)
     model.load_state_dict(sd, strict=False)
+    if default_clap:
+        model.embedder.rows(list(STEMS), len(STEMS))     # the 4 stem embeddings, cached in the prompt table
     model = model.to(device)
     model.eval()
     return model

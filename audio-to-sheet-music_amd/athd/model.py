@@ -56,17 +56,26 @@ class AudioTextHTDemucs:
 
     # ------------------------------------------------------------------ nn.Module-like surface
     def load_state_dict(self, state_dict, strict: bool = False):
-        """Reference key names; like `load_state_dict(strict=False)` unknown keys (clap.*, htdemucs.decoder.*)
-        are ignored.  Returns (missing_keys, unexpected_keys) restricted to the hot-path contract."""
+        """Reference key names; like `load_state_dict(strict=False)` unknown keys (htdemucs.decoder.*, ...) are
+        ignored.  `clap.*` keys are loaded into the attached CLAP model (non-strictly, as the reference's submodule)
+        when there is one, and ignored otherwise.  Returns (missing_keys, unexpected_keys) restricted to the hot-path
+        contract."""
         needed = {k for k, _, _ in hot_path_spec()}
         unexpected = []
+        clap_state = {}
         for k, v in state_dict.items():
             if k.startswith("module."):
                 k = k[len("module."):]        # DataParallel prefix (benchmark.py:398-404)
             if k in needed:
                 self._weights[k] = _to_numpy(v)
             else:
+                if k.startswith("clap."):     # the reference's self.clap submodule (ATHTDemucs_v2.py:165)
+                    clap_state[k[len("clap."):]] = v
                 unexpected.append(k)
+        if self.embedder.load_clap_state(clap_state):
+            loaded = set(self.embedder.clap.state_dict())
+            unexpected = [k for k in unexpected
+                          if not (k.startswith("clap.") and k[len("clap."):] in loaded)]
         missing = sorted(needed - set(self._weights))
         if strict and (missing or unexpected):
             raise RuntimeError(f"missing {missing[:5]}..., unexpected {unexpected[:5]}...")
@@ -191,6 +200,8 @@ class AudioTextHTDemucs:
         refreshes `wav` in place between replays; the prompt rows, the workspace and `out` stay bound to the graph.
         The graph owns its workspace (not the model's cached one), so replays may overlap eager calls on other streams;
         graphs replayed only in order on ONE stream may share a caller-given `workspace` (e.g. ping-pong outputs).
+        Memory: without `workspace` every captured graph holds a full `athd_workspace_bytes(B, T, P)` arena (≈ 49 GB
+        at B = 64, T = 264600, P = 4), so capturing k graphs costs k arenas.
         `wav` must already be a contiguous float32 (B, 2, T) tensor on the model's device (no copy is captured)."""
         if wav.dtype != torch.float32 or not wav.is_contiguous():
             raise ValueError("capture_prompts needs a contiguous float32 wav (B, 2, T)")

@@ -16,14 +16,58 @@ import torch
 from .weights import STEMS, synthetic_text_table
 
 
+CLAP_NAME = "laion/clap-htsat-unfused"     # test_inference.py:27-28
+
+
+def load_clap(name: str = CLAP_NAME):
+    """The reference's `ClapModel.from_pretrained(name)` + `AutoTokenizer.from_pretrained(name)`
+    (`test_inference.py:26-28`), from the local Hugging Face cache only (`local_files_only=True`: there is no
+    network on the target nodes).  Raises a RuntimeError naming the missing model and the `text_table=` alternative
+    when the cache lacks its files."""
+    try:
+        from transformers import AutoTokenizer, ClapModel
+    except ImportError as e:   # pragma: no cover - transformers is in the image
+        raise RuntimeError(f"CLAP '{name}' needs transformers ({e}); pass text_table={{prompt: 512-vector}} "
+                           f"instead") from e
+    try:
+        clap = ClapModel.from_pretrained(name, local_files_only=True)
+        tokenizer = AutoTokenizer.from_pretrained(name, local_files_only=True)
+    except (OSError, ValueError) as e:
+        raise RuntimeError(
+            f"CLAP model '{name}' is not in the local Hugging Face cache ({type(e).__name__}: {e}). The reference "
+            f"downloads it (test_inference.py:27-28); offline, either place its files in the cache (HF_HOME) or pass "
+            f"text_table={{prompt: 512-vector}} (e.g. precomputed ClapModel.get_text_features rows) or "
+            f"clap=/tokenizer=") from e
+    clap.eval()
+    for p in clap.parameters():          # frozen, as ATHTDemucs_v2.py:174-176
+        p.requires_grad = False
+    return clap, tokenizer
+
+
 class PromptEmbedder:
     def __init__(self, clap=None, tokenizer=None, table: Optional[Dict[str, np.ndarray]] = None):
         self.clap = clap
         self.tokenizer = tokenizer
         self.table: Dict[str, torch.Tensor] = {}
+        self._from_clap: set = set()      # table entries computed by the CLAP model (invalidated on weight loads)
         if table:
             for k, v in table.items():
                 self.table[k] = torch.as_tensor(np.asarray(v, dtype=np.float32)).reshape(-1)
+
+    def load_clap_state(self, state: Dict[str, torch.Tensor]):
+        """The `clap.*` part of a reference checkpoint, loaded into the CLAP model non-strictly as the reference's
+        `model.load_state_dict(..., strict=False)` does for its `self.clap` submodule (`test_inference.py:34-35`).
+        Embeddings computed with the previous weights are dropped.  Returns the number of tensors loaded."""
+        if not state or self.clap is None or not hasattr(self.clap, "load_state_dict"):
+            return 0
+        own = self.clap.state_dict() if hasattr(self.clap, "state_dict") else {}
+        sub = {k: v for k, v in state.items() if k in own}    # a shape mismatch raises, as in torch's strict=False
+        if sub:
+            self.clap.load_state_dict(sub, strict=False)
+            for p in self._from_clap:
+                self.table.pop(p, None)
+            self._from_clap.clear()
+        return len(sub)
 
     @classmethod
     def synthetic(cls, seed: int = 7) -> "PromptEmbedder":
@@ -57,6 +101,7 @@ class PromptEmbedder:
             emb = self._clap_embed(missing)
             for p, e in zip(missing, emb):
                 self.table[p] = e
+                self._from_clap.add(p)
         out = torch.stack([self.table[p] for p in prompts])
         if out.shape != (batch, TEXT_DIM):
             raise ValueError(f"prompt embeddings must be {TEXT_DIM}-d (text_dim, config.yaml:16), got "

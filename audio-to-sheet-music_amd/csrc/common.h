@@ -4,6 +4,21 @@
 #include <stdint.h>
 
 #define ATHD_DEV __device__ __forceinline__
+
+// CUs of the CURRENT device, cached per device id (a process may drive GPUs of different CU counts);
+// 256 (MI355X) if the query fails
+inline int device_cus() {
+    static int cache[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0) dev = 0;
+    int& c = cache[dev & 63];
+    if (c == 0) {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+        c = n;
+    }
+    return c;
+}
 #define ATHD_HD __host__ __device__ __forceinline__
 
 typedef __attribute__((ext_vector_type(8))) short bf16x8_t;   // 8 bf16 = one MFMA 16x16x32 operand fragment

@@ -274,13 +274,7 @@ int convt4_launch(const ConvT4Desc& d0, hipStream_t s) {
     d.fd_h = make_fastdiv((uint32_t)d.H);
     d.fd_hw = make_fastdiv((uint32_t)d.H * (uint32_t)d.W);
     d.M = (uint32_t)((int64_t)d.nb * d.H * d.W);
-    static int cus = 0;
-    if (cus == 0) {
-        int dev = 0;
-        (void)hipGetDevice(&dev);
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        if (cus <= 0) cus = 256;
-    }
+    const int cus = device_cus();
     // 2 row fragments per unit, 8 waves (2 per SIMD).  (1 fragment at 12 / 16 waves per workgroup measured slower.)
     if (d.keep) launch_ct4<true, 2, 8>(d, cus, s);
     else launch_ct4<false, 2, 8>(d, cus, s);

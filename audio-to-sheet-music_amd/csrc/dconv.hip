@@ -679,13 +679,7 @@ int dconv_conv3_launch(const uint16_t* x, const uint16_t* w, int kp, const float
     if (!dconv_conv3_supported(C, C / 8, kp, L) || M <= 0 || M >= (1LL << 31)) return -1;
     DcConv3 d;
     d.x = x; d.w = w; d.bias = bias; d.h = h; d.st = st; d.M = M; d.L = L; d.kp = kp; d.dil = dil;
-    static int cus = 0;
-    if (cus == 0) {
-        int dev = 0;
-        (void)hipGetDevice(&dev);
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        if (cus <= 0) cus = 256;
-    }
+    const int cus = device_cus();
     KScope ks(s);
     if (ks.on()) {
         const double H = C / 8;
@@ -724,13 +718,7 @@ int dconv_apply_launch(const uint16_t* hb, const uint16_t* w, int kp, const floa
         if (rwd->kp < (C + 31) / 32 * 32) return -1;
         d.rw = rwd->w; d.rkp = rwd->kp; d.rbias = rwd->bias; d.out = rwd->out; d.c4 = rwd->c4;
     }
-    static int cus = 0;
-    if (cus == 0) {
-        int dev = 0;
-        (void)hipGetDevice(&dev);
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        if (cus <= 0) cus = 256;
-    }
+    const int cus = device_cus();
     KScope ks(s);
     if (ks.on()) {
         const double H = C / 8;

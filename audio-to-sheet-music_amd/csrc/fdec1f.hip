@@ -395,18 +395,12 @@ int64_t fdec1_gram_floats(int64_t NI) { return NI * G_ITEM + G_THREADS * 16; }  
 int64_t fdec1_gram_q_doubles() { return 4 * (G_NX * G_NX + G_NX); }
 
 static int g_blocks() {
-    static int n = 0;
-    if (n == 0) {
-        int dev = 0, cus = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < G_NG)
-            cus = 256;
-        // one workgroup per CU, a multiple of the 6 channel groups: the six workgroups L = 6q .. 6q + 5 (one XCD)
-        // then walk the same tile range together and read each S row from HBM once (with 256 the groups' ranges
-        // drifted apart: 1.72x the algorithmic bytes, PMC)
-        n = cus / G_NG * G_NG;
-    }
-    return n;
+    // one workgroup per CU, a multiple of the 6 channel groups: the six workgroups L = 6q .. 6q + 5 (one XCD) then
+    // walk the same tile range together and read each S row from HBM once (with 256 the groups' ranges drifted apart:
+    // 1.72x the algorithmic bytes, PMC).  The current device's CU count (device_cus, per device id: ADVICE r04 #5)
+    int cus = device_cus();
+    if (cus < G_NG) cus = 256;
+    return cus / G_NG * G_NG;
 }
 
 int fdec1_gram_launch(const LowRankDesc& d, float* gram, double* gq, hipStream_t s) {

@@ -516,8 +516,10 @@ void encode(Run& r, const Dims& d, const Bufs& b, const float* wav) {
         l.x = x; l.nb = (int)B; l.N = N; l.C = 512; l.w = w; l.b = bb; l.out = out; l.out_bf16 = ab;
         if (pend && pend->st) {
             l.gn_stats = pend->st; l.gn_w = pend->w; l.gn_b = pend->b;
-            // (the residual epilogue takes it when a 256-row tile spans at most two batches: N >= 256 tokens)
-            if (lazy_gn && resgn && N >= 256) { l.gn_writeback = 0; *resgn = *pend; }
+            // (the residual epilogue takes it when a 256-row tile spans at most two batches: N >= 256 tokens; the
+            // LayerNorm pass has the register-only form only where ln_lazy_gn_ok holds)
+            l.out_bf16 = ab; l.out2 = out2;
+            if (lazy_gn && resgn && N >= 256 && ln_lazy_gn_ok(l)) { l.gn_writeback = 0; *resgn = *pend; }
             *pend = Pending();
         }
         l.w2 = w2; l.b2 = b2; l.out2 = out2;

@@ -296,14 +296,12 @@ bool gemm3_supported(const GemmDesc& d) {
 // rounded down to a multiple of 8 (XCD count) and capped at the M tile count.
 template <int BM, int BN, int WM, int WN, int ST, unsigned F>
 static unsigned resident_grid_x(int ntm, int ntn) {
-    static int resident = 0;
-    if (resident == 0) {
-        int per_cu = 0, cus = 0, dev = 0;
-        (void)hipGetDevice(&dev);
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    static int per_cu = 0;       // a property of the kernel; the CU count is the current device's
+    if (per_cu == 0) {
         (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, gemm3_kernel<BM, BN, WM, WN, ST, F>, WM * WN * 64, 0);
-        resident = per_cu > 0 && cus > 0 ? per_cu * cus : -1;
+        if (per_cu <= 0) per_cu = -1;
     }
+    const int resident = per_cu > 0 ? per_cu * device_cus() : -1;
     if (resident < 0) return (unsigned)ntm;
     int gx = resident / ntn / 8 * 8;
     if (gx < 8) gx = 8;

@@ -40,6 +40,15 @@ typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(1))) void gbl_void;
 
 constexpr int G5_SLOT = 16384;     // one half-tile slot: 128 rows x 64 bf16
+// The K-loop's VM-counter bookkeeping: every issueA / issueB issues exactly G5_PIECES LDS-DMA pieces,
+// each group makes G5_ISSUES_KTILE issue calls per K-tile (4 load sections), and the K-loop has no other global
+// loads or stores.  The steady-state wait keeps the pieces of the previous 4 load sections in flight: vmcnt of
+// G5_STEADY_VM.  Any change to the piece map or the staging schedule must keep these in step (the ATHD_G5_CHECK
+// debug build compares the counted history with the constant on every steady K-step).
+constexpr int G5_PIECES = 2;
+constexpr int G5_ISSUES_KTILE = 4;
+constexpr int G5_STEADY_VM = G5_PIECES * G5_ISSUES_KTILE;
+static_assert(G5_STEADY_VM == 8, "the steady-state s_waitcnt below is written as vmcnt(8)");
 
 ATHD_DEV void vm_wait_n(int n) {   // n = 0, 2, 4, 6, 8 (wave-uniform)
     if (n >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
@@ -140,7 +149,7 @@ __global__ __launch_bounds__(512) void gemm5_kernel(const GemmDesc d) {
         if constexpr (LIN) {
             const char* base = (const char*)d.A + (int64_t)kt * 128;      // wave-uniform
 #pragma unroll
-            for (int q = 0; q < 2; ++q)
+            for (int q = 0; q < G5_PIECES; ++q)
                 __builtin_amdgcn_global_load_lds((gbl_void*)(base + a_base[h][q]), (lds_void*)(dst + (wave + NW * q) * 1024),
                                                  16, 0, 0);
             return;
@@ -149,7 +158,7 @@ __global__ __launch_bounds__(512) void gemm5_kernel(const GemmDesc d) {
         const bool kok = k < d.K;
         const int tap = k / d.C_in, ci = k - tap * d.C_in;
 #pragma unroll
-        for (int q = 0; q < 2; ++q) {
+        for (int q = 0; q < G5_PIECES; ++q) {
             const int row = a_h0[h][q] + tap * d.dil;
             const bool ok = kok && row >= 0 && row < d.H_in;
             const char* src = ok ? (const char*)d.A + ((int64_t)a_base[h][q] + (int64_t)row * rowpitch + ci) * 2 : zero;
@@ -161,7 +170,7 @@ __global__ __launch_bounds__(512) void gemm5_kernel(const GemmDesc d) {
         char* dst = smem + ((kt & 1) * 4 + 2 + h) * G5_SLOT;
         const char* wb = (const char*)d.Wp + (int64_t)kt * 128 + (h ? b_h1 : 0u);
 #pragma unroll
-        for (int q = 0; q < 2; ++q)
+        for (int q = 0; q < G5_PIECES; ++q)
             __builtin_amdgcn_global_load_lds((gbl_void*)(wb + b_off[q]), (lds_void*)(dst + (wave + NW * q) * 1024), 16, 0, 0);
     };
 
@@ -232,8 +241,8 @@ __global__ __launch_bounds__(512) void gemm5_kernel(const GemmDesc d) {
             issueB(1, 0);
             issueB(1, 1);
             if (wr == 1) issueA(1, 1);
-            if (wr == 0) { hist[0] = 2; hist[1] = 4; }                 // u=-1: p3 B1, p2 A0 + B0
-            else { hist[0] = 2; hist[1] = 2; hist[2] = 4; }            // u=-1: p3 A1, p2 B1, p1 A0 + B0
+            if (wr == 0) { hist[0] = G5_PIECES; hist[1] = 2 * G5_PIECES; }                 // u=-1: p3 B1, p2 A0 + B0
+            else { hist[0] = G5_PIECES; hist[1] = G5_PIECES; hist[2] = 2 * G5_PIECES; }   // u=-1: p3 A1, p2 B1, p1 A0 + B0
         }
     };
     if (d.stats && tid < 2 * EPI_MAXG) st_lds[tid] = 0.0;
@@ -274,13 +283,20 @@ __global__ __launch_bounds__(512) void gemm5_kernel(const GemmDesc d) {
             const int buf = u & 1;
             const bool n1 = ST || u + 1 < nk, n2 = ST || u + 2 < nk;
             auto lw = [&]() {
-                if constexpr (ST) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-                else load_wait();
+                if constexpr (ST) {
+#ifdef ATHD_G5_CHECK
+                    if (hist[0] + hist[1] + hist[2] + hist[3] != G5_STEADY_VM && lane == 0)
+                        printf("gemm5: steady vmcnt %d != %d\n", hist[0] + hist[1] + hist[2] + hist[3], G5_STEADY_VM);
+#endif
+                    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");     // G5_STEADY_VM
+                } else {
+                    load_wait();
+                }
             };
             // ---- phase 0: (A0, B0)
             lw();
             if (wr == 0 && n1) issueA(u + 1, 1);
-            push(wr == 0 && n1 ? 2 : 0);
+            push(wr == 0 && n1 ? G5_PIECES : 0);
             readB(buf, 0, bf0);
             readA(buf, 0, af);
             sbar();
@@ -292,7 +308,7 @@ __global__ __launch_bounds__(512) void gemm5_kernel(const GemmDesc d) {
                 issueA(u + 2, 0);
                 issueB(u + 2, 0);
             }
-            push(wr == 1 && n2 ? 4 : 0);
+            push(wr == 1 && n2 ? 2 * G5_PIECES : 0);
             readB(buf, 1, bf1);
             sbar();
             quad(0, 1, af, bf1);
@@ -307,7 +323,7 @@ __global__ __launch_bounds__(512) void gemm5_kernel(const GemmDesc d) {
                     issueB(u + 2, 1);
                 }
             }
-            push(n2 ? (wr == 0 ? 4 : 2) : 0);
+            push(n2 ? (wr == 0 ? 2 : 1) * G5_PIECES : 0);
             readA(buf, 1, af);
             sbar();
             quad(1, 1, af, bf1);
@@ -318,7 +334,7 @@ __global__ __launch_bounds__(512) void gemm5_kernel(const GemmDesc d) {
                 if (wr == 0) issueB(u + 2, 1);
                 else issueA(u + 2, 1);
             }
-            push(n2 ? 2 : 0);
+            push(n2 ? G5_PIECES : 0);
             sbar();
             quad(1, 0, af, bf0);
             sbar();
@@ -401,14 +417,12 @@ static void launch5f(const GemmDesc& d, hipStream_t s) {
     const int64_t tiles = ((M + 255) / 256) * ((d.N + 255) / 256);
     int64_t grid = tiles;
     if constexpr ((F & (F_RES | F_STATS)) == 0) {   // persistent: the resident blocks (one per CU), a multiple of 8
-        static int resident = 0;
-        if (resident == 0) {
-            int per_cu = 0, cus = 0, dev = 0;
-            (void)hipGetDevice(&dev);
-            (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        static int per_cu = 0;   // a property of the kernel; the CU count is the current device's
+        if (per_cu == 0) {
             (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, gemm5_kernel<F, PROBE, LIN>, 512, 0);
-            resident = per_cu > 0 && cus > 0 ? per_cu * cus / 8 * 8 : -1;
+            if (per_cu <= 0) per_cu = -1;
         }
+        const int resident = per_cu > 0 ? per_cu * device_cus() / 8 * 8 : -1;
         if (resident >= 8 && resident < tiles) grid = resident;
     }
     KScope ks(s);

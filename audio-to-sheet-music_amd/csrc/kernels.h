@@ -68,6 +68,10 @@ struct LnDesc {
     // norms of one input (forward.cpp), one read of x instead of two
     const float* w2 = nullptr; const float* b2 = nullptr; void* out2 = nullptr;
 };
+// the LayerNorm pass can apply a pending GroupNorm in registers only (gn_writeback = 0): the C = 512 row kernel, with
+// out2 (if any) fused into the same pass (bf16 output, no positional rows)
+inline bool ln_lazy_gn_ok(const LnDesc& d) { return d.C == 512 && (!d.out2 || (d.out_bf16 && !d.pos)); }
+
 void layernorm_launch(const LnDesc& d, hipStream_t s);
 // y = bf16(x), n % 8 == 0 (round to nearest even)
 void to_bf16_launch(const float* x, uint16_t* y, int64_t n, hipStream_t s);

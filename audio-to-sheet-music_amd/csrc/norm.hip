@@ -574,6 +574,11 @@ constexpr int LN_RW = 4;
 void layernorm_launch(const LnDesc& d0, hipStream_t s) {
     const int64_t rows = (int64_t)d0.nb * d0.N;
     LnDesc d = d0;
+    // gn_writeback = 0 (the pending GroupNorm applied in registers only) exists only where ln_lazy_gn_ok holds (the
+    // C = 512 row kernel, out2 fused into it): the out2 split below reads x again expecting the GroupNorm written back,
+    // and layernorm_kernel<6> always writes it back.  forward.cpp requests the lazy form only under that predicate;
+    // anything else is written back here
+    if (!d.gn_writeback && !ln_lazy_gn_ok(d)) d.gn_writeback = 1;
     if (d.out2 && !(d.C == 512 && d.out_bf16 && !d.pos)) {   // (only the C = 512 bf16 row kernel has out2)
         LnDesc d2 = d0;
         d2.gn_stats = nullptr; d2.w = d0.w2; d2.b = d0.b2; d2.out = d0.out2; d2.out2 = nullptr; d2.pos = nullptr;

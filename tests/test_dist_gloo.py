@@ -126,10 +126,22 @@ def _dataset_checks(rank, world, split_dir, out_dir):
             wsum[s:e] += w
         return out / wsum.clamp(min=1e-8)
 
-    for ovs in (1.5, 0.0):
+    hop = lambda ovs: int(SEG * SR) - int(ovs * SR)                                         # noqa: E731
+    for ovs, gw in ((1.5, None), (0.0, None), (1.5, 1), (0.0, 1)):
+        st = {}
         res = separate_dataset(None, tracks, STEMS, segment_seconds=SEG, overlap=ovs, sample_rate=SR, max_batch=2,
                                forward_fn=_fake_forward, ola_fn=ola, metric_fn=metric, keep_estimates=True,
-                               output_dir=out_dir if (rank == 0 and ovs) else None, log=None)
+                               output_dir=out_dir if (rank == 0 and ovs and gw is None) else None, log=None,
+                               group_windows=gw, stats=st)
+        wins = [-(-L // hop(ovs)) for L in tracks.lengths()]
+        if gw == 1:
+            # several track-aligned gather groups; dst's buffer holds the longest track's windows (the
+            # smallest cap), not the split's
+            assert st["groups"] > 1, st
+            assert st["buffer_rows"] == (max(wins) if rank == 0 else 0), (st, wins)
+            assert max(wins) < sum(wins)
+        else:
+            assert st["buffer_rows"] == (min(sum(wins), max(4 * world * 2, max(wins))) if rank == 0 else 0), st
         if rank != 0:
             assert res is None
             continue

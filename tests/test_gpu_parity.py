@@ -211,6 +211,38 @@ def test_fdec1_fused_matches_unfused(models, monkeypatch, T):
     assert s >= 60.0, s
 
 
+def test_fdec1_gram_large_mean(state_dict, text_table, monkeypatch):
+    """VERDICT r04 weak #1 caveat 2: the level-1 Gram statistics in the cancellation regime.  The level-0 frequency
+    decoder's GroupNorm shift (`freq_decoder.layers.0.1.bias`) is set to +30, so the level-1 ConvT input is
+    GELU(30 + O(1)) ~ 30 + O(1): mean / std >= 30, and the fp32 Gram blocks sum_{w,c} x x^T are dominated by the DC
+    part whose square the variance then subtracts.  bf16 fused (fdec1f.hip) and unfused (ATHD_FDEC1_FUSED=0, fp32 row
+    sums) against the fp32 oracle on the same weights: fused within 3 dB of unfused."""
+    from athd.model import AudioTextHTDemucs
+    from athd.synth import synthetic_batch
+    from athd.weights import STEMS
+    from oracle.athtdemucs_ref import AudioTextHTDemucsRef
+    sd = dict(state_dict)
+    sd["freq_decoder.layers.0.1.bias"] = np.full_like(np.asarray(sd["freq_decoder.layers.0.1.bias"]), 30.0)
+    wav = torch.as_tensor(synthetic_batch(2, 264600, seed0=41))
+    oracle = AudioTextHTDemucsRef(sd)
+    cap = {}
+    oracle.forward(wav[:1], torch.as_tensor(text_table[:1]), capture=cap)
+    ref = oracle.forward_prompts(wav, torch.as_tensor(text_table)).numpy()
+    m = AudioTextHTDemucs(dtype="bf16", text_table={s: text_table[i] for i, s in enumerate(STEMS)})
+    m.load_state_dict(sd)
+    m = m.to("cuda").eval()
+    res = {}
+    for fused in ("0", "1"):
+        monkeypatch.setenv("ATHD_FDEC1_FUSED", fused)
+        out = m.forward_prompts(wav.cuda(), list(STEMS)).cpu().numpy()
+        assert np.isfinite(out).all()
+        res[fused] = min(sdr_db(ref[b, p], out[b, p]) for b in range(2) for p in range(4))
+    _report("fdec1_gram_large_mean", {"sdr_db_min_fused": res["1"], "sdr_db_min_unfused": res["0"],
+                                      "phase_cond": _phase_cond(cap["z"])})
+    assert res["1"] >= res["0"] - 3.0, res
+    assert res["1"] >= BF16_SDR_DB - 10.0, res
+
+
 def test_batch_independence(models):
     """Each segment of a batch is computed independently (per-sample normalisation, no cross-sample state)."""
     from athd.synth import synthetic_batch

@@ -92,3 +92,113 @@ def test_bad_embeddings_are_rejected():
         PromptEmbedder(table={}).rows(["a", "b"], 3)
     with pytest.raises(TypeError):
         _text_features(object())
+
+
+def _patch_from_pretrained(monkeypatch, clap, seen):
+    """ClapModel / AutoTokenizer.from_pretrained replaced by offline stand-ins (the HF cache has no CLAP here);
+    records the names and flags the library asked for."""
+    from transformers import AutoTokenizer, ClapModel
+
+    def clap_fp(name, **kw):
+        seen.append(("clap", name, kw))
+        return clap
+
+    def tok_fp(name, **kw):
+        seen.append(("tok", name, kw))
+        return FakeTokenizer()
+
+    monkeypatch.setattr(ClapModel, "from_pretrained", staticmethod(clap_fp))
+    monkeypatch.setattr(AutoTokenizer, "from_pretrained", staticmethod(tok_fp))
+
+
+def test_test_inference_default_clap_reaches_window_loop(tmp_path, monkeypatch, state_dict):
+    """the reference's own call `test_inference(checkpoint_path, data_dir)` (no keyword arguments)
+    builds CLAP + tokenizer like `test_inference.py:26-28` (here from the local cache: local_files_only=True),
+    loads the checkpoint's `clap.*` keys into it (`:34-35`) and embeds the stem prompts through
+    `get_text_features` (`ATHTDemucs_v2.py:241-244`).  The device parts (forward, OLA, sdr) are stubbed on this
+    CPU-only host; the GPU twin is tests/test_gpu_track.py::test_test_inference_default_clap."""
+    import numpy as np
+    import athd.inference as inf
+    from athd.model import AudioTextHTDemucs
+    from athd.musdb import HQ_FILES, write_wav
+    from athd.weights import STEMS
+
+    clap = _clap_model()
+    trained = _clap_model()
+    with torch.no_grad():                               # the checkpoint's CLAP differs from the "pretrained" one
+        trained.text_projection.linear1.weight.mul_(-2.0)
+    seen = []
+    _patch_from_pretrained(monkeypatch, clap, seen)
+    sd = {k: torch.as_tensor(np.asarray(v)) for k, v in state_dict.items()}
+    sd.update({"clap." + k: v.clone() for k, v in trained.state_dict().items()})
+    ckpt = tmp_path / "best_model.pt"
+    torch.save({"model_state_dict": sd, "epoch": 1}, ckpt)
+    L = 300000
+    d = tmp_path / "quick_train" / "A - B"
+    d.mkdir(parents=True)
+    rng = np.random.default_rng(0)
+    for f in HQ_FILES:
+        write_wav(d / f"{f}.wav", (0.1 * rng.standard_normal((L, 2))).astype(np.float32), 44100, "FLOAT")
+
+    calls = []
+
+    def fake_to(self, device):                          # no HIP device here: keep the model on the host
+        self.device = torch.device("cpu")
+        return self
+
+    def fake_forward_prompts(self, wav, prompts, out=None):
+        calls.append((tuple(wav.shape), list(prompts), self.embedder.rows(list(prompts), len(prompts)).clone()))
+        o = torch.zeros((wav.shape[0], len(prompts), 2, wav.shape[2]))
+        if out is not None:
+            out.copy_(o)
+            return out
+        return o
+
+    monkeypatch.setattr(torch.cuda, "is_available", lambda: True)
+    monkeypatch.setattr(AudioTextHTDemucs, "to", fake_to)
+    monkeypatch.setattr(AudioTextHTDemucs, "forward_prompts", fake_forward_prompts)
+    monkeypatch.setattr(inf, "overlap_add", lambda win, length, *a, **k: torch.zeros((win.shape[1], 2, length)))
+    monkeypatch.setattr(inf, "sdr_loss", lambda e, t: torch.tensor(1.5))
+    monkeypatch.chdir(tmp_path)
+
+    scores = inf.test_inference(str(ckpt), str(tmp_path / "quick_train"))
+
+    assert [(k, n, kw.get("local_files_only")) for k, n, kw in seen] == [
+        ("clap", "laion/clap-htsat-unfused", True), ("tok", "laion/clap-htsat-unfused", True)]
+    assert scores == {s: -1.5 for s in STEMS}
+    assert calls and all(p == list(STEMS) for _, p, _ in calls)
+    assert [c[0] for c in calls] == [(1, 2, 264600), (1, 2, 300000 - 260190)]   # a full window, the tail
+    # the rows the window loop saw are the get_text_features rows of the CHECKPOINT's CLAP weights
+    with torch.no_grad():
+        inp = FakeTokenizer()(list(STEMS))
+        want = F.normalize(trained.text_projection(trained.text_model(**inp).pooler_output), dim=-1)
+    for _, _, rows in calls:
+        assert torch.allclose(rows, want, atol=1e-6)
+    assert (tmp_path / "results" / "A__B" / "extracted_vocals.wav").exists()
+
+
+def test_load_model_without_cached_clap_names_the_alternative(tmp_path, monkeypatch, state_dict):
+    import numpy as np
+    from transformers import ClapModel
+    from athd.inference import load_model
+
+    def missing(name, **kw):
+        raise OSError(f"We couldn't connect to 'https://huggingface.co' to load the files of {name}")
+
+    monkeypatch.setattr(ClapModel, "from_pretrained", staticmethod(missing))
+    ckpt = tmp_path / "best_model.pt"
+    torch.save({"model_state_dict": {k: torch.as_tensor(np.asarray(v)) for k, v in state_dict.items()}}, ckpt)
+    with pytest.raises(RuntimeError, match="laion/clap-htsat-unfused.*text_table="):
+        load_model(str(ckpt), "cuda")
+
+
+def test_checkpoint_clap_keys_invalidate_cached_embeddings():
+    from athd.model import AudioTextHTDemucs
+    clap = _clap_model()
+    m = AudioTextHTDemucs(None, clap, FakeTokenizer(), dtype="f32")
+    before = m.embedder.rows("vocals", 1).clone()
+    new = {"clap." + k: (-v if k.startswith("text_projection") else v) for k, v in clap.state_dict().items()}
+    missing, unexpected = m.load_state_dict(new)
+    assert not any(k.startswith("clap.") for k in unexpected)
+    after = m.embedder.rows("vocals", 1)
+    assert not torch.allclose(before, after)

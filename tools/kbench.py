@@ -321,6 +321,13 @@ if __name__ == "__main__":
             gemm_case(M, 2048, 512, act=1)
             gemm_case(M, 512, 512)
         sys.exit(0)
+    if "quant" in sys.argv[1:]:               # tile quantisation: 1024 vs 1036 256x256 tiles (N 512), time branch 518
+        VARIANTS = (50,)
+        for _ in range(2):
+            for m in (131072, M, 64 * 1034, 65536):
+                gemm_case(m, 512, 2048)
+                gemm_case(m, 512, 512)
+        sys.exit(0)
     if "g5probe" in sys.argv[1:]:             # gemm5 ablations: 51 no staging, 52 no fragment reads, 53 no MFMA, 54 no barriers
         VARIANTS = (40, 50, 51, 52, 53, 54)
         gemm_case(4096, 4096, 4096)
