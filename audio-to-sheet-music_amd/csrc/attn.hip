@@ -506,6 +506,21 @@ ATHD_DEV float vmax3(float a, float b, float c) {
     return r;
 }
 
+// exp2 on the FMA pipe (VERDICT r04 #3 experiment; kbench builds with -DATHD_ATTN_POLY=n, the product keeps n = 0):
+// x -> n + f with n = rint(x) by the 1.5 * 2^23 magic add (its low mantissa bits hold n), 2^f on [-0.5, 0.5] as a
+// degree-3 polynomial fitted to the relative error (max 1.4e-4, below bf16's 2^-9), and n added to the exponent field by
+// one v_lshl_add_u32 ((bits(t) << 23) == n << 23 mod 2^32).  Arguments below -126 are clamped (P underflows to ~0).
+#ifndef ATHD_ATTN_POLY
+#define ATHD_ATTN_POLY 0        // exp2 calls of every 16 per key block evaluated by exp2_poly
+#endif
+ATHD_DEV float exp2_poly(float x) {
+    x = __builtin_fmaxf(x, -126.0f);
+    const float t = x + 12582912.0f;
+    const float f = x - (t - 12582912.0f);
+    const float p = fmaf(fmaf(fmaf(0.05502927f, f, 0.24225698f), f, 0.69325305f), f, 0.99995134f);
+    return __uint_as_float((__float_as_uint(t) << 23) + __float_as_uint(p));
+}
+
 #define ATHD_A32_QK(INIT)                                                                                      \
     do {                                                                                                       \
         const float init_ = (INIT);                                                                            \
@@ -676,8 +691,10 @@ __global__ __launch_bounds__(256, MINW) void attn32_kernel(const AttnDesc d) {
                 ls2[kb] = (athd_f2v){0.f, 0.f};
 #pragma unroll
                 for (int i = 0; i < 16; i += 2) {
-                    sc[kb][i] = __builtin_amdgcn_exp2f(sc[kb][i]);
-                    sc[kb][i + 1] = __builtin_amdgcn_exp2f(sc[kb][i + 1]);
+                    // (ATHD_ATTN_POLY of the 16 on the FMA pipe, spread over the block: pairs i with i % 8 >= 8 - n/2)
+                    const bool poly = ATHD_ATTN_POLY > 0 && (i & 7) >= 8 - ATHD_ATTN_POLY / 2;
+                    sc[kb][i] = poly ? exp2_poly(sc[kb][i]) : __builtin_amdgcn_exp2f(sc[kb][i]);
+                    sc[kb][i + 1] = poly ? exp2_poly(sc[kb][i + 1]) : __builtin_amdgcn_exp2f(sc[kb][i + 1]);
                     ls2[kb] += (athd_f2v){sc[kb][i], sc[kb][i + 1]};
                 }
             }

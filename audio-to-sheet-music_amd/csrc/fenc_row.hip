@@ -73,6 +73,15 @@ ATHD_DEV void gn_from_sums(float s1, float s2, float cnt, float& mean, float& rs
 
 }  // namespace
 
+#ifdef ATHD_FR_STAMP
+// measurement build only (-DATHD_FR_STAMP, tools/fr_stamps.py): s_memtime at the phase boundaries of
+// fenc_row0_kernel and fenc_row_kernel, wave 0 of every workgroup -> g_fr_stamp[block][16]; read back with athd_fr_stamps
+__device__ uint64_t g_fr_stamp[65536 * 16];
+#define FR_STAMP(k) do { if (threadIdx.x == 0) g_fr_stamp[(size_t)blockIdx.x * 16 + (k)] = __builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define FR_STAMP(k) do { } while (0)
+#endif
+
 // NW waves per workgroup (6 for C = 48, 12 for C = 96: one workgroup per CU either way at C = 96 (114 KB LDS), so
 // twice the waves per row halve each wave's m-tiles (and the residual stream's registers: 36 instead of 68))
 #define FR_SCHED() __builtin_amdgcn_sched_barrier(0)      // (no instruction is scheduled across it)
@@ -121,6 +130,7 @@ __global__ __launch_bounds__(NW * 64, CIN == 4 ? 3 : 1) void fenc_row_kernel(con
     const int ct = wave % NCT, mg = wave / NCT;
     const int cb = ct * 16 + 4 * l4;             // first of this lane's 4 x channels
 
+    FR_STAMP(0);
     if constexpr (GRAM) {
         for (int i = tid; i < 2 * (H * H + 2 * H + 2); i += NW * 64) {
             const int l = i / (H * H + 2 * H + 2), e = i % (H * H + 2 * H + 2);
@@ -172,6 +182,7 @@ __global__ __launch_bounds__(NW * 64, CIN == 4 ? 3 : 1) void fenc_row_kernel(con
             }
         }
     }
+    FR_STAMP(1);
     {
         const float4 bc = *reinterpret_cast<const float4*>(d.bc + cb);
         const float bcv[4] = {bc.x, bc.y, bc.z, bc.w};
@@ -186,6 +197,7 @@ __global__ __launch_bounds__(NW * 64, CIN == 4 ? 3 : 1) void fenc_row_kernel(con
         }
     }
     __syncthreads();
+    FR_STAMP(2);
     // the conv input stage is dead: zero the hidden tile's K padding columns 16..31 (columns 0..15 are written by
     // every conv3 pass, zeros past H included)
     for (int i = tid; i < TPM * 2; i += (NW * 64))
@@ -231,7 +243,9 @@ __global__ __launch_bounds__(NW * 64, CIN == 4 ? 3 : 1) void fenc_row_kernel(con
                 }
             }
         }
+        FR_STAMP(3 + 4 * dd);
         block_sum2<NW>(s1, s2, red[2 * dd]);
+        FR_STAMP(4 + 4 * dd);
         float hm, hr;
         gn_from_sums(s1, s2, (float)(H * T), hm, hr);
 #pragma unroll
@@ -320,6 +334,7 @@ __global__ __launch_bounds__(NW * 64, CIN == 4 ? 3 : 1) void fenc_row_kernel(con
             }
         }
         block_sum2<NW>(s1, s2, red[2 * dd + 1]);      // (its barrier also publishes hs)
+        FR_STAMP(5 + 4 * dd);
         float ym, yr;
         gn_from_sums(s1, s2, (float)(2 * C * T), ym, yr);
         // (y + b - mean) * rstd * w + beta as y * wa + ca, the LayerScale folded into the 'a' half and -log2(e) into
@@ -352,6 +367,7 @@ __global__ __launch_bounds__(NW * 64, CIN == 4 ? 3 : 1) void fenc_row_kernel(con
             st4bf(&xs[(FR_HALO + m) * XS_P + cb], xr[i][0], xr[i][1], xr[i][2], xr[i][3]);
         }
         __syncthreads();
+        FR_STAMP(6 + 4 * dd);
     }
 
     // ---------------------------------------------------------------- rewrite 1x1 (C -> 2C) + GLU (+ freq embedding)
@@ -393,6 +409,7 @@ __global__ __launch_bounds__(NW * 64, CIN == 4 ? 3 : 1) void fenc_row_kernel(con
                 ov[i] = make_uint2(pack2bf(o[0], o[1]), pack2bf(o[2], o[3]));
             }
         }
+        FR_STAMP(11);
         __syncthreads();         // every wave has read xs: stage the output row [T][C] there
         bf16_t* ob = xs;
 #pragma unroll
@@ -405,6 +422,7 @@ __global__ __launch_bounds__(NW * 64, CIN == 4 ? 3 : 1) void fenc_row_kernel(con
         bf16_t* dst = d.out + ((int64_t)b * d.Fout + f) * (int64_t)T * C;
         for (int i = tid; i < T * C / 8; i += (NW * 64))
             reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(ob)[i];
+        FR_STAMP(12);
     }
 }
 
@@ -489,14 +507,6 @@ ATHD_DEV int opaque_lane() {
 
 }  // namespace
 
-#ifdef ATHD_FR_STAMP
-// measurement build only (-DATHD_FR_STAMP, tools/fr_stamps.py): s_memtime at the phase boundaries of
-// fenc_row0_kernel, wave 0 of every workgroup -> g_fr_stamp[block][16]; read back with athd_fr_stamps
-__device__ uint64_t g_fr_stamp[65536 * 16];
-#define FR_STAMP(k) do { if (threadIdx.x == 0) g_fr_stamp[(size_t)blockIdx.x * 16 + (k)] = __builtin_amdgcn_s_memtime(); } while (0)
-#else
-#define FR_STAMP(k) do { } while (0)
-#endif
 
 __global__ __launch_bounds__(FR_NT, 4) void fenc_row0_kernel(const FencRowDesc d) {
     constexpr int C = F0_C, H = F0_H, NCT = 3, MTW = 9;
@@ -789,6 +799,383 @@ __global__ __launch_bounds__(FR_NT, 4) void fenc_row0_kernel(const FencRowDesc d
     }
 }
 
+// ---------------------------------------------------------------------------------------------------------
+// Level 1 (Cin = 48, C = 96, 12 waves, one workgroup per CU): the generic kernel's contractions and arithmetic with the
+// latency taken out of its two longest phases (s_memtime phase stamps, tools/fr_stamps.py FR_LEVEL=1: the four
+// register-staged conv stages took 36 % of a row, the two conv3 passes with their weights read from global memory
+// another 17 %):
+//   - conv: one stage per tap.  The [T][48] input rows of one frequency row are one contiguous slab of T x 96 B; it is
+//     moved by LDS-DMA (global_load_lds_dwordx4, no VGPR round trip) as a linear copy into a 3-deep ring of 272-row
+//     images (96-B rows; rows >= T and taps outside [0, Fin) from a zero page), so taps t + 1 and t + 2 are in flight
+//     while tap t's MFMAs run.  The tap's weights ([96][48], 112-B rows: conflict-free 16-row fragment reads) arrive
+//     the same way one tap ahead in a 2-deep ring.  Nothing but LDS-DMA is in flight in the loop: a VGPR-returning
+//     global load among the DMAs makes the compiler's wait counting give up (vmcnt(0) before the next MFMA, i.e. the
+//     ring serialised).  Every wave issues exactly 4 pieces per stage (surplus pieces load the zero page into a
+//     scratch KB), so the explicit counted waits are exact.  A tap's 48 channels are one 16x16x32 and one 16x16x16 MFMA.
+//   - conv3 weights of both DConv layers moved into the dead tap ring at the end of the conv and read from LDS.
+//   - the 1x1 weights issued before the barrier that precedes their use.
+namespace {
+constexpr int F1_C = 96, F1_CIN = 48, F1_H = 12, F1_NW = 12, F1_NT = 64 * F1_NW;
+constexpr int F1_NCT = F1_C / 16, F1_MG = F1_NW / F1_NCT, F1_MTW = (FR_MT_MAX + F1_MG - 1) / F1_MG;
+constexpr int F1_TPM = 16 * FR_MT_MAX;          // 272 positions
+constexpr int F1_PIECES = (F1_TPM * 96 + 1023) / 1024;   // 26 DMA pieces of 1 KB per tap image
+constexpr int F1_STB = F1_PIECES * 1024;        // one tap image (bytes), 96-B rows
+constexpr int F1_RING = 3;
+constexpr int F1_WROW = 112;                    // tap weight rows in LDS (bytes): 96 used
+constexpr int F1_WPC = (F1_C * F1_WROW + 1023) / 1024;   // 11 pieces per tap's weights
+constexpr int F1_WSB = F1_WPC * 1024;
+constexpr int F1_XS_P = F1_C + 8;               // residual image pitch (elements)
+constexpr int F1_HS_P = 40;                     // hidden tile pitch (elements)
+constexpr int F1_W3_P = 3 * F1_C + 8;           // conv3 weight rows in LDS (elements): 592 B, 16 rows on distinct banks
+constexpr int F1_W3C = F1_W3_P / 8;             // 37 chunks per conv3 row (36 used)
+constexpr int F1_W3PC = (2 * 16 * F1_W3C * 16 + 1023) / 1024;   // 19 pieces for both layers
+constexpr int F1_K3S = 3 * F1_C / 32;           // 9 conv3 K-steps
+constexpr int F1_C3I = (FR_MT_MAX + F1_NW - 1) / F1_NW;
+constexpr int F1_GSZ = F1_H * F1_H + 2 * F1_H + 2;
+static_assert(F1_TPM * 96 + 64 <= F1_STB && F1_TPM * F1_HS_P * 2 <= F1_STB && F1_W3PC * 1024 <= F1_STB,
+              "fenc_row1 LDS layout");
+static_assert(F1_PIECES <= 3 * F1_NW && F1_WPC <= F1_NW && F1_W3PC <= 2 * F1_NW, "DMA pieces per wave");
+typedef short short4_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void f1_lds_void;
+typedef __attribute__((address_space(1))) void f1_gbl_void;
+__device__ __attribute__((aligned(64))) uint4 g_zero_f1[4];
+}  // namespace
+
+__global__ __launch_bounds__(F1_NT, 1) void fenc_row1_kernel(const FencRowDesc d) {
+    constexpr int C = F1_C, H = F1_H, NW = F1_NW, MG = F1_MG, MTW = F1_MTW, TPM = F1_TPM;
+    constexpr int XS_P = F1_XS_P, HS_P = F1_HS_P;
+    // tap image ring; after the conv: the hidden tile (slot 0) and the conv3 weights (slot 2)
+    __shared__ __attribute__((aligned(16))) char stg[F1_RING * F1_STB];
+    __shared__ __attribute__((aligned(16))) char wring[2 * F1_WSB];
+    __shared__ __attribute__((aligned(16))) bf16_t xs[(TPM + 2 * FR_HALO) * XS_P];
+    __shared__ float red[4][2 * NW];
+    __shared__ float gsh[2][F1_GSZ];
+    __shared__ __attribute__((aligned(16))) char dma_sink[1024];
+    bf16_t* const hs = reinterpret_cast<bf16_t*>(stg);
+    const bf16_t* const w3s = reinterpret_cast<const bf16_t*>(stg + 2 * F1_STB);   // [2][16][F1_W3_P]
+
+    FR_STAMP(0);
+    const int R = d.B * d.Fout;
+    const int per = (R + 7) / 8;
+    const int r = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
+    if (r >= R) return;
+    const int b = r / d.Fout, f = r % d.Fout;
+    const int T = d.T;
+    const int MT = (T + 15) >> 4;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int l15 = lane & 15, l4 = lane >> 4;
+    const int ct = wave % F1_NCT, mg = wave / F1_NCT;
+    const int cb = ct * 16 + 4 * l4;
+
+    const char* const zero = reinterpret_cast<const char*>(g_zero_f1);
+    auto dma = [&](const char* src, char* dst) {
+        __builtin_amdgcn_global_load_lds((f1_gbl_void*)src, (f1_lds_void*)dst, 16, 0, 0);
+    };
+    // tap t's input image -> ring slot t % 3: a linear copy of the T x 96 B slab, piece p = image bytes
+    // [1024 p, 1024 p + 1024), wave w: pieces w, w + 12, w + 24 (past 26: zero page -> scratch)
+    auto dma_tap = [&](int t) {
+        const int fi = 4 * f - 2 + t;
+        const bool fok = fi >= 0 && fi < d.Fin;
+        const char* slab = (const char*)d.in + ((int64_t)b * d.Fin + (fok ? fi : 0)) * (int64_t)T * (F1_CIN * 2);
+        char* dst = stg + (t % F1_RING) * F1_STB;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const int p = wave + NW * j;
+            const int byte = 1024 * p + 16 * lane;
+            dma(fok && byte < T * (F1_CIN * 2) ? slab + byte : zero, p < F1_PIECES ? dst + p * 1024 : dma_sink);
+        }
+    };
+    // tap t's weights [96 rows][48] -> wring[t & 1], 112-B rows (16 B of zeros): wave w loads piece w (< 11)
+    auto dma_wt = [&](int t) {
+        const int e = 1024 * wave + 16 * lane;
+        const int row = e / F1_WROW, col = e - row * F1_WROW;
+        const bool ok = wave < F1_WPC && row < C && col < 96;
+        dma(ok ? (const char*)d.wc + (int64_t)row * d.wc_ld * 2 + t * 96 + col : zero,
+            wave < F1_WPC ? wring + (t & 1) * F1_WSB + 1024 * wave : dma_sink);
+    };
+    // the conv3 weights of both layers [2][16][296] -> ring slot 2 (free once tap 5 is read): 19 pieces, 2 per wave.
+    // (the two base pointers laundered into SGPRs: a per-lane select between two kernel-argument fields otherwise
+    // becomes a per-lane load of the field, a VGPR-returning load among the DMAs)
+    const char* const w3g0 = launder((const char*)d.w3[0]);
+    const char* const w3g1 = launder((const char*)d.w3[1]);
+    auto dma_w3 = [&]() {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int p = wave + NW * j;
+            const int e = (1024 * p + 16 * lane) >> 4;                   // chunk index in the LDS image
+            const int lr = e / F1_W3C, ch = e - lr * F1_W3C;             // (layer * 16 + row), chunk
+            const int dd = lr >> 4, row = lr & 15;
+            const bool ok = p < F1_W3PC && dd < 2 && ch < 3 * C / 8;
+            const char* w3g = dd ? w3g1 : w3g0;
+            dma(ok ? w3g + ((int64_t)row * d.w3_ld + 8 * ch) * 2 : zero,
+                p < F1_W3PC ? stg + 2 * F1_STB + 1024 * p : dma_sink);
+        }
+    };
+    for (int i = tid; i < 2 * F1_GSZ; i += F1_NT) gsh[i / F1_GSZ][i % F1_GSZ] = d.gram[i / F1_GSZ][i % F1_GSZ];
+    for (int i = tid; i < (TPM + 2 * FR_HALO) * XS_P / 8; i += F1_NT)
+        reinterpret_cast<uint4*>(xs)[i] = make_uint4(0u, 0u, 0u, 0u);
+    const float4 bc = *reinterpret_cast<const float4*>(d.bc + cb);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");          // (only LDS-DMA in flight from here on)
+    // VMEM issue order, for the counted waits below: img(0), wt(0), img(1); stage t: wt(t + 1), img(t + 2) (stage 6:
+    // wt(7), the conv3 weights)
+    dma_tap(0);
+    dma_wt(0);
+    dma_tap(1);
+
+    // ---------------------------------------------------------------- conv (8,1)/(4,1)/(2,0): 8 tap stages
+    f32x4_t xr[MTW];
+#pragma unroll
+    for (int i = 0; i < MTW; ++i) xr[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    const int wrow = (ct * 16 + l15) * F1_WROW;
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+        // this wave's img(t) and wt(t) landed: only the 3 pieces issued after wt(t) (img(t + 1); at t = 7 the conv3
+        // weights' 2) may still be in flight
+        if (t == 7) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+        // every wave's pieces landed; tap t - 1's reads done.  (A raw s_barrier: __syncthreads' fences would add a
+        // full vmcnt(0).)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        if (t + 1 < 8) dma_wt(t + 1);
+        if (t + 2 < 8) dma_tap(t + 2);                        // into the slot tap t - 1 was read from
+        if (t == 6) dma_w3();                                 // slot 2 held tap 5
+        const char* img = stg + (t % F1_RING) * F1_STB;
+        const char* wl = wring + (t & 1) * F1_WSB + wrow;
+        const bf16x8_t a0 = *reinterpret_cast<const bf16x8_t*>(wl + 16 * l4);
+        const short4_t a1 = *reinterpret_cast<const short4_t*>(wl + 64 + 8 * l4);
+#pragma unroll
+        for (int i = 0; i < MTW; ++i) {
+            // branch-free: a tile past MT reads rows clamped into the image and its accumulators are never used
+            const int mt = min(mg + MG * i, FR_MT_MAX - 1);
+            if (i % 3 == 0) FR_SCHED();           // (else all nine tiles' fragment reads are hoisted: spills)
+            const char* rp = img + (mt * 16 + l15) * (F1_CIN * 2);
+            xr[i] = mfma(a0, *reinterpret_cast<const bf16x8_t*>(rp + 16 * l4), xr[i]);
+            xr[i] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a1, *reinterpret_cast<const short4_t*>(rp + 64 + 8 * l4),
+                                                             xr[i], 0, 0, 0);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");          // the conv3 weights landed (published by the barrier below)
+    FR_STAMP(1);
+    {
+        const float bcv[4] = {bc.x, bc.y, bc.z, bc.w};
+#pragma unroll
+        for (int i = 0; i < MTW; ++i) {
+            const int mt = mg + MG * i;
+            const int m = mt * 16 + l15;
+            if (mt >= MT) continue;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) xr[i][q] = m < T ? gelu_fast(xr[i][q] + bcv[q]) : 0.f;
+            st4bf(&xs[(FR_HALO + m) * XS_P + cb], xr[i][0], xr[i][1], xr[i][2], xr[i][3]);
+        }
+    }
+    __syncthreads();
+    FR_STAMP(2);
+    // the tap ring is dead: zero the hidden tile's K padding columns 16..31 (columns 0..15 are written by every conv3)
+    for (int i = tid; i < TPM * 2; i += F1_NT)
+        *reinterpret_cast<uint4*>(&hs[(i >> 1) * HS_P + 16 + 8 * (i & 1)]) = make_uint4(0u, 0u, 0u, 0u);
+
+    // ---------------------------------------------------------------- DConv: x += LayerScale(GLU(GN(1x1(GELU(GN(conv3(x)))))))
+#pragma unroll 1
+    for (int dd = 0; dd < 2; ++dd) {
+        const int dil = 1 << dd;
+        f32x4_t ha[F1_C3I];
+#pragma unroll
+        for (int i = 0; i < F1_C3I; ++i) ha[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < F1_K3S; ++ks) {
+            const int k0 = ks * 32 + 8 * l4;
+            const bf16x8_t wf = *reinterpret_cast<const bf16x8_t*>(&w3s[(dd * 16 + l15) * F1_W3_P + k0]);
+            const int tap = k0 / C, c0 = k0 - tap * C;
+#pragma unroll
+            for (int i = 0; i < F1_C3I; ++i) {
+                const int mt = wave + NW * i;
+                if (mt >= MT) continue;
+                ha[i] = mfma(wf, ldfrag(&xs[(FR_HALO + mt * 16 + l15 + (tap - 1) * dil) * XS_P + c0]), ha[i]);
+            }
+        }
+        float hb[4], g1w[4], g1b[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int j = 4 * l4 + q < H ? 4 * l4 + q : H - 1;
+            hb[q] = d.b3[dd][j];
+            g1w[q] = d.g1w[dd][j];
+            g1b[q] = d.g1b[dd][j];
+        }
+        float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int i = 0; i < F1_C3I; ++i) {
+            const int mt = wave + NW * i;
+            const int m = mt * 16 + l15;
+            if (mt >= MT || m >= T) continue;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                if (4 * l4 + q < H) {
+                    const float v = ha[i][q] + hb[q];
+                    s1 += v;
+                    s2 += v * v;
+                }
+            }
+        }
+        FR_STAMP(3 + 4 * dd);
+        block_sum2<NW>(s1, s2, red[2 * dd]);
+        FR_STAMP(4 + 4 * dd);
+        float hm, hr;
+        gn_from_sums(s1, s2, (float)(H * T), hm, hr);
+#pragma unroll
+        for (int i = 0; i < F1_C3I; ++i) {
+            const int mt = wave + NW * i;
+            if (mt >= MT) continue;
+            float g[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                g[q] = 4 * l4 + q < H ? gelu_fast((ha[i][q] + hb[q] - hm) * hr * g1w[q] + g1b[q]) : 0.f;
+            st4bf(&hs[(mt * 16 + l15) * HS_P + 4 * l4], g[0], g[1], g[2], g[3]);
+        }
+        // the 1x1 output's GroupNorm statistics from the 1x1 conv's moments over the hidden rows this wave wrote
+        s1 = 0.f;
+        s2 = 0.f;
+        {
+            const float* G = gsh[dd];
+#pragma unroll
+            for (int i = 0; i < F1_C3I; ++i) {
+                const int mt = wave + NW * i;
+                if (mt >= MT || mt * 16 + l15 >= T) continue;
+                FR_SCHED();
+                float x[16];
+                const uint4* hr_ = reinterpret_cast<const uint4*>(&hs[(mt * 16 + l15) * HS_P]);
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                    const uint4 hq = hr_[u];
+                    const uint32_t w4[4] = {hq.x, hq.y, hq.z, hq.w};
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        x[8 * u + 2 * e] = __uint_as_float(w4[e] << 16);
+                        x[8 * u + 2 * e + 1] = __uint_as_float(w4[e] & 0xFFFF0000u);
+                    }
+                }
+                float qf = 0.f, lv = 0.f, lw = 0.f;
+#pragma unroll
+                for (int jj = 0; jj < H / 4; ++jj) {
+                    const int j = 4 * jj + l4;
+                    const float xj = x[j];
+                    float tq = 0.f;
+#pragma unroll
+                    for (int kk = 0; kk < H; ++kk) tq += G[j * H + kk] * x[kk];
+                    qf += xj * tq;
+                    lv += G[H * H + j] * xj;
+                    lw += G[H * H + H + j] * xj;
+                }
+                s1 += (l4 == 0 ? G[H * H + 2 * H] : 0.f) + lw;
+                s2 += (l4 == 0 ? G[H * H + 2 * H + 1] : 0.f) + (2.f * lv + qf);
+            }
+        }
+        // the apply pass's 1x1 weights and GroupNorm affine (issued before the reduction's barrier)
+        const bf16x8_t wa = ldfrag(d.w1[dd] + (int64_t)(32 * ct + l15) * d.w1_ld + 8 * l4);
+        const bf16x8_t wg = ldfrag(d.w1[dd] + (int64_t)(32 * ct + 16 + l15) * d.w1_ld + 8 * l4);
+        const int pa = 32 * ct + 4 * l4;
+        block_sum2<NW>(s1, s2, red[2 * dd + 1]);      // (its barrier also publishes hs)
+        FR_STAMP(5 + 4 * dd);
+        const float4 ba4 = *reinterpret_cast<const float4*>(d.b1[dd] + pa);
+        const float4 bg4 = *reinterpret_cast<const float4*>(d.b1[dd] + pa + 16);
+        const float4 gwa = *reinterpret_cast<const float4*>(d.g2w[dd] + pa);
+        const float4 gba = *reinterpret_cast<const float4*>(d.g2b[dd] + pa);
+        const float4 gwg = *reinterpret_cast<const float4*>(d.g2w[dd] + pa + 16);
+        const float4 gbg = *reinterpret_cast<const float4*>(d.g2b[dd] + pa + 16);
+        const float4 sc4 = *reinterpret_cast<const float4*>(d.scale[dd] + cb);
+        float ym, yr;
+        gn_from_sums(s1, s2, (float)(2 * C * T), ym, yr);
+        const float ba[4] = {ba4.x, ba4.y, ba4.z, ba4.w}, bg[4] = {bg4.x, bg4.y, bg4.z, bg4.w};
+        const float gwav[4] = {gwa.x, gwa.y, gwa.z, gwa.w}, gbav[4] = {gba.x, gba.y, gba.z, gba.w};
+        const float gwgv[4] = {gwg.x, gwg.y, gwg.z, gwg.w}, gbgv[4] = {gbg.x, gbg.y, gbg.z, gbg.w};
+        const float scv[4] = {sc4.x, sc4.y, sc4.z, sc4.w};
+        float wav[4], cav[4], wgv[4], cgv[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const float wa_ = gwav[q] * yr, wg_ = gwgv[q] * yr;
+            wav[q] = wa_ * scv[q];
+            cav[q] = ((ba[q] - ym) * wa_ + gbav[q]) * scv[q];
+            wgv[q] = wg_ * -1.4426950408889634f;
+            cgv[q] = ((bg[q] - ym) * wg_ + gbgv[q]) * -1.4426950408889634f;
+        }
+#pragma unroll
+        for (int i = 0; i < MTW; ++i) {
+            const int mt = mg + MG * i;
+            const int m = mt * 16 + l15;
+            if (mt >= MT) continue;
+            const bf16x8_t hf = ldfrag(&hs[(mt * 16 + l15) * HS_P + 8 * l4]);
+            const f32x4_t z = f32x4_t{0.f, 0.f, 0.f, 0.f};
+            const f32x4_t ya = mfma(wa, hf, z), yg = mfma(wg, hf, z);
+            if (m >= T) continue;                 // positions >= T stay 0 in xr and xs
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float a = ya[q] * wav[q] + cav[q];
+                const float g = yg[q] * wgv[q] + cgv[q];
+                xr[i][q] = a * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(g)) + xr[i][q];
+            }
+            st4bf(&xs[(FR_HALO + m) * XS_P + cb], xr[i][0], xr[i][1], xr[i][2], xr[i][3]);
+        }
+        __syncthreads();
+        FR_STAMP(6 + 4 * dd);
+    }
+
+    // ---------------------------------------------------------------- rewrite 1x1 (C -> 2C) + GLU
+    {
+        const int l15 = opaque_lane() & 15;      // (per-tile addresses recomputed here, not held across the DConv)
+        const int pa = 32 * ct + 4 * l4;
+        float ba[4], bg[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            ba[q] = d.br[pa + q];
+            bg[q] = d.br[pa + 16 + q];
+        }
+        bf16x8_t wra[3], wrg[3];
+#pragma unroll
+        for (int ks = 0; ks < 3; ++ks) {
+            wra[ks] = ldfrag(d.wr + (int64_t)(32 * ct + l15) * d.wr_ld + ks * 32 + 8 * l4);
+            wrg[ks] = ldfrag(d.wr + (int64_t)(32 * ct + 16 + l15) * d.wr_ld + ks * 32 + 8 * l4);
+        }
+        uint2 ov[MTW];
+#pragma unroll
+        for (int i = 0; i < MTW; ++i) {
+            const int mt = mg + MG * i;
+            const int m = mt * 16 + l15;
+            ov[i] = make_uint2(0u, 0u);
+            if (mt >= MT) continue;
+            f32x4_t za = f32x4_t{0.f, 0.f, 0.f, 0.f}, zg = za;
+#pragma unroll
+            for (int ks = 0; ks < 3; ++ks) {
+                const bf16x8_t xf = ldfrag(&xs[(FR_HALO + m) * XS_P + ks * 32 + 8 * l4]);
+                za = mfma(wra[ks], xf, za);
+                zg = mfma(wrg[ks], xf, zg);
+            }
+            if (m < T) {
+                float o[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) o[q] = (za[q] + ba[q]) * sigmoid_fast(zg[q] + bg[q]);
+                ov[i] = make_uint2(pack2bf(o[0], o[1]), pack2bf(o[2], o[3]));
+            }
+        }
+        FR_STAMP(11);
+        __syncthreads();         // every wave has read xs: stage the output row [T][C] there
+        bf16_t* ob = xs;
+#pragma unroll
+        for (int i = 0; i < MTW; ++i) {
+            const int mt = mg + MG * i;
+            const int m = mt * 16 + l15;
+            if (mt < MT && m < T) *reinterpret_cast<uint2*>(&ob[m * C + cb]) = ov[i];
+        }
+        __syncthreads();
+        bf16_t* dst = d.out + ((int64_t)b * d.Fout + f) * (int64_t)T * C;
+        for (int i = tid; i < T * C / 8; i += F1_NT)
+            reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(ob)[i];
+        FR_STAMP(12);
+    }
+}
+
 bool fenc_row_supported(int cin, int c, int T) {
     return ((cin == 4 && c == 48) || (cin == 48 && c == 96)) && T >= 1 && T <= 16 * FR_MT_MAX;
 }
@@ -798,6 +1185,12 @@ extern "C" int athd_fr_stamps(void* host, int blocks) {
     return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_fr_stamp), (size_t)blocks * 16 * 8, 0, hipMemcpyDeviceToHost);
 }
 #endif
+
+static bool fr1_v2() {                 // (round-5 A/B: ATHD_FR1=0 takes the generic level-1 kernel)
+    static int v = -1;
+    if (v < 0) { const char* e = getenv("ATHD_FR1"); v = (e && e[0] == '0') ? 0 : 1; }
+    return v == 1;
+}
 
 int fenc_row_launch(const FencRowDesc& d, int cin, int c, hipStream_t s) {
     // (the 1x1 convs' GroupNorm statistics come from their moments, d.gram)
@@ -814,6 +1207,7 @@ int fenc_row_launch(const FencRowDesc& d, int cin, int c, hipStream_t s) {
         ks.begin(cin == 4 ? "fenc_row0_kernel" : "fenc_row_kernel<48,96,12,true>", 2.0 * macs, in_b + rows * T * c * 2);
     }
     if (cin == 4) hipLaunchKernelGGL(fenc_row0_kernel, grid, dim3(FR_NT), 0, s, d);
+    else if (fr1_v2()) hipLaunchKernelGGL(fenc_row1_kernel, grid, dim3(F1_NT), 0, s, d);
     else hipLaunchKernelGGL((fenc_row_kernel<48, 96, 12, true>), grid, dim3(12 * 64), 0, s, d);
     return (int)hipGetLastError();
 }
