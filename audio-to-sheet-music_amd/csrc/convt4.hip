@@ -18,6 +18,8 @@
 //     item change: wave reduction + one fp64 atomic pair), bf16 8-B stores of the stored residues.
 // keep = 1 (freq level 2): only residues 1, 2 are stored, as rows 2t, 2t+1 (the rows a following /4 bilinear
 // resize reads); keep = 0 (time level 2): all four, as rows 4t + rho.  Row t = (b, u) = m / W, column w = m % W.
+#include <cstdlib>
+
 #include "common.h"
 #include "prof.h"
 #include "gemm.h"
@@ -242,6 +244,170 @@ __global__ __launch_bounds__(NW * 64) void convt4_kernel(const ConvT4Desc d) {
     flush();
 }
 
+// ---------------------------------------------------------------------------------------------------------------
+// Column walk (W >= 32, the frequency branch: H = W = Tspec).  The unit kernel above reads every input row three
+// times (as tap u-1, u and u+1 of three units 259 rows apart) and relied on L2 for the re-reads; with the waves of an
+// XCD drifting apart, PMC showed 1.29x the algorithmic HBM bytes.  Here a wave owns a column block (item b, 32
+// consecutive w) and a segment of rows u0 .. u1-1 and walks it row by row: the tap fragments of rows u-1, u, u+1 are
+// kept in three register sets that rotate, so each step loads ONE new row (u+2) - every input row is read once per
+// column block and the loads are a third of the unit kernel's.  Rows and columns outside the item read a zero page;
+// columns past W are neither stored nor counted.  GroupNorm statistics: per lane fp32 per step, fp64 across the
+// segment, one fp64 atomic pair per segment (a segment lies in one item).
+constexpr int CW_RF = 1, CW_NW = 12, CW_SEG = 8;  // 16-wide column blocks, 12 waves per workgroup, 8 row segments
+template <bool KEEP>
+__global__ __launch_bounds__(CW_NW * 64) void convt4_walk_kernel(const ConvT4Desc d) {
+    constexpr int RF = CW_RF;
+    __shared__ __attribute__((aligned(16))) char wl[4 * CT_CO * CT_WROW];   // 73,728 B
+    for (int c = threadIdx.x; c < 4 * CT_CO * 24; c += CW_NW * 64) {
+        const int n = c / 24, ch = c - 24 * (c / 24);
+        const uint4 v = reinterpret_cast<const uint4*>(d.w)[c];
+        *reinterpret_cast<uint4*>(wl + n * CT_WROW + ((ch ^ (n & 7)) * 16)) = v;
+    }
+    __syncthreads();
+
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int fr = lane & 15, g = lane >> 4;
+    const int H = d.H, W = d.W;
+    const int nwb = (W + 16 * RF - 1) / (16 * RF);
+    const int items = d.nb * nwb * CW_SEG;
+    // items in (segment, w block, item b) order, each XCD a contiguous range (neighbouring column blocks share the
+    // L2 lines of a row: 32 x 192 B = 6 KB of each 50-KB row); waves of the XCD stride through it
+    const int xcd = blockIdx.x & 7;
+    const int nwx = (int)(gridDim.x >> 3) * CW_NW;
+    const int i0 = (int)((int64_t)items * xcd / 8), i1 = (int)((int64_t)items * (xcd + 1) / 8);
+    int it = i0 + (int)(blockIdx.x >> 3) * CW_NW + wave;
+    if (it >= i1) return;
+
+    float4 b4[3];
+#pragma unroll
+    for (int jj = 0; jj < 3; ++jj) b4[jj] = *reinterpret_cast<const float4*>(d.bias + 16 * jj + 4 * g);
+    const int f7 = fr & 7;
+    const uint32_t wb_even = (uint32_t)(fr * CT_WROW + (4 * (f7 >> 2) + (g ^ (f7 & 3))) * 16);
+    const uint32_t wb_odd = (uint32_t)(fr * CT_WROW + (4 * (1 - (f7 >> 2)) + (g ^ (f7 & 3))) * 16);
+    uint32_t wbe = wb_even, wbo = wb_odd;
+    auto fence = [&]() { asm volatile("" : "+v"(wbe), "+v"(wbo)); };
+    auto wfrag = [&](int p, int jj, int s) -> bf16v8 {
+        const uint32_t a = ((s & 1) ? wbo : wbe) + (uint32_t)((96 * p + 16 * jj) * CT_WROW + 128 * (s >> 1));
+        return *reinterpret_cast<const bf16v8*>(wl + a);
+    };
+    const char* const xb = reinterpret_cast<const char*>(d.x);
+    const char* const zero = reinterpret_cast<const char*>(g_zero_ct4);
+    const f32x4_t z4 = {0.f, 0.f, 0.f, 0.f};
+    f32x4_t acc[RF][6];
+    auto mma = [&](int p, int h, const bf16v8 (&F)[RF][3]) {
+#pragma unroll
+        for (int s = 0; s < 3; ++s) {
+            fence();
+#pragma unroll
+            for (int jj = 0; jj < 6; ++jj) {
+                const bf16v8 wf = wfrag(p, jj, 3 * h + s);
+#pragma unroll
+                for (int i = 0; i < RF; ++i)
+                    acc[i][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, F[i][s], (h == 0 && s == 0) ? z4 : acc[i][jj], 0, 0, 0);
+            }
+        }
+    };
+
+    for (;;) {
+        const int seg = it / (d.nb * nwb), rem = it - seg * (d.nb * nwb);
+        const int wblk = rem / d.nb, b = rem - wblk * d.nb;
+        const int u0 = (int)((int64_t)H * seg / CW_SEG), u1 = (int)((int64_t)H * (seg + 1) / CW_SEG);
+        // this lane's columns w = 32 wblk + 16 i + fr: per-lane byte offsets (32 bits) from the item's wave-uniform
+        // row bases, which carry the row index
+        uint32_t cin_off[RF], cout_off[RF];
+        bool cok[RF];
+#pragma unroll
+        for (int i = 0; i < RF; ++i) {
+            const int cw = 16 * RF * wblk + 16 * i + fr;
+            cok[i] = cw < W;
+            cin_off[i] = (uint32_t)(cok[i] ? cw : 0) * (CT_CI * 2) + 16 * g;
+            cout_off[i] = (uint32_t)(cok[i] ? cw : 0) * (CT_CO * 2) + 8 * g;
+        }
+        const char* const xitem = xb + (int64_t)b * H * W * (CT_CI * 2);
+        char* const oitem = reinterpret_cast<char*>(d.out) + (int64_t)b * H * (KEEP ? 2 : 4) * W * (CT_CO * 2);
+        const int64_t rowB = (int64_t)W * (CT_CI * 2), orowB = (int64_t)W * (CT_CO * 2);
+        // row u through a buffer descriptor of that row (wave-uniform): a row outside the item has zero records and a
+        // column past W an out-of-range offset, so those loads return zeros (no per-lane 64-bit address selects)
+        uint32_t lofs[RF];
+#pragma unroll
+        for (int i = 0; i < RF; ++i) lofs[i] = cok[i] ? cin_off[i] : 0x40000000u;
+        auto load_row = [&](int u, bf16v8 (&F)[RF][3]) {
+            const bool uok = u >= 0 && u < H;                 // (wave-uniform)
+            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                (void*)(xitem + (uok ? (int64_t)u * rowB : 0)), (short)0, uok ? (int)rowB : 0, 0x00020000);
+#pragma unroll
+            for (int i = 0; i < RF; ++i)
+#pragma unroll
+                for (int s3 = 0; s3 < 3; ++s3)
+                    F[i][s3] = __builtin_bit_cast(bf16v8, __builtin_amdgcn_raw_buffer_load_b128(rs, lofs[i] + 64 * s3, 0, 0));
+        };
+        double r1 = 0.0, r2 = 0.0;
+        // one row u with taps (Fa, Fb, Fc) = rows (u-1, u, u+1); Fa is refilled with row u+2 once pair 0 is done
+        auto step = [&](int u, bf16v8 (&Fa)[RF][3], bf16v8 (&Fb)[RF][3], bf16v8 (&Fc)[RF][3]) {
+            float p1 = 0.f, p2 = 0.f;
+            auto epi = [&](int p) {
+#pragma unroll
+                for (int i = 0; i < RF; ++i) {
+#pragma unroll
+                    for (int j = 0; j < 6; ++j) {
+                        const int rho = 2 * p + j / 3, jj = j - 3 * (j / 3);
+                        const float4 bb = b4[jj];
+                        const float v0 = acc[i][j][0] + bb.x, v1 = acc[i][j][1] + bb.y;
+                        const float v2 = acc[i][j][2] + bb.z, v3 = acc[i][j][3] + bb.w;
+                        const float q1 = (v0 + v1) + (v2 + v3), q2 = (v0 * v0 + v1 * v1) + (v2 * v2 + v3 * v3);
+                        p1 += cok[i] ? q1 : 0.f;
+                        p2 += cok[i] ? q2 : 0.f;
+                        if (KEEP ? (rho == 1 || rho == 2) : true) {
+                            // output row (KEEP) 2u + rho - 1 / (all) 4u + rho of the item: a wave-uniform base
+                            const char* ob = oitem + (KEEP ? (int64_t)(2 * u + rho - 1) : (int64_t)(4 * u + rho)) * orowB;
+                            if (cok[i])
+                                *reinterpret_cast<uint2*>((char*)ob + cout_off[i] + 32 * jj) =
+                                    make_uint2(pack2bf(v0, v1), pack2bf(v2, v3));
+                        }
+                    }
+                }
+            };
+            mma(0, 0, Fa);
+            load_row(u + 2, Fa);                  // (row u+2 is the next step's upper tap)
+            mma(0, 1, Fb);
+            epi(0);
+            mma(1, 0, Fb);
+            mma(1, 1, Fc);
+            epi(1);
+            r1 += (double)p1;
+            r2 += (double)p2;
+        };
+        bf16v8 FA[RF][3], FB[RF][3], FC[RF][3];
+        load_row(u0 - 1, FA);
+        load_row(u0, FB);
+        load_row(u0 + 1, FC);
+#pragma unroll 1
+        for (int u = u0; u < u1; ++u) {
+            asm volatile("" : "+v"(wbe), "+v"(wbo));   // (weight fragment reads stay in the loop, not hoisted)
+            step(u, FA, FB, FC);                  // (FA now holds row u + 2)
+#pragma unroll
+            for (int i = 0; i < RF; ++i)          // rotate the taps: (u-1, u, u+1) <- (u, u+1, u+2)
+#pragma unroll
+                for (int s3 = 0; s3 < 3; ++s3) {
+                    const bf16v8 t = FA[i][s3];
+                    FA[i][s3] = FB[i][s3];
+                    FB[i][s3] = FC[i][s3];
+                    FC[i][s3] = t;
+                }
+        }
+        {
+            const double t1 = wave_sum_d(r1), t2 = wave_sum_d(r2);
+            if (lane == 0) {
+                atomicAdd(&d.stats[2 * b], t1);
+                atomicAdd(&d.stats[2 * b + 1], t2);
+            }
+        }
+        it += nwx;
+        if (it >= i1) break;
+    }
+}
+
 // A 32-row unit covers at most two items (its statistics split at one item boundary: bf / bl in the loop above), which
 // holds when an item has at least 32 rows, H*W >= 32: Tspec >= 6 for the freq branch (H*W = Tspec^2 after the
 // 259 -> Tspec resize), L >= 32 for the time branch.  Shorter inputs take the tiled GEMM (forward.cpp conv_t).
@@ -267,6 +433,12 @@ static void launch_ct4(const ConvT4Desc& d, int cus, hipStream_t s) {
     hipLaunchKernelGGL((convt4_kernel<KEEP, RF, NW>), dim3((unsigned)blocks), dim3(NW * 64), 0, s, d);
 }
 
+static bool ct4_walk() {               // (round-5 A/B: ATHD_CT4W=0 takes the unit kernel)
+    static int v = -1;
+    if (v < 0) { const char* e = getenv("ATHD_CT4W"); v = (e && e[0] == '0') ? 0 : 1; }
+    return v == 1;
+}
+
 int convt4_launch(const ConvT4Desc& d0, hipStream_t s) {
     if (!convt4_supported(CT_CI, CT_CO, d0.nb, d0.H, d0.W)) return -1;
     ConvT4Desc d = d0;
@@ -275,6 +447,23 @@ int convt4_launch(const ConvT4Desc& d0, hipStream_t s) {
     d.fd_hw = make_fastdiv((uint32_t)d.H * (uint32_t)d.W);
     d.M = (uint32_t)((int64_t)d.nb * d.H * d.W);
     const int cus = device_cus();
+    if (d.W >= 16 * CW_RF && ct4_walk()) {
+        // column walk: one workgroup (72 KB LDS) per CU, a multiple of 8
+        const int64_t items = (int64_t)d.nb * ((d.W + 16 * CW_RF - 1) / (16 * CW_RF)) * CW_SEG;
+        int64_t blocks = cus;
+        if (blocks * CW_NW > items) blocks = (items + CW_NW - 1) / CW_NW;
+        blocks = (blocks + 7) / 8 * 8;
+        KScope ks(s);
+        if (ks.on()) {
+            const double M = (double)d.M;
+            const double flops = 2.0 * M * (4 * CT_CO) * CT_KP;
+            const double bytes = M * CT_CI * 2 + M * (d.keep ? 2 : 4) * CT_CO * 2 + 4.0 * CT_CO * CT_KP * 2;
+            ks.begin(d.keep ? "convt4_walk_kernel<true>" : "convt4_walk_kernel<false>", flops, bytes);
+        }
+        if (d.keep) hipLaunchKernelGGL(convt4_walk_kernel<true>, dim3((unsigned)blocks), dim3(CW_NW * 64), 0, s, d);
+        else hipLaunchKernelGGL(convt4_walk_kernel<false>, dim3((unsigned)blocks), dim3(CW_NW * 64), 0, s, d);
+        return (int)hipGetLastError();
+    }
     // 2 row fragments per unit, 8 waves (2 per SIMD).  (1 fragment at 12 / 16 waves per workgroup measured slower.)
     if (d.keep) launch_ct4<true, 2, 8>(d, cus, s);
     else launch_ct4<false, 2, 8>(d, cus, s);

@@ -8,8 +8,8 @@
 // unfused path makes 8 HBM passes over the C x T activations per level (conv out, 2 x [conv3, 1x1 stats, 1x1
 // apply], rewrite); this makes one read of the level input and one write of its output.
 //
-// Work split (6 waves): wave w owns x channel tile ct = w % (C/16) (16 channels) and the m-tiles (16 positions)
-// mt = w / (C/16) + (6 / (C/16)) * i.  Every contraction is v_mfma_f32_16x16x32_bf16 with the weights as the A
+// Work split (level 0: 6 waves, level 1: 12): wave w owns x channel tile ct = w % (C/16) (16 channels) and the
+// m-tiles (16 positions) mt = w / (C/16) + (NW / (C/16)) * i.  Every contraction is v_mfma_f32_16x16x32_bf16 with the weights as the A
 // operand (rows = output channels) and the activations as the B operand, so a lane holds 4 consecutive channels
 // of one position:  acc[r] = out[channel 16*tile + 4*(lane>>4) + r][position 16*mt + (lane&15)].
 //   conv    K = 8*Cin  (level 0: the 8 taps x 4 CaC channels of the frame-major spectrogram, normalised on load;
@@ -18,7 +18,7 @@
 //   1x1     K = C/8 (padded to 32), N = 2C GLU-interleaved: rows 32*ct + [0,16) = 'a', + [16,32) = gate, so the
 //           lane's 'a' and gate values are the two halves of one x channel tile; computed twice (statistics pass,
 //           then the GroupNorm -> GLU -> LayerScale -> residual pass) instead of being kept
-//   rewrite K = C, N = 2C GLU-interleaved, output staged in LDS and stored as one contiguous T x C bf16 row.
+//   rewrite K = C, N = 2C GLU-interleaved, stored from registers (the waves of a position complete its row in L2).
 // Throughput (bf16) mode only; T <= 16 * FR_MT_MAX (the forward falls back to the unfused path otherwise).
 #include <cstdlib>
 
@@ -75,360 +75,18 @@ ATHD_DEV void gn_from_sums(float s1, float s2, float cnt, float& mean, float& rs
 
 #ifdef ATHD_FR_STAMP
 // measurement build only (-DATHD_FR_STAMP, tools/fr_stamps.py): s_memtime at the phase boundaries of
-// fenc_row0_kernel and fenc_row_kernel, wave 0 of every workgroup -> g_fr_stamp[block][16]; read back with athd_fr_stamps
+// fenc_row0_kernel and fenc_row1_kernel, wave 0 of every workgroup -> g_fr_stamp[block][16]; read back with athd_fr_stamps
 __device__ uint64_t g_fr_stamp[65536 * 16];
 #define FR_STAMP(k) do { if (threadIdx.x == 0) g_fr_stamp[(size_t)blockIdx.x * 16 + (k)] = __builtin_amdgcn_s_memtime(); } while (0)
 #else
 #define FR_STAMP(k) do { } while (0)
 #endif
 
-// NW waves per workgroup (6 for C = 48, 12 for C = 96: one workgroup per CU either way at C = 96 (114 KB LDS), so
-// twice the waves per row halve each wave's m-tiles (and the residual stream's registers: 36 instead of 68))
 #define FR_SCHED() __builtin_amdgcn_sched_barrier(0)      // (no instruction is scheduled across it)
-// GRAM: the 1x1 output's GroupNorm statistics from the 1x1 conv's moments (d.gram) instead of a statistics pass
-template <int CIN, int C, int NW, bool GRAM>
-__global__ __launch_bounds__(NW * 64, CIN == 4 ? 3 : 1) void fenc_row_kernel(const FencRowDesc d) {
-    constexpr int NCT = C / 16;                  // x channel tiles
-    constexpr int MG = NW / NCT;              // m-tile groups per channel tile
-    constexpr int MTW = (FR_MT_MAX + MG - 1) / MG;
-    constexpr int TPM = FR_MT_MAX * 16;
-    constexpr int H = C / 8;
-    constexpr int KC = 8 * CIN;                  // conv K
-    constexpr int KS = CIN == 4 ? 32 : 2 * CIN;  // conv K per LDS stage
-    constexpr int NSTAGE = KC / KS;
-    constexpr int XIN_P = KS + 8;                // LDS pitches (elements): +16 B keeps 16-row fragment reads
-    constexpr int XS_P = C + 8;                  //   on distinct banks
-    constexpr int HS_P = 40;
-    constexpr int K3 = 3 * C, K3S = (K3 + 31) / 32;
-    constexpr int KRS = (C + 31) / 32;
-    constexpr int C3I = (FR_MT_MAX + NW - 1) / NW;  // conv3 m-tiles per wave
-    // LDS: the conv input stage and the DConv hidden tile share one buffer (the conv is done before the first
-    // hidden tile is written); the output row is staged in xs once the rewrite has read it.  C = 48: 52.7 KB and
-    // <= 168 VGPRs (launch bound: 3 waves per SIMD), so two 6-wave workgroups share a CU.
-    constexpr int XIN_E = (TPM * XIN_P > TPM * HS_P) ? TPM * XIN_P : TPM * HS_P;
-    static_assert(C % 16 == 0 && NW % NCT == 0 && KC % KS == 0 && KS % 32 == 0 && (CIN == 4 || CIN % 8 == 0),
-                  "fenc_row shape");
-    static_assert(TPM * C <= (TPM + 2 * FR_HALO) * XS_P, "output staging fits xs");
-    __shared__ __attribute__((aligned(16))) bf16_t xin[XIN_E];
-    __shared__ __attribute__((aligned(16))) bf16_t xs[(TPM + 2 * FR_HALO) * XS_P];
-    bf16_t* const hs = xin;
-    __shared__ float red[4][2 * NW];
-    __shared__ float gsh[2][H * H + 2 * H + 2];  // the 1x1 convs' moments (when d.gram is set)
-
-    // row r -> block: the 8 XCDs each take a contiguous run of rows, so neighbouring output rows (which share 4 of
-    // their 8 input rows) run on one XCD and re-read those rows from its L2
-    const int R = d.B * d.Fout;
-    const int per = (R + 7) / 8;
-    const int r = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
-    if (r >= R) return;
-    const int b = r / d.Fout, f = r % d.Fout;
-    const int T = d.T;
-    const int MT = (T + 15) >> 4;
-    const int TP = MT * 16;
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const int l15 = lane & 15, l4 = lane >> 4;
-    const int ct = wave % NCT, mg = wave / NCT;
-    const int cb = ct * 16 + 4 * l4;             // first of this lane's 4 x channels
-
-    FR_STAMP(0);
-    if constexpr (GRAM) {
-        for (int i = tid; i < 2 * (H * H + 2 * H + 2); i += NW * 64) {
-            const int l = i / (H * H + 2 * H + 2), e = i % (H * H + 2 * H + 2);
-            gsh[l][e] = d.gram[l][e];
-        }
-    }
-    // zero xs (conv3 zero padding: halo rows and positions >= T)
-    for (int i = tid; i < (TPM + 2 * FR_HALO) * XS_P / 8; i += (NW * 64))
-        reinterpret_cast<uint4*>(xs)[i] = make_uint4(0u, 0u, 0u, 0u);
-
-    // ---------------------------------------------------------------- conv (8,1)/(4,1)/(2,0) + GELU
-    f32x4_t xr[MTW];
-#pragma unroll
-    for (int i = 0; i < MTW; ++i) xr[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-    for (int s = 0; s < NSTAGE; ++s) {
-        if (s > 0) __syncthreads();
-        for (int c = tid; c < TP * (KS / 8); c += (NW * 64)) {
-            const int m = c / (KS / 8), q = c - m * (KS / 8);
-            uint4 v = make_uint4(0u, 0u, 0u, 0u);
-            if constexpr (CIN == 4) {
-                // level 0: k = tap * 4 + ch over the frame-major, L|R-interleaved CaC spectrogram specT[b][t][F][4];
-                // chunk q = taps 2q, 2q+1 = input rows 4f-2+2q, +1 (both in or both out of [0, Fin))
-                const int fi = 4 * f - 2 + 2 * q;
-                if (m < T && fi >= 0 && fi + 1 < d.Fin) {
-                    const float* p = (const float*)d.in + (((int64_t)b * T + m) * d.Fin + fi) * 4;
-                    const float4 u0 = *reinterpret_cast<const float4*>(p);
-                    const float4 u1 = *reinterpret_cast<const float4*>(p + 4);
-                    const float sub = d.a_norm[2 * b], rdv = 1.0f / d.a_norm[2 * b + 1];
-                    v = make_uint4(pack2bf((u0.x - sub) * rdv, (u0.y - sub) * rdv), pack2bf((u0.z - sub) * rdv, (u0.w - sub) * rdv),
-                                   pack2bf((u1.x - sub) * rdv, (u1.y - sub) * rdv), pack2bf((u1.z - sub) * rdv, (u1.w - sub) * rdv));
-                }
-            } else {
-                const int k0 = s * KS + q * 8;
-                const int tap = k0 / CIN, ci = k0 - tap * CIN;
-                const int fi = 4 * f - 2 + tap;
-                if (m < T && fi >= 0 && fi < d.Fin)
-                    v = *reinterpret_cast<const uint4*>((const bf16_t*)d.in + (((int64_t)b * d.Fin + fi) * T + m) * CIN + ci);
-            }
-            *reinterpret_cast<uint4*>(&xin[m * XIN_P + q * 8]) = v;
-        }
-        __syncthreads();
-#pragma unroll
-        for (int ks = 0; ks < KS / 32; ++ks) {
-            const bf16x8_t wf = ldfrag(d.wc + (int64_t)(ct * 16 + l15) * d.wc_ld + s * KS + ks * 32 + 8 * l4);
-#pragma unroll
-            for (int i = 0; i < MTW; ++i) {
-                const int mt = mg + MG * i;
-                if (mt < MT) xr[i] = mfma(wf, ldfrag(&xin[(mt * 16 + l15) * XIN_P + ks * 32 + 8 * l4]), xr[i]);
-            }
-        }
-    }
-    FR_STAMP(1);
-    {
-        const float4 bc = *reinterpret_cast<const float4*>(d.bc + cb);
-        const float bcv[4] = {bc.x, bc.y, bc.z, bc.w};
-#pragma unroll
-        for (int i = 0; i < MTW; ++i) {
-            const int mt = mg + MG * i;
-            const int m = mt * 16 + l15;
-            if (mt >= MT) continue;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) xr[i][q] = m < T ? gelu_fast(xr[i][q] + bcv[q]) : 0.f;
-            st4bf(&xs[(FR_HALO + m) * XS_P + cb], xr[i][0], xr[i][1], xr[i][2], xr[i][3]);
-        }
-    }
-    __syncthreads();
-    FR_STAMP(2);
-    // the conv input stage is dead: zero the hidden tile's K padding columns 16..31 (columns 0..15 are written by
-    // every conv3 pass, zeros past H included)
-    for (int i = tid; i < TPM * 2; i += (NW * 64))
-        *reinterpret_cast<uint4*>(&hs[(i >> 1) * HS_P + 16 + 8 * (i & 1)]) = make_uint4(0u, 0u, 0u, 0u);
-
-    // ---------------------------------------------------------------- DConv: x += LayerScale(GLU(GN(1x1(GELU(GN(conv3(x)))))))
-#pragma unroll 1
-    for (int dd = 0; dd < 2; ++dd) {
-        const int dil = 1 << dd;
-        // conv3 (C -> H, 3 taps, dilation dil, zero padding) on m-tiles wave, wave + 6, wave + 12
-        f32x4_t ha[C3I];
-#pragma unroll
-        for (int i = 0; i < C3I; ++i) ha[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int ks = 0; ks < K3S; ++ks) {
-            const int k0 = ks * 32 + 8 * l4;
-            const bf16x8_t wf = ldfrag(d.w3[dd] + (int64_t)l15 * d.w3_ld + k0);   // rows >= H and k >= 3C are zero
-            const int tap = k0 / C, c0 = k0 - tap * C;
-#pragma unroll
-            for (int i = 0; i < C3I; ++i) {
-                const int mt = wave + NW * i;
-                if (mt >= MT) continue;
-                bf16x8_t xf = bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
-                if (k0 < K3) xf = ldfrag(&xs[(FR_HALO + mt * 16 + l15 + (tap - 1) * dil) * XS_P + c0]);
-                ha[i] = mfma(wf, xf, ha[i]);
-            }
-        }
-        float hb[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) hb[q] = (4 * l4 + q < H) ? d.b3[dd][4 * l4 + q] : 0.f;
-        float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-        for (int i = 0; i < C3I; ++i) {
-            const int mt = wave + NW * i;
-            const int m = mt * 16 + l15;
-            if (mt >= MT || m >= T) continue;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                if (4 * l4 + q < H) {
-                    const float v = ha[i][q] + hb[q];
-                    s1 += v;
-                    s2 += v * v;
-                }
-            }
-        }
-        FR_STAMP(3 + 4 * dd);
-        block_sum2<NW>(s1, s2, red[2 * dd]);
-        FR_STAMP(4 + 4 * dd);
-        float hm, hr;
-        gn_from_sums(s1, s2, (float)(H * T), hm, hr);
-#pragma unroll
-        for (int i = 0; i < C3I; ++i) {
-            const int mt = wave + NW * i;
-            if (mt >= MT) continue;
-            float g[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int j = 4 * l4 + q;
-                g[q] = j < H ? gelu_fast((ha[i][q] + hb[q] - hm) * hr * d.g1w[dd][j] + d.g1b[dd][j]) : 0.f;
-            }
-            st4bf(&hs[(mt * 16 + l15) * HS_P + 4 * l4], g[0], g[1], g[2], g[3]);
-        }
-        s1 = 0.f;
-        s2 = 0.f;
-        if constexpr (GRAM) {
-            // the 1x1 output's GroupNorm statistics from the moments of the 1x1 conv (see fenc_row0_kernel) from the
-            // hidden rows this wave wrote (in-wave LDS order): lane (l15, l4) takes rows j = l4, l4 + 4, .. of the
-            // quadratic form for position l15 of each of the wave's m-tiles (the workgroup sum adds the parts)
-            const float* G = gsh[dd];
-            {
-#pragma unroll
-                for (int i = 0; i < C3I; ++i) {
-                    const int mt = wave + NW * i;
-                    if (mt >= MT || mt * 16 + l15 >= T) continue;
-                    FR_SCHED();
-                    float x[16];
-                    const uint4* hr_ = reinterpret_cast<const uint4*>(&hs[(mt * 16 + l15) * HS_P]);
-#pragma unroll
-                    for (int u = 0; u < (H + 7) / 8; ++u) {
-                        const uint4 hq = hr_[u];
-                        const uint32_t w4[4] = {hq.x, hq.y, hq.z, hq.w};
-#pragma unroll
-                        for (int e = 0; e < 4; ++e) {
-                            x[8 * u + 2 * e] = __uint_as_float(w4[e] << 16);
-                            x[8 * u + 2 * e + 1] = __uint_as_float(w4[e] & 0xFFFF0000u);
-                        }
-                    }
-                    float q = 0.f, lv = 0.f, lw = 0.f;
-#pragma unroll
-                    for (int jj = 0; jj < (H + 3) / 4; ++jj) {
-                        const int j = 4 * jj + l4;
-                        if (j >= H) break;
-                        const float xj = __uint_as_float((uint32_t)hs[(mt * 16 + l15) * HS_P + j] << 16);
-                        float t = 0.f;
-#pragma unroll
-                        for (int kk = 0; kk < H; ++kk) t += G[j * H + kk] * x[kk];
-                        q += xj * t;
-                        lv += G[H * H + j] * xj;
-                        lw += G[H * H + H + j] * xj;
-                    }
-                    s1 += (l4 == 0 ? G[H * H + 2 * H] : 0.f) + lw;
-                    s2 += (l4 == 0 ? G[H * H + 2 * H + 1] : 0.f) + (2.f * lv + q);
-                }
-            }
-        }
-        if constexpr (!GRAM) __syncthreads();
-
-        // 1x1 (H -> 2C), GLU-interleaved rows: 'a' = 32 ct + l15, gate = 32 ct + 16 + l15; K = 32 (H zero-padded)
-        const bf16x8_t wa = ldfrag(d.w1[dd] + (int64_t)(32 * ct + l15) * d.w1_ld + 8 * l4);
-        const bf16x8_t wg = ldfrag(d.w1[dd] + (int64_t)(32 * ct + 16 + l15) * d.w1_ld + 8 * l4);
-        const int pa = 32 * ct + 4 * l4;           // packed column of this lane's 'a' values; gate = pa + 16
-        float ba[4], bg[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            ba[q] = d.b1[dd][pa + q];
-            bg[q] = d.b1[dd][pa + 16 + q];
-        }
-        if constexpr (!GRAM) {                      // statistics pass: the 1x1 computed once more
-#pragma unroll
-            for (int i = 0; i < MTW; ++i) {
-                const int mt = mg + MG * i;
-                const int m = mt * 16 + l15;
-                if (mt >= MT) continue;               // wave-uniform: the MFMAs run on full waves
-                const bf16x8_t hf = ldfrag(&hs[(mt * 16 + l15) * HS_P + 8 * l4]);
-                const f32x4_t z = f32x4_t{0.f, 0.f, 0.f, 0.f};
-                const f32x4_t ya = mfma(wa, hf, z), yg = mfma(wg, hf, z);
-                if (m >= T) continue;
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const float a = ya[q] + ba[q], g = yg[q] + bg[q];
-                    s1 += a + g;
-                    s2 += a * a + g * g;
-                }
-            }
-        }
-        block_sum2<NW>(s1, s2, red[2 * dd + 1]);      // (its barrier also publishes hs)
-        FR_STAMP(5 + 4 * dd);
-        float ym, yr;
-        gn_from_sums(s1, s2, (float)(2 * C * T), ym, yr);
-        // (y + b - mean) * rstd * w + beta as y * wa + ca, the LayerScale folded into the 'a' half and -log2(e) into
-        // the gate half: x += a' / (1 + 2^g')
-        float wav[4], cav[4], wgv[4], cgv[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const float sc = d.scale[dd][cb + q];
-            const float wa_ = d.g2w[dd][pa + q] * yr, wg_ = d.g2w[dd][pa + 16 + q] * yr;
-            wav[q] = wa_ * sc;
-            cav[q] = ((ba[q] - ym) * wa_ + d.g2b[dd][pa + q]) * sc;
-            wgv[q] = wg_ * -1.4426950408889634f;
-            cgv[q] = ((bg[q] - ym) * wg_ + d.g2b[dd][pa + 16 + q]) * -1.4426950408889634f;
-        }
-#pragma unroll
-        for (int i = 0; i < MTW; ++i) {
-            const int mt = mg + MG * i;
-            const int m = mt * 16 + l15;
-            if (mt >= MT) continue;
-            const bf16x8_t hf = ldfrag(&hs[(mt * 16 + l15) * HS_P + 8 * l4]);
-            const f32x4_t z = f32x4_t{0.f, 0.f, 0.f, 0.f};
-            const f32x4_t ya = mfma(wa, hf, z), yg = mfma(wg, hf, z);
-            if (m >= T) continue;                 // positions >= T stay 0 in xr and xs
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const float a = ya[q] * wav[q] + cav[q];
-                const float g = yg[q] * wgv[q] + cgv[q];
-                xr[i][q] = a * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(g)) + xr[i][q];
-            }
-            st4bf(&xs[(FR_HALO + m) * XS_P + cb], xr[i][0], xr[i][1], xr[i][2], xr[i][3]);
-        }
-        __syncthreads();
-        FR_STAMP(6 + 4 * dd);
-    }
-
-    // ---------------------------------------------------------------- rewrite 1x1 (C -> 2C) + GLU (+ freq embedding)
-    {
-        const int pa = 32 * ct + 4 * l4;
-        float ba[4], bg[4], ra[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            ba[q] = d.br[pa + q];
-            bg[q] = d.br[pa + 16 + q];
-            if (d.row_add) ra[q] = d.row_add[(int64_t)f * C + cb + q];
-        }
-        bf16x8_t wa[KRS], wg[KRS];
-#pragma unroll
-        for (int ks = 0; ks < KRS; ++ks) {
-            wa[ks] = ldfrag(d.wr + (int64_t)(32 * ct + l15) * d.wr_ld + ks * 32 + 8 * l4);
-            wg[ks] = ldfrag(d.wr + (int64_t)(32 * ct + 16 + l15) * d.wr_ld + ks * 32 + 8 * l4);
-        }
-        uint2 ov[MTW];           // the wave's output values (bf16 x 4 per m-tile), held until xs is free
-#pragma unroll
-        for (int i = 0; i < MTW; ++i) {
-            const int mt = mg + MG * i;
-            const int m = mt * 16 + l15;
-            ov[i] = make_uint2(0u, 0u);
-            if (mt >= MT) continue;
-            f32x4_t za = f32x4_t{0.f, 0.f, 0.f, 0.f}, zg = za;
-#pragma unroll
-            for (int ks = 0; ks < KRS; ++ks) {
-                const int k0 = ks * 32 + 8 * l4;
-                bf16x8_t xf = bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
-                if (k0 < C) xf = ldfrag(&xs[(FR_HALO + m) * XS_P + k0]);
-                za = mfma(wa[ks], xf, za);
-                zg = mfma(wg[ks], xf, zg);
-            }
-            if (m < T) {
-                float o[4];
-#pragma unroll
-                for (int q = 0; q < 4; ++q) o[q] = (za[q] + ba[q]) * sigmoid_fast(zg[q] + bg[q]) + ra[q];
-                ov[i] = make_uint2(pack2bf(o[0], o[1]), pack2bf(o[2], o[3]));
-            }
-        }
-        FR_STAMP(11);
-        __syncthreads();         // every wave has read xs: stage the output row [T][C] there
-        bf16_t* ob = xs;
-#pragma unroll
-        for (int i = 0; i < MTW; ++i) {
-            const int mt = mg + MG * i;
-            const int m = mt * 16 + l15;
-            if (mt < MT && m < T) *reinterpret_cast<uint2*>(&ob[m * C + cb]) = ov[i];
-        }
-        __syncthreads();
-        bf16_t* dst = d.out + ((int64_t)b * d.Fout + f) * (int64_t)T * C;
-        for (int i = tid; i < T * C / 8; i += (NW * 64))
-            reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(ob)[i];
-        FR_STAMP(12);
-    }
-}
 
 // ---------------------------------------------------------------------------------------------------------
-// Level 0 (Cin = 4 CaC channels, C = 48) as a branch-free kernel.  Same contractions and arithmetic as
-// fenc_row_kernel<4, 48>, restructured for latency:
+// Level 0 (Cin = 4 CaC channels, C = 48) as a branch-free kernel: the contractions and arithmetic above (round 2's
+// generic kernel), restructured for latency:
 //   - a fixed 18-tile (288-position) row: wave w owns channel tile w % 3 and m-tiles w / 3 + 2 i (i < 9), conv3
 //     m-tiles w + 6 i (i < 3); positions >= T are computed and masked with selects instead of per-tile branches
 //     (the data-dependent `mt < MT` / `m < T` branches of the generic kernel cost exec-mask save/restore and
@@ -780,30 +438,27 @@ __global__ __launch_bounds__(FR_NT, 4) void fenc_row0_kernel(const FencRowDesc d
             ov[i] = make_uint2(pack2bf(o[0], o[1]), pack2bf(o[2], o[3]));
         }
         FR_STAMP(11);
-        __syncthreads();         // every wave has read xs: stage the output row [T][C] there
-        bf16_t* ob = xs;
+        // straight from registers (8 B per lane, 32 B per position and wave-instruction; the 3 channel-tile waves of a
+        // position complete its 96-B row in L2): no LDS staging and its two barriers
+        bf16_t* dst = d.out + ((int64_t)b * d.Fout + f) * (int64_t)T * C;
+        uint2* d4 = d.out4 ? reinterpret_cast<uint2*>(d.out4 + ((int64_t)b * d.Fout + f) * (int64_t)T * 4) : nullptr;
 #pragma unroll
         for (int i = 0; i < MTW; ++i) {
             const int m = (mg + 2 * i) * 16 + l15;
-            if (m < T) *reinterpret_cast<uint2*>(&ob[m * C + cb]) = ov[i];
-        }
-        __syncthreads();
-        bf16_t* dst = d.out + ((int64_t)b * d.Fout + f) * (int64_t)T * C;
-        for (int i = tid; i < T * C / 8; i += FR_NT)
-            reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(ob)[i];
-        if (d.out4) {            // the decoder's level-3 skip reads channels 0..3 only: a compact copy
-            uint2* d4 = reinterpret_cast<uint2*>(d.out4 + ((int64_t)b * d.Fout + f) * (int64_t)T * 4);
-            for (int m = tid; m < T; m += FR_NT) d4[m] = *reinterpret_cast<const uint2*>(&ob[m * C]);
+            if (m < T) {
+                *reinterpret_cast<uint2*>(&dst[(int64_t)m * C + cb]) = ov[i];
+                if (cb == 0 && d4) d4[m] = ov[i];    // the decoder's level-3 skip reads channels 0..3: a compact copy
+            }
         }
         FR_STAMP(12);
     }
 }
 
 // ---------------------------------------------------------------------------------------------------------
-// Level 1 (Cin = 48, C = 96, 12 waves, one workgroup per CU): the generic kernel's contractions and arithmetic with the
-// latency taken out of its two longest phases (s_memtime phase stamps, tools/fr_stamps.py FR_LEVEL=1: the four
-// register-staged conv stages took 36 % of a row, the two conv3 passes with their weights read from global memory
-// another 17 %):
+// Level 1 (Cin = 48, C = 96, 12 waves, one workgroup per CU; round 5, replacing the generic kernel of rounds 2-4, 1.40
+// -> 1.05 ms per launch): the contractions and arithmetic above with the latency taken out of the generic kernel's two
+// longest phases (s_memtime phase stamps, tools/fr_stamps.py FR_LEVEL=1: the four register-staged conv stages took
+// 36 % of a row, the two conv3 passes with their weights read from global memory another 17 %):
 //   - conv: one stage per tap.  The [T][48] input rows of one frequency row are one contiguous slab of T x 96 B; it is
 //     moved by LDS-DMA (global_load_lds_dwordx4, no VGPR round trip) as a linear copy into a 3-deep ring of 272-row
 //     images (96-B rows; rows >= T and taps outside [0, Fin) from a zero page), so taps t + 1 and t + 2 are in flight
@@ -811,7 +466,8 @@ __global__ __launch_bounds__(FR_NT, 4) void fenc_row0_kernel(const FencRowDesc d
 //     the same way one tap ahead in a 2-deep ring.  Nothing but LDS-DMA is in flight in the loop: a VGPR-returning
 //     global load among the DMAs makes the compiler's wait counting give up (vmcnt(0) before the next MFMA, i.e. the
 //     ring serialised).  Every wave issues exactly 4 pieces per stage (surplus pieces load the zero page into a
-//     scratch KB), so the explicit counted waits are exact.  A tap's 48 channels are one 16x16x32 and one 16x16x16 MFMA.
+//     scratch KB), so the explicit counted waits are exact.  A tap's 48 channels are two 16x16x32 MFMAs (the second
+//     half zero weights).
 //   - conv3 weights of both DConv layers moved into the dead tap ring at the end of the conv and read from LDS.
 //   - the 1x1 weights issued before the barrier that precedes their use.
 namespace {
@@ -830,12 +486,18 @@ constexpr int F1_W3_P = 3 * F1_C + 8;           // conv3 weight rows in LDS (ele
 constexpr int F1_W3C = F1_W3_P / 8;             // 37 chunks per conv3 row (36 used)
 constexpr int F1_W3PC = (2 * 16 * F1_W3C * 16 + 1023) / 1024;   // 19 pieces for both layers
 constexpr int F1_K3S = 3 * F1_C / 32;           // 9 conv3 K-steps
+constexpr int F1_WRC = 13;                      // rewrite weight rows in LDS: 13 chunks (208 B, 192 used; conflict-free)
+constexpr int F1_WRB = 2 * F1_C * F1_WRC * 16;  // rewrite weight image (bytes)
+constexpr int F1_W3B = 2 * 16 * F1_W3_P * 2;    // conv3 weight image (bytes)
+constexpr int F1_LPC = F1_WRB / 1024;           // DMA pieces of the rewrite weight image
 constexpr int F1_C3I = (FR_MT_MAX + F1_NW - 1) / F1_NW;
 constexpr int F1_GSZ = F1_H * F1_H + 2 * F1_H + 2;
-static_assert(F1_TPM * 96 + 64 <= F1_STB && F1_TPM * F1_HS_P * 2 <= F1_STB && F1_W3PC * 1024 <= F1_STB,
+static_assert((F1_TPM - 1) * 96 + 128 <= F1_STB && F1_TPM * F1_HS_P * 2 <= F1_STB && F1_W3PC * 1024 <= F1_STB,
               "fenc_row1 LDS layout");
-static_assert(F1_PIECES <= 3 * F1_NW && F1_WPC <= F1_NW && F1_W3PC <= 2 * F1_NW, "DMA pieces per wave");
-typedef short short4_t __attribute__((ext_vector_type(4)));
+static_assert(F1_PIECES <= 3 * F1_NW && F1_WPC <= F1_NW && F1_W3PC <= 2 * F1_NW && F1_LPC <= 4 * F1_NW,
+              "DMA pieces per wave");
+// after the conv the ring is reused: slot 0 = hidden tile, slot 1 + weight ring = rewrite weights, slot 2 = conv3 weights
+static_assert(F1_WRB <= F1_STB + 2 * F1_WSB && F1_W3B <= F1_STB && F1_WRB % 1024 == 0, "late images");
 typedef __attribute__((address_space(3))) void f1_lds_void;
 typedef __attribute__((address_space(1))) void f1_gbl_void;
 __device__ __attribute__((aligned(64))) uint4 g_zero_f1[4];
@@ -844,15 +506,26 @@ __device__ __attribute__((aligned(64))) uint4 g_zero_f1[4];
 __global__ __launch_bounds__(F1_NT, 1) void fenc_row1_kernel(const FencRowDesc d) {
     constexpr int C = F1_C, H = F1_H, NW = F1_NW, MG = F1_MG, MTW = F1_MTW, TPM = F1_TPM;
     constexpr int XS_P = F1_XS_P, HS_P = F1_HS_P;
-    // tap image ring; after the conv: the hidden tile (slot 0) and the conv3 weights (slot 2)
-    __shared__ __attribute__((aligned(16))) char stg[F1_RING * F1_STB];
-    __shared__ __attribute__((aligned(16))) char wring[2 * F1_WSB];
-    __shared__ __attribute__((aligned(16))) bf16_t xs[(TPM + 2 * FR_HALO) * XS_P];
-    __shared__ float red[4][2 * NW];
-    __shared__ float gsh[2][F1_GSZ];
-    __shared__ __attribute__((aligned(16))) char dma_sink[1024];
+    // [slot 0 | slot 1 | tap weight ring (2) | slot 2]: the 3-deep tap image ring and the weight ring; after the conv
+    // the hidden tile (slot 0), the rewrite weights (slot 1 + weight ring) and the conv3 weights (slot 2)
+    // One LDS array with the LDS-DMA destinations first (the rings, then the scratch KB the surplus pieces go to),
+    // then the residual image and the small tables
+    constexpr int O_SINK = 3 * F1_STB + 2 * F1_WSB, O_XS = O_SINK + 1024;
+    constexpr int O_RED = O_XS + (TPM + 2 * FR_HALO) * XS_P * 2, O_GSH = O_RED + 4 * 2 * NW * 4;
+    constexpr int O_P3 = O_GSH + 2 * F1_GSZ * 4, O_END = O_P3 + 2 * 3 * 16 * 4;
+    __shared__ __attribute__((aligned(1024))) char smem1[O_END];
+    char* const stg = smem1;
+    char* const wring = stg + 2 * F1_STB;
+    char* const dma_sink = smem1 + O_SINK;
+    auto slot = [&](int k) -> char* { return stg + (k == 2 ? 2 * F1_STB + 2 * F1_WSB : k * F1_STB); };
+    bf16_t* const xs = reinterpret_cast<bf16_t*>(smem1 + O_XS);
+    float (*const red)[2 * NW] = reinterpret_cast<float (*)[2 * NW]>(smem1 + O_RED);
+    float (*const gsh)[F1_GSZ] = reinterpret_cast<float (*)[F1_GSZ]>(smem1 + O_GSH);
+    float (*const p3)[3][16] = reinterpret_cast<float (*)[3][16]>(smem1 + O_P3);   // conv3 bias, GN affine (padded)
     bf16_t* const hs = reinterpret_cast<bf16_t*>(stg);
-    const bf16_t* const w3s = reinterpret_cast<const bf16_t*>(stg + 2 * F1_STB);   // [2][16][F1_W3_P]
+    char* const late2 = stg + 2 * F1_STB + 2 * F1_WSB;                              // slot 2
+    const bf16_t* const w3s = reinterpret_cast<const bf16_t*>(late2);               // [2][16][F1_W3_P]
+    const char* const wrs = stg + F1_STB;                                           // [2C][F1_WRC chunks]
 
     FR_STAMP(0);
     const int R = d.B * d.Fout;
@@ -878,7 +551,7 @@ __global__ __launch_bounds__(F1_NT, 1) void fenc_row1_kernel(const FencRowDesc d
         const int fi = 4 * f - 2 + t;
         const bool fok = fi >= 0 && fi < d.Fin;
         const char* slab = (const char*)d.in + ((int64_t)b * d.Fin + (fok ? fi : 0)) * (int64_t)T * (F1_CIN * 2);
-        char* dst = stg + (t % F1_RING) * F1_STB;
+        char* dst = slot(t % F1_RING);
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
             const int p = wave + NW * j;
@@ -909,19 +582,42 @@ __global__ __launch_bounds__(F1_NT, 1) void fenc_row1_kernel(const FencRowDesc d
             const bool ok = p < F1_W3PC && dd < 2 && ch < 3 * C / 8;
             const char* w3g = dd ? w3g1 : w3g0;
             dma(ok ? w3g + ((int64_t)row * d.w3_ld + 8 * ch) * 2 : zero,
-                p < F1_W3PC ? stg + 2 * F1_STB + 1024 * p : dma_sink);
+                p < F1_W3PC ? late2 + 1024 * p : dma_sink);
+        }
+    };
+    // after the conv: the rewrite weights [2C][C] (rows of F1_WRC chunks), 4 pieces per wave
+    const char* const wrg0 = launder((const char*)d.wr);
+    auto dma_late = [&]() {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int p = wave + NW * j;
+            const int e = (1024 * p + 16 * lane) >> 4;                  // 16-B chunk of the image
+            const int row = e / F1_WRC, ch = e - row * F1_WRC;
+            const bool ok = p < F1_LPC && ch < C / 8;
+            dma(ok ? wrg0 + ((int64_t)row * d.wr_ld + 8 * ch) * 2 : zero, p < F1_LPC ? (char*)wrs + 1024 * p : dma_sink);
         }
     };
     for (int i = tid; i < 2 * F1_GSZ; i += F1_NT) gsh[i / F1_GSZ][i % F1_GSZ] = d.gram[i / F1_GSZ][i % F1_GSZ];
+    if (tid < 2 * 3 * 16) {      // (in LDS: a VGPR-returning load while the late DMA is in flight would wait it out)
+        const int dd = tid / 48, k = (tid / 16) % 3, j = tid % 16;
+        const float* src = k == 0 ? d.b3[dd] : k == 1 ? d.g1w[dd] : d.g1b[dd];
+        p3[dd][k][j] = j < H ? src[j] : 0.f;
+    }
     for (int i = tid; i < (TPM + 2 * FR_HALO) * XS_P / 8; i += F1_NT)
         reinterpret_cast<uint4*>(xs)[i] = make_uint4(0u, 0u, 0u, 0u);
     const float4 bc = *reinterpret_cast<const float4*>(d.bc + cb);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");          // (only LDS-DMA in flight from here on)
     // VMEM issue order, for the counted waits below: img(0), wt(0), img(1); stage t: wt(t + 1), img(t + 2) (stage 6:
     // wt(7), the conv3 weights)
+    // (the counted waits rely on this issue order: a compiler fence between the groups keeps the scheduler from
+    // interleaving them - they are independent memory operations to it)
+    auto order = []() { asm volatile("" ::: "memory"); };
     dma_tap(0);
+    order();
     dma_wt(0);
+    order();
     dma_tap(1);
+    order();
 
     // ---------------------------------------------------------------- conv (8,1)/(4,1)/(2,0): 8 tap stages
     f32x4_t xr[MTW];
@@ -941,12 +637,19 @@ __global__ __launch_bounds__(F1_NT, 1) void fenc_row1_kernel(const FencRowDesc d
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
         if (t + 1 < 8) dma_wt(t + 1);
+        order();
         if (t + 2 < 8) dma_tap(t + 2);                        // into the slot tap t - 1 was read from
         if (t == 6) dma_w3();                                 // slot 2 held tap 5
-        const char* img = stg + (t % F1_RING) * F1_STB;
+        order();
+        const char* img = slot(t % F1_RING);
         const char* wl = wring + (t & 1) * F1_WSB + wrow;
+        // K-step 0: channels 0..31; K-step 1: channels 32..47 in lanes l4 = 0, 1 and zero weights in l4 = 2 (the row's
+        // zero padding) and l4 = 3 (the next row's first chunk, zeroed here), so the B lanes l4 >= 2 - the next image
+        // row's first channels - contribute nothing.  (A 16x16x16 MFMA for channels 32..47 in the same accumulation
+        // chain made the results nondeterministic on gfx950: measured, not kept.)
         const bf16x8_t a0 = *reinterpret_cast<const bf16x8_t*>(wl + 16 * l4);
-        const short4_t a1 = *reinterpret_cast<const short4_t*>(wl + 64 + 8 * l4);
+        bf16x8_t a1 = *reinterpret_cast<const bf16x8_t*>(wl + 64 + 16 * l4);
+        if (l4 == 3) a1 = bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
         for (int i = 0; i < MTW; ++i) {
             // branch-free: a tile past MT reads rows clamped into the image and its accumulators are never used
@@ -954,8 +657,7 @@ __global__ __launch_bounds__(F1_NT, 1) void fenc_row1_kernel(const FencRowDesc d
             if (i % 3 == 0) FR_SCHED();           // (else all nine tiles' fragment reads are hoisted: spills)
             const char* rp = img + (mt * 16 + l15) * (F1_CIN * 2);
             xr[i] = mfma(a0, *reinterpret_cast<const bf16x8_t*>(rp + 16 * l4), xr[i]);
-            xr[i] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a1, *reinterpret_cast<const short4_t*>(rp + 64 + 8 * l4),
-                                                             xr[i], 0, 0, 0);
+            xr[i] = mfma(a1, *reinterpret_cast<const bf16x8_t*>(rp + 64 + 16 * l4), xr[i]);
         }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");          // the conv3 weights landed (published by the barrier below)
@@ -974,6 +676,7 @@ __global__ __launch_bounds__(F1_NT, 1) void fenc_row1_kernel(const FencRowDesc d
     }
     __syncthreads();
     FR_STAMP(2);
+    dma_late();              // (the ring is dead; waited for before the last DConv barrier)
     // the tap ring is dead: zero the hidden tile's K padding columns 16..31 (columns 0..15 are written by every conv3)
     for (int i = tid; i < TPM * 2; i += F1_NT)
         *reinterpret_cast<uint4*>(&hs[(i >> 1) * HS_P + 16 + 8 * (i & 1)]) = make_uint4(0u, 0u, 0u, 0u);
@@ -1000,10 +703,9 @@ __global__ __launch_bounds__(F1_NT, 1) void fenc_row1_kernel(const FencRowDesc d
         float hb[4], g1w[4], g1b[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            const int j = 4 * l4 + q < H ? 4 * l4 + q : H - 1;
-            hb[q] = d.b3[dd][j];
-            g1w[q] = d.g1w[dd][j];
-            g1b[q] = d.g1b[dd][j];
+            hb[q] = p3[dd][0][4 * l4 + q];
+            g1w[q] = p3[dd][1][4 * l4 + q];
+            g1b[q] = p3[dd][2][4 * l4 + q];
         }
         float s1 = 0.f, s2 = 0.f;
 #pragma unroll
@@ -1077,8 +779,6 @@ __global__ __launch_bounds__(F1_NT, 1) void fenc_row1_kernel(const FencRowDesc d
         const bf16x8_t wa = ldfrag(d.w1[dd] + (int64_t)(32 * ct + l15) * d.w1_ld + 8 * l4);
         const bf16x8_t wg = ldfrag(d.w1[dd] + (int64_t)(32 * ct + 16 + l15) * d.w1_ld + 8 * l4);
         const int pa = 32 * ct + 4 * l4;
-        block_sum2<NW>(s1, s2, red[2 * dd + 1]);      // (its barrier also publishes hs)
-        FR_STAMP(5 + 4 * dd);
         const float4 ba4 = *reinterpret_cast<const float4*>(d.b1[dd] + pa);
         const float4 bg4 = *reinterpret_cast<const float4*>(d.b1[dd] + pa + 16);
         const float4 gwa = *reinterpret_cast<const float4*>(d.g2w[dd] + pa);
@@ -1086,6 +786,8 @@ __global__ __launch_bounds__(F1_NT, 1) void fenc_row1_kernel(const FencRowDesc d
         const float4 gwg = *reinterpret_cast<const float4*>(d.g2w[dd] + pa + 16);
         const float4 gbg = *reinterpret_cast<const float4*>(d.g2b[dd] + pa + 16);
         const float4 sc4 = *reinterpret_cast<const float4*>(d.scale[dd] + cb);
+        block_sum2<NW>(s1, s2, red[2 * dd + 1]);      // (its barrier also publishes hs)
+        FR_STAMP(5 + 4 * dd);
         float ym, yr;
         gn_from_sums(s1, s2, (float)(2 * C * T), ym, yr);
         const float ba[4] = {ba4.x, ba4.y, ba4.z, ba4.w}, bg[4] = {bg4.x, bg4.y, bg4.z, bg4.w};
@@ -1118,7 +820,8 @@ __global__ __launch_bounds__(F1_NT, 1) void fenc_row1_kernel(const FencRowDesc d
             }
             st4bf(&xs[(FR_HALO + m) * XS_P + cb], xr[i][0], xr[i][1], xr[i][2], xr[i][3]);
         }
-        __syncthreads();
+        if (dd == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's rewrite-weight pieces landed ...
+        __syncthreads();                                                 // ... and every wave's are published
         FR_STAMP(6 + 4 * dd);
     }
 
@@ -1132,11 +835,11 @@ __global__ __launch_bounds__(F1_NT, 1) void fenc_row1_kernel(const FencRowDesc d
             ba[q] = d.br[pa + q];
             bg[q] = d.br[pa + 16 + q];
         }
-        bf16x8_t wra[3], wrg[3];
+        bf16x8_t wra[3], wrg[3];                 // (from the LDS image)
 #pragma unroll
         for (int ks = 0; ks < 3; ++ks) {
-            wra[ks] = ldfrag(d.wr + (int64_t)(32 * ct + l15) * d.wr_ld + ks * 32 + 8 * l4);
-            wrg[ks] = ldfrag(d.wr + (int64_t)(32 * ct + 16 + l15) * d.wr_ld + ks * 32 + 8 * l4);
+            wra[ks] = *reinterpret_cast<const bf16x8_t*>(wrs + ((32 * ct + l15) * F1_WRC + 4 * ks + l4) * 16);
+            wrg[ks] = *reinterpret_cast<const bf16x8_t*>(wrs + ((32 * ct + 16 + l15) * F1_WRC + 4 * ks + l4) * 16);
         }
         uint2 ov[MTW];
 #pragma unroll
@@ -1160,18 +863,15 @@ __global__ __launch_bounds__(F1_NT, 1) void fenc_row1_kernel(const FencRowDesc d
             }
         }
         FR_STAMP(11);
-        __syncthreads();         // every wave has read xs: stage the output row [T][C] there
-        bf16_t* ob = xs;
+        // straight from registers: 8 B per lane, 32 B per position and wave-instruction; the 6 channel-tile waves of a
+        // position complete its 192-B row in L2 (the LDS-staged form took two more barriers: 7.8k cycles per row)
+        bf16_t* dst = d.out + ((int64_t)b * d.Fout + f) * (int64_t)T * C;
 #pragma unroll
         for (int i = 0; i < MTW; ++i) {
             const int mt = mg + MG * i;
             const int m = mt * 16 + l15;
-            if (mt < MT && m < T) *reinterpret_cast<uint2*>(&ob[m * C + cb]) = ov[i];
+            if (mt < MT && m < T) *reinterpret_cast<uint2*>(&dst[(int64_t)m * C + cb]) = ov[i];
         }
-        __syncthreads();
-        bf16_t* dst = d.out + ((int64_t)b * d.Fout + f) * (int64_t)T * C;
-        for (int i = tid; i < T * C / 8; i += F1_NT)
-            reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(ob)[i];
         FR_STAMP(12);
     }
 }
@@ -1186,12 +886,6 @@ extern "C" int athd_fr_stamps(void* host, int blocks) {
 }
 #endif
 
-static bool fr1_v2() {                 // (round-5 A/B: ATHD_FR1=0 takes the generic level-1 kernel)
-    static int v = -1;
-    if (v < 0) { const char* e = getenv("ATHD_FR1"); v = (e && e[0] == '0') ? 0 : 1; }
-    return v == 1;
-}
-
 int fenc_row_launch(const FencRowDesc& d, int cin, int c, hipStream_t s) {
     // (the 1x1 convs' GroupNorm statistics come from their moments, d.gram)
     if (!fenc_row_supported(cin, c, d.T) || d.Fout * 4 != d.Fin || !d.gram[0] || !d.gram[1]) return -1;
@@ -1204,11 +898,10 @@ int fenc_row_launch(const FencRowDesc& d, int cin, int c, hipStream_t s) {
         const double H = c / 8.0;
         const double macs = rows * T * (c * 8.0 * cin + 2 * (H * 3 * c + 2.0 * c * H) + 2.0 * c * c);
         const double in_b = cin == 4 ? (double)d.B * d.Fin * T * 4 * 4 : (double)d.B * d.Fin * T * cin * 2;
-        ks.begin(cin == 4 ? "fenc_row0_kernel" : "fenc_row_kernel<48,96,12,true>", 2.0 * macs, in_b + rows * T * c * 2);
+        ks.begin(cin == 4 ? "fenc_row0_kernel" : "fenc_row1_kernel", 2.0 * macs, in_b + rows * T * c * 2);
     }
     if (cin == 4) hipLaunchKernelGGL(fenc_row0_kernel, grid, dim3(FR_NT), 0, s, d);
-    else if (fr1_v2()) hipLaunchKernelGGL(fenc_row1_kernel, grid, dim3(F1_NT), 0, s, d);
-    else hipLaunchKernelGGL((fenc_row_kernel<48, 96, 12, true>), grid, dim3(12 * 64), 0, s, d);
+    else hipLaunchKernelGGL(fenc_row1_kernel, grid, dim3(F1_NT), 0, s, d);
     return (int)hipGetLastError();
 }
 

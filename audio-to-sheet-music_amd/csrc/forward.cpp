@@ -910,6 +910,30 @@ void dump_all(const Dims& d, const Bufs& b, hipStream_t s) {
         es.push_back({"saved" + std::to_string(i), b.saved[i], B * d.F[i + 1] * Ts * ENC_CH[i], "B,F,Ts,C"});
         es.push_back({"saved_t" + std::to_string(i), b.saved_t[i], B * d.L[i + 1] * ENC_CH[i], "B,L,C"});
     }
+    for (int i = 0; i < 4 && b.ea == 2; ++i) {      // bf16 mode: the encoder levels as raw bf16 (<name>.bf16)
+        for (int tb = 0; tb < 2; ++tb) {            // (freq level, time level)
+            const int64_t n = tb ? B * d.L[i + 1] * ENC_CH[i] : B * d.F[i + 1] * Ts * ENC_CH[i];
+            std::vector<uint16_t> h((size_t)n);
+            if (hipMemcpy(h.data(), tb ? b.saved_t[i] : b.saved[i], (size_t)n * 2, hipMemcpyDeviceToHost) != hipSuccess)
+                continue;
+            std::string fn = std::string(dir) + (tb ? "/saved_t" : "/saved") + std::to_string(i) + ".bf16";
+            FILE* f = std::fopen(fn.c_str(), "wb");
+            if (f) { std::fwrite(h.data(), 2, h.size(), f); std::fclose(f); }
+        }
+    }
+    {   // the decoder's scratch buffers as raw bytes (<name>.raw; sizes from the arena order in plan())
+        struct Rw { const char* name; const void* p; const void* end; };
+        const Rw rws[] = {{"G", b.G, b.D}, {"D", b.D, b.Gt}, {"Gt", b.Gt, b.Dt}, {"Dt", b.Dt, b.S}, {"S", b.S, b.Z},
+                          {"Z", b.Z, b.Zs}, {"Zs", b.Zs, b.FO}, {"stats", b.stats, b.specT}};
+        for (const auto& e : rws) {
+            if (!e.p || !e.end || e.end <= e.p) continue;
+            std::vector<char> h((size_t)((const char*)e.end - (const char*)e.p));
+            if (hipMemcpy(h.data(), e.p, h.size(), hipMemcpyDeviceToHost) != hipSuccess) continue;
+            std::string fn = std::string(dir) + "/" + e.name + ".raw";
+            FILE* f = std::fopen(fn.c_str(), "wb");
+            if (f) { std::fwrite(h.data(), 1, h.size(), f); std::fclose(f); }
+        }
+    }
     std::string idx = std::string(dir) + "/index.txt";
     FILE* fi = std::fopen(idx.c_str(), "w");
     for (const auto& e : es) {

@@ -1,0 +1,42 @@
+"""Diagnostics (tooling, not a test): run the bf16 forward twice with ATHD_DUMP and report where the encoder level
+outputs (saved0..3, bf16) differ between the two runs."""
+import os
+import sys
+import tempfile
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "audio-to-sheet-music_amd"))
+
+
+def main():
+    import torch
+    from athd.model import AudioTextHTDemucs
+    from athd.synth import synthetic_batch
+    from athd.weights import STEMS, synthetic_state_dict, synthetic_text_table
+    if len(sys.argv) > 1:
+        os.environ["ATHD_LIB"] = os.path.realpath(sys.argv[1])
+    t = synthetic_text_table(4, seed=7)
+    m = AudioTextHTDemucs(dtype="bf16", text_table={s: t[i] for i, s in enumerate(STEMS)})
+    m.load_state_dict(synthetic_state_dict(seed=0))
+    m = m.to("cuda").eval()
+    wav = torch.as_tensor(synthetic_batch(2, 264600, seed0=31)).cuda()
+    outs = []
+    for k in range(2):
+        d = tempfile.mkdtemp()
+        os.environ["ATHD_DUMP"] = d
+        m.forward_prompts(wav, list(STEMS))
+        torch.cuda.synchronize()
+        outs.append({n: np.fromfile(os.path.join(d, n), np.uint8) for n in sorted(os.listdir(d)) if n != "index.txt"})
+    del os.environ["ATHD_DUMP"]
+    for n in outs[0]:
+        a, b = outs[0][n], outs[1][n]
+        print(f"{n}: {int((a != b).sum())} of {a.size} bytes differ", flush=True)
+        if n == "stats.raw" and (a != b).any():
+            da, db = a.view(np.float64), b.view(np.float64)
+            for i in np.nonzero(da != db)[0][:40]:
+                print(f"   stats[{i}]: {da[i]!r} vs {db[i]!r}", flush=True)
+
+if __name__ == "__main__":
+    main()
