@@ -113,27 +113,55 @@ ATHD_DEV void exchange(cx<R> (&v)[16], void* lds, Dst dst, int j) {
 
 // v[r] = x[threadIdx.x + 256 r] on entry; X[threadIdx.x + 256 q] = v[vq(q)] on exit.  tw[m] = e^{-2 pi i m/4096}.
 // j = threadIdx.x (a parameter so that a caller looping over frames can make it opaque per iteration)
+// Twiddles of the Ns = 16 and Ns = 256 passes: w^r for r = 1..15 with w = tw[16 (j & 15)] and w = tw[j].  R = double
+// (the f32 parity mode) reads every power from the table; R = float takes them as running products of the two base
+// twiddles the caller loaded once (tw16, tw256): no table loads per frame (30 dependent L2 round trips per frame were
+// most of the iSTFT's wait time, SQ), at <= 15 ulp of twiddle error, below the fp32 FFT's own rounding over 12 stages.
 template <typename R, typename TW>
-ATHD_DEV void fft4096(cx<R> (&v)[16], void* lds, const TW* __restrict__ tw, int j) {
+ATHD_DEV void fft4096(cx<R> (&v)[16], void* lds, const TW* __restrict__ tw, int j, cpx tw16 = {}, cpx tw256 = {}) {
+    constexpr bool REC = sizeof(R) == 4;
     dft16(v);                                                       // Ns = 1: no twiddles
     exchange(v, lds, [j](int q) { return 16 * j + q; }, j);
     {                                                               // Ns = 16
         const int k = j & 15;
+        cx<R> w = {(R)tw16.x, (R)tw16.y};
 #pragma unroll
         for (int r = 1; r < 16; ++r) {
-            const TW w = tw[k * r * 16];
-            v[r] = cmul(v[r], {w.x, w.y});
+            if constexpr (REC) {
+                v[r] = cmul(v[r], w);
+                // (pinned: the product chain interleaved with its uses, not all 15 powers held at once)
+                asm volatile("" : "+v"(w.x), "+v"(w.y), "+v"(v[r].x), "+v"(v[r].y));
+                if (r < 15) w = cmul(w, {(R)tw16.x, (R)tw16.y});
+            } else {
+                const TW t = tw[k * r * 16];
+                v[r] = cmul(v[r], {t.x, t.y});
+            }
         }
         dft16(v);
         const int base = (j >> 4) * 256 + k;
         exchange(v, lds, [base](int q) { return base + 16 * q; }, j);
     }
+    cx<R> w = {(R)tw256.x, (R)tw256.y};
 #pragma unroll
     for (int r = 1; r < 16; ++r) {                                  // Ns = 256
-        const TW w = tw[j * r];
-        v[r] = cmul(v[r], {w.x, w.y});
+        if constexpr (REC) {
+            v[r] = cmul(v[r], w);
+            // (pinned: the product chain interleaved with its uses, not all 15 powers held at once)
+            asm volatile("" : "+v"(w.x), "+v"(w.y), "+v"(v[r].x), "+v"(v[r].y));
+            if (r < 15) w = cmul(w, {(R)tw256.x, (R)tw256.y});
+        } else {
+            const TW t = tw[j * r];
+            v[r] = cmul(v[r], {t.x, t.y});
+        }
     }
     dft16(v);
+}
+// the two base twiddles of fft4096's running products for thread j (R = float only)
+template <typename TW>
+ATHD_DEV void fft4096_base(const TW* __restrict__ tw, int j, cpx& tw16, cpx& tw256) {
+    const TW a = tw[16 * (j & 15)], c = tw[j];
+    tw16 = {(float)a.x, (float)a.y};
+    tw256 = {(float)c.x, (float)c.y};
 }
 
 ATHD_DEV float pad_sample(const float* __restrict__ x, int64_t p, const PadPlan& pp) {
@@ -170,7 +198,9 @@ __global__ __launch_bounds__(256) void stft_kernel(const float* __restrict__ wav
         const float w = win[n];
         v[r] = {(R)(pad_sample(xl, p0 + n, pp) * w), (R)(pad_sample(xr, p0 + n, pp) * w)};
     }
-    fft4096(v, buf, tw, (int)threadIdx.x);
+    cpx tw16, tw256;
+    fft4096_base(tw, (int)threadIdx.x, tw16, tw256);
+    fft4096(v, buf, tw, (int)threadIdx.x, tw16, tw256);
 #pragma unroll
     for (int q = 0; q < 16; ++q) buf[pidx(threadIdx.x + 256 * q)] = {(float)v[vq(q)].x, (float)v[vq(q)].y};
     __syncthreads();
@@ -322,6 +352,8 @@ __global__ __launch_bounds__(256, MINW) void istft_ola_kernel(const float* __res
 #pragma unroll
         for (int o = 0; o < 4; ++o) env_in[o] = __builtin_amdgcn_rcpf(env_in[o]);
     }
+    cpx tw16, tw256;                    // (frame-invariant: fft4096's base twiddles, R = float)
+    if constexpr (FAST) fft4096_base(tw, (int)threadIdx.x, tw16, tw256);
     float acc[4][4][2];
 #pragma unroll
     for (int h = 0; h < 4; ++h)
@@ -409,7 +441,7 @@ __global__ __launch_bounds__(256, MINW) void istft_ola_kernel(const float* __res
             v[r] = {(R)z.x, (R)z.y};
         }
         __syncthreads();
-        fft4096(v, buf, tw, j);                            // ends synced: buf is free for the next frame
+        fft4096(v, buf, tw, j, tw16, tw256);               // ends synced: buf is free for the next frame
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
             const float wq = win[j + 256 * q] * (1.f / 64.f);   // (L1-resident 16 KB table)
