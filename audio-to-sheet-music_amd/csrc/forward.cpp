@@ -241,6 +241,13 @@ struct Run {
 // the second stream (time branch of the transformer and of the decoder) and its fork / join events, made once
 // ATHD_SERIAL=1: both branches on the caller's stream (profiling runs whose per-kernel times should be the kernel's
 // own; also the behaviour while an athd_profile window is open)
+// round-5 A/B switch: ATHD_ROWLN=0 keeps out_proj and the FFN's LayerNorm as two launches
+static bool rowln_enabled() {
+    static int v = -1;
+    if (v < 0) { const char* e = std::getenv("ATHD_ROWLN"); v = (e && e[0] == '0') ? 0 : 1; }
+    return v == 1;
+}
+
 bool serial_branches(const Run& r) {
     static int env = -1;
     if (env < 0) {
@@ -565,8 +572,17 @@ void encode(Run& r, const Dims& d, const Bufs& b, const float* wav) {
             go.res_gn_stats = resgn->st; go.res_gn_count = N * 512; go.res_gn_w = resgn->w; go.res_gn_b = resgn->b;
             *resgn = Pending();
         }
-        r.gemm(go, "out_proj");
-        ln(X, N, L.cross ? L.n3w : L.n2w, L.cross ? L.n3b : L.n2b, nullptr, Hq, nullptr);
+        const float* n2w = L.cross ? L.n3w : L.n2w;
+        const float* n2b = L.cross ? L.n3b : L.n2b;
+        if (r.actbf && rowln_enabled() && N >= 128) {
+            // bf16 mode: out_proj with the FFN's LayerNorm in its epilogue (rowln.hip: whole 512-column rows per
+            // workgroup; the LayerNorm pass and its second read of X are gone)
+            go.ln_w = n2w; go.ln_b = n2b; go.ln_out = Hq;
+            r.gemm(go, "out_proj.ln");
+        } else {
+            r.gemm(go, "out_proj");
+            ln(X, N, n2w, n2b, nullptr, Hq, nullptr);
+        }
         GemmDesc g1 = r.lin(L.l1, Hq, ab, (int)B, N, 512);
         g1.C = sF1; g1.c_bf16 = ab; g1.act = ACT_GELU;
         r.gemm(g1, "linear1");

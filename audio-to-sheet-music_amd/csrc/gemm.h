@@ -106,6 +106,8 @@ struct GemmDesc {
     // v are stored as (v - mean) * rstd * ln_w[n] + ln_b[n] (eps 1e-5, two-pass statistics as layernorm_kernel)
     const float* ln_w = nullptr;
     const float* ln_b = nullptr;
+    // with an f32 C and a residual (rowln.hip, N = 512): C keeps the rows, ln_out gets their LayerNorm as bf16
+    void* ln_out = nullptr;
 };
 
 // Algorithmic work of one launch (prof.h): 2 M N K flops; bytes = unique activations read once + packed weights +

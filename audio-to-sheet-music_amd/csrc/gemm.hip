@@ -285,10 +285,15 @@ int gemm3_ln_launch(const GemmDesc& d, hipStream_t s);
 bool gemm5_supported(const GemmDesc& d);
 int gemm5_launch(const GemmDesc& d, hipStream_t s);
 
+bool rowln_supported(const GemmDesc& d);
+int rowln_launch(const GemmDesc& d, hipStream_t s);
+
 int gemm_launch(const GemmDesc& d0, int mode, hipStream_t s) {
     if (d0.Kp % BK != 0 || d0.Kp < d0.K || d0.C_in <= 0 || d0.N <= 0) return -2;
     const GemmDesc d = with_fastdiv(d0);
     if (d.act == ACT_GLU && (d.N % 32 != 0)) return -2;
+    // residual projection + the next LayerNorm (rowln.hip), bf16 mode only
+    if (d.ln_out) return mode == 1 && rowln_supported(d) ? rowln_launch(d, s) : -2;
     if (d.ln_w) return mode == 1 ? gemm3_ln_launch(d, s) : -2;      // row-LayerNorm epilogue: gemm3 only
     // the GroupNorm folded into the A load (a_gn_*, the transformer's last pending GroupNorm): gemm2 only; refuse
     // rather than silently skip it on another kernel
