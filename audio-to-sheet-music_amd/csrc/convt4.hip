@@ -245,19 +245,37 @@ __global__ __launch_bounds__(NW * 64) void convt4_kernel(const ConvT4Desc d) {
 }
 
 // ---------------------------------------------------------------------------------------------------------------
-// Column walk (W >= 32, the frequency branch: H = W = Tspec).  The unit kernel above reads every input row three
-// times (as tap u-1, u and u+1 of three units 259 rows apart) and relied on L2 for the re-reads; with the waves of an
-// XCD drifting apart, PMC showed 1.29x the algorithmic HBM bytes.  Here a wave owns a column block (item b, 32
-// consecutive w) and a segment of rows u0 .. u1-1 and walks it row by row: the tap fragments of rows u-1, u, u+1 are
-// kept in three register sets that rotate, so each step loads ONE new row (u+2) - every input row is read once per
-// column block and the loads are a third of the unit kernel's.  Rows and columns outside the item read a zero page;
-// columns past W are neither stored nor counted.  GroupNorm statistics: per lane fp32 per step, fp64 across the
-// segment, one fp64 atomic pair per segment (a segment lies in one item).
-constexpr int CW_RF = 1, CW_NW = 12, CW_SEG = 8;  // 16-wide column blocks, 12 waves per workgroup, 8 row segments
+// Column walk (W >= 16 RF, the frequency branch: H = W = Tspec; round 5).  The unit kernel above reads every input
+// row three times (as tap u-1, u and u+1 of three units 259 rows apart) and relied on L2 for the re-reads; with the
+// waves of an XCD drifting apart, PMC showed 1.29x the algorithmic HBM bytes.  Here a wave owns a column block (item
+// b, 16 RF consecutive w) and a segment of rows u0 .. u1-1 and walks it row by row: the tap fragments of rows u-1, u,
+// u+1 are kept in three register sets that rotate, so each step loads ONE new row (u+2) - every input row is read once
+// per column block (+ 2 halo rows per segment).  Rows and columns outside the item read zeros (buffer descriptors);
+// columns past W are neither stored nor counted.  One residue at a time (3 x RF accumulators live, each weight
+// fragment read from LDS feeds RF MFMAs), and the two stored rows of a step leave through a per-wave LDS stage as
+// contiguous 16-B-per-lane segments.  GroupNorm statistics: per lane fp32 per step, fp64 across the segment, one fp64
+// atomic pair per segment (a segment lies in one item).
+// Measured (freq level 2 per forward, serialised events, one box): unit kernel 2.07 ms; walk, RF = 1, 12 waves 2.02
+// (HBM bytes 8.48 -> 5.12 GB per launch, time unchanged: not memory-bound); one residue at a time 1.95; RF = 2 at 8
+// waves (2 per SIMD; at 12 waves it spills) 1.94; + staged stores 1.82 (staged stores at RF = 1: 1.95).
+#ifndef ATHD_CW_RF
+#define ATHD_CW_RF 2
+#endif
+#ifndef ATHD_CW_SEG
+#define ATHD_CW_SEG 14
+#endif
+#ifndef ATHD_CW_NW
+#define ATHD_CW_NW 8
+#endif
+constexpr int CW_RF = ATHD_CW_RF, CW_NW = ATHD_CW_NW, CW_SEG = ATHD_CW_SEG;  // 32-wide column blocks, 8 waves per workgroup, 14 row segments
 template <bool KEEP>
 __global__ __launch_bounds__(CW_NW * 64) void convt4_walk_kernel(const ConvT4Desc d) {
     constexpr int RF = CW_RF;
+    constexpr int OSB = 16 * RF * CT_CO * 2;      // bytes of one stored output row segment of a wave (16 RF columns)
     __shared__ __attribute__((aligned(16))) char wl[4 * CT_CO * CT_WROW];   // 73,728 B
+    // KEEP: per wave the two stored rows of a step ([2][16 RF columns][48] bf16), written to HBM as whole contiguous
+    // segments (16 B per lane) instead of 32-B pieces at a 96-B stride (16 per store instruction)
+    __shared__ __attribute__((aligned(16))) char ostg[KEEP ? CW_NW : 1][2 * OSB];
     for (int c = threadIdx.x; c < 4 * CT_CO * 24; c += CW_NW * 64) {
         const int n = c / 24, ch = c - 24 * (c / 24);
         const uint4 v = reinterpret_cast<const uint4*>(d.w)[c];
@@ -294,14 +312,17 @@ __global__ __launch_bounds__(CW_NW * 64) void convt4_walk_kernel(const ConvT4Des
     const char* const xb = reinterpret_cast<const char*>(d.x);
     const char* const zero = reinterpret_cast<const char*>(g_zero_ct4);
     const f32x4_t z4 = {0.f, 0.f, 0.f, 0.f};
-    f32x4_t acc[RF][6];
-    auto mma = [&](int p, int h, const bf16v8 (&F)[RF][3]) {
+    // one residue rho at a time (its 3 channel tiles: pair p = rho / 2, pair-local tiles 3 (rho & 1) ..): each weight
+    // fragment feeds RF MFMAs, and only 3 x RF accumulators are live
+    f32x4_t acc[RF][3];
+    auto mma = [&](int rho, int h, const bf16v8 (&F)[RF][3]) {
+        const int p = rho >> 1, j0 = 3 * (rho & 1);
 #pragma unroll
         for (int s = 0; s < 3; ++s) {
             fence();
 #pragma unroll
-            for (int jj = 0; jj < 6; ++jj) {
-                const bf16v8 wf = wfrag(p, jj, 3 * h + s);
+            for (int jj = 0; jj < 3; ++jj) {
+                const bf16v8 wf = wfrag(p, j0 + jj, 3 * h + s);
 #pragma unroll
                 for (int i = 0; i < RF; ++i)
                     acc[i][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, F[i][s], (h == 0 && s == 0) ? z4 : acc[i][jj], 0, 0, 0);
@@ -327,6 +348,8 @@ __global__ __launch_bounds__(CW_NW * 64) void convt4_walk_kernel(const ConvT4Des
         const char* const xitem = xb + (int64_t)b * H * W * (CT_CI * 2);
         char* const oitem = reinterpret_cast<char*>(d.out) + (int64_t)b * H * (KEEP ? 2 : 4) * W * (CT_CO * 2);
         const int64_t rowB = (int64_t)W * (CT_CI * 2), orowB = (int64_t)W * (CT_CO * 2);
+        const int ocol0 = 16 * RF * wblk * (CT_CO * 2);                       // the segment's byte offset in a row
+        const int ovalid = min(16 * RF, W - 16 * RF * wblk) * (CT_CO * 2);   // its stored bytes
         // row u through a buffer descriptor of that row (wave-uniform): a row outside the item has zero records and a
         // column past W an out-of-range offset, so those loads return zeros (no per-lane 64-bit address selects)
         uint32_t lofs[RF];
@@ -346,21 +369,24 @@ __global__ __launch_bounds__(CW_NW * 64) void convt4_walk_kernel(const ConvT4Des
         // one row u with taps (Fa, Fb, Fc) = rows (u-1, u, u+1); Fa is refilled with row u+2 once pair 0 is done
         auto step = [&](int u, bf16v8 (&Fa)[RF][3], bf16v8 (&Fb)[RF][3], bf16v8 (&Fc)[RF][3]) {
             float p1 = 0.f, p2 = 0.f;
-            auto epi = [&](int p) {
+            auto epi = [&](int rho) {
 #pragma unroll
                 for (int i = 0; i < RF; ++i) {
 #pragma unroll
-                    for (int j = 0; j < 6; ++j) {
-                        const int rho = 2 * p + j / 3, jj = j - 3 * (j / 3);
+                    for (int jj = 0; jj < 3; ++jj) {
                         const float4 bb = b4[jj];
-                        const float v0 = acc[i][j][0] + bb.x, v1 = acc[i][j][1] + bb.y;
-                        const float v2 = acc[i][j][2] + bb.z, v3 = acc[i][j][3] + bb.w;
+                        const float v0 = acc[i][jj][0] + bb.x, v1 = acc[i][jj][1] + bb.y;
+                        const float v2 = acc[i][jj][2] + bb.z, v3 = acc[i][jj][3] + bb.w;
                         const float q1 = (v0 + v1) + (v2 + v3), q2 = (v0 * v0 + v1 * v1) + (v2 * v2 + v3 * v3);
                         p1 += cok[i] ? q1 : 0.f;
                         p2 += cok[i] ? q2 : 0.f;
-                        if (KEEP ? (rho == 1 || rho == 2) : true) {
-                            // output row (KEEP) 2u + rho - 1 / (all) 4u + rho of the item: a wave-uniform base
-                            const char* ob = oitem + (KEEP ? (int64_t)(2 * u + rho - 1) : (int64_t)(4 * u + rho)) * orowB;
+                        if constexpr (KEEP) {
+                            if (rho == 1 || rho == 2)     // staged: row segment rho - 1, column 16 i + fr
+                                *reinterpret_cast<uint2*>(ostg[wave] + (rho - 1) * OSB + (16 * i + fr) * (CT_CO * 2) +
+                                                          32 * jj + 8 * g) = make_uint2(pack2bf(v0, v1), pack2bf(v2, v3));
+                        } else {
+                            // output row 4u + rho of the item: a wave-uniform base
+                            const char* ob = oitem + (int64_t)(4 * u + rho) * orowB;
                             if (cok[i])
                                 *reinterpret_cast<uint2*>((char*)ob + cout_off[i] + 32 * jj) =
                                     make_uint2(pack2bf(v0, v1), pack2bf(v2, v3));
@@ -368,13 +394,32 @@ __global__ __launch_bounds__(CW_NW * 64) void convt4_walk_kernel(const ConvT4Des
                     }
                 }
             };
+            // residues 0, 1 read rows u-1, u (Fa, Fb); 2, 3 read u, u+1 (Fb, Fc).  Fa is free after residue 1.
             mma(0, 0, Fa);
-            load_row(u + 2, Fa);                  // (row u+2 is the next step's upper tap)
             mma(0, 1, Fb);
             epi(0);
-            mma(1, 0, Fb);
-            mma(1, 1, Fc);
+            mma(1, 0, Fa);
+            load_row(u + 2, Fa);                  // (row u+2 is the next step's upper tap)
+            mma(1, 1, Fb);
             epi(1);
+            mma(2, 0, Fb);
+            mma(2, 1, Fc);
+            epi(2);
+            if constexpr (KEEP) {
+                // the staged rows 2u, 2u + 1 (this wave's segment): 16 B per lane, columns past W not stored
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_wave_barrier();
+#pragma unroll
+                for (int k = 0; k < 2 * OSB / (16 * 64); ++k) {
+                    const int c = lane + 64 * k, r = c / (OSB / 16), wb = (c % (OSB / 16)) * 16;
+                    const uint4 v = *reinterpret_cast<const uint4*>(ostg[wave] + r * OSB + wb);
+                    if (wb < ovalid)
+                        *reinterpret_cast<uint4*>(oitem + (int64_t)(2 * u + r) * orowB + ocol0 + wb) = v;
+                }
+            }
+            mma(3, 0, Fb);
+            mma(3, 1, Fc);
+            epi(3);
             r1 += (double)p1;
             r2 += (double)p2;
         };
@@ -433,12 +478,6 @@ static void launch_ct4(const ConvT4Desc& d, int cus, hipStream_t s) {
     hipLaunchKernelGGL((convt4_kernel<KEEP, RF, NW>), dim3((unsigned)blocks), dim3(NW * 64), 0, s, d);
 }
 
-static bool ct4_walk() {               // (round-5 A/B: ATHD_CT4W=0 takes the unit kernel)
-    static int v = -1;
-    if (v < 0) { const char* e = getenv("ATHD_CT4W"); v = (e && e[0] == '0') ? 0 : 1; }
-    return v == 1;
-}
-
 int convt4_launch(const ConvT4Desc& d0, hipStream_t s) {
     if (!convt4_supported(CT_CI, CT_CO, d0.nb, d0.H, d0.W)) return -1;
     ConvT4Desc d = d0;
@@ -447,8 +486,8 @@ int convt4_launch(const ConvT4Desc& d0, hipStream_t s) {
     d.fd_hw = make_fastdiv((uint32_t)d.H * (uint32_t)d.W);
     d.M = (uint32_t)((int64_t)d.nb * d.H * d.W);
     const int cus = device_cus();
-    if (d.W >= 16 * CW_RF && ct4_walk()) {
-        // column walk: one workgroup (72 KB LDS) per CU, a multiple of 8
+    if (d.W >= 16 * CW_RF) {
+        // column walk: one workgroup (72 KB of weights + the store stages) per CU, a multiple of 8
         const int64_t items = (int64_t)d.nb * ((d.W + 16 * CW_RF - 1) / (16 * CW_RF)) * CW_SEG;
         int64_t blocks = cus;
         if (blocks * CW_NW > items) blocks = (items + CW_NW - 1) / CW_NW;
