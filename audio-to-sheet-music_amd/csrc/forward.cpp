@@ -574,12 +574,13 @@ void encode(Run& r, const Dims& d, const Bufs& b, const float* wav) {
         }
         const float* n2w = L.cross ? L.n3w : L.n2w;
         const float* n2b = L.cross ? L.n3b : L.n2b;
-        if (r.actbf && rowln_enabled() && N >= 128) {
+        go.ln_w = n2w; go.ln_b = n2b; go.ln_out = Hq;
+        if (r.actbf && rowln_enabled() && rowln_supported(go)) {
             // bf16 mode: out_proj with the FFN's LayerNorm in its epilogue (rowln.hip: whole 512-column rows per
             // workgroup; the LayerNorm pass and its second read of X are gone)
-            go.ln_w = n2w; go.ln_b = n2b; go.ln_out = Hq;
             r.gemm(go, "out_proj.ln");
         } else {
+            go.ln_w = go.ln_b = nullptr; go.ln_out = nullptr;
             r.gemm(go, "out_proj");
             ln(X, N, n2w, n2b, nullptr, Hq, nullptr);
         }

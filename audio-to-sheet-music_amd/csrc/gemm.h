@@ -124,6 +124,8 @@ inline void gemm_work(const GemmDesc& d, int mode, double& flops, double& bytes)
 
 // mode: 0 = exact fp32 (v_mfma_f32_16x16x4_f32), 1 = bf16 (v_mfma_f32_16x16x32_bf16, fp32 accumulate)
 int gemm_launch(const GemmDesc& d, int mode, hipStream_t s);
+// the shapes the residual projection + LayerNorm pass (rowln.hip, GemmDesc::ln_out) handles
+bool rowln_supported(const GemmDesc& d);
 // d with its fast-division constants filled (every kernel launcher passes this copy to the kernel)
 inline GemmDesc with_fastdiv(const GemmDesc& d) {
     GemmDesc e = d;

@@ -45,6 +45,7 @@ __global__ __launch_bounds__(G6_NT, 2) void gemm6_kernel(const GemmDesc d) {
     constexpr int TM = G6_TM, TN = G6_TN;
     __shared__ __attribute__((aligned(1024))) char ring[G6_NS * G6_STAGE];
     __shared__ double st_lds[2 * EPI_MAXG];
+    __shared__ __attribute__((aligned(1024))) char sink[1024];
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -65,6 +66,7 @@ __global__ __launch_bounds__(G6_NT, 2) void gemm6_kernel(const GemmDesc d) {
     uint32_t m0 = 0;
     int n0 = 0;
     uint32_t aoff[G6_AQ];
+    const char* bbase[TN];
     const char* const abase = (const char*)d.A;
     const uint32_t boff = (uint32_t)(l15 * d.Kp + 8 * l4) * 2;
     auto setup = [&](int t) {
@@ -72,19 +74,23 @@ __global__ __launch_bounds__(G6_NT, 2) void gemm6_kernel(const GemmDesc d) {
         m0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)((L / ntn) * G6_BM));
         n0 = __builtin_amdgcn_readfirstlane((L % ntn) * G6_BN);
 #pragma unroll
+        for (int j = 0; j < TN; ++j) bbase[j] = (const char*)d.Wp + (int64_t)(n0 + wn0 + 16 * j) * d.Kp * 2;
+#pragma unroll
         for (int q = 0; q < G6_AQ; ++q) {
             uint32_t m = m0 + 8 * (wave + G6_NW * q) + lrow;
             m = m < M ? m : M - 1;
             aoff[q] = (m * (uint32_t)d.a_ld + 8 * chunk) * 2;
         }
     };
+    // K-tile kt of A into ring slot kt % 4; past the last K-tile the same pieces re-read K-tile 0 into a 1-KB sink, so that every K-step issues the same operations and the wait counts are constants
     auto dma_a = [&](int kt) {
-        char* dst = ring + (kt % G6_NS) * G6_STAGE;
-        const char* ab = abase + (int64_t)kt * 128;
+        const bool real = kt < KT;                   // (wave-uniform)
+        char* dst = real ? ring + (kt % G6_NS) * G6_STAGE : sink;
+        const char* ab = abase + (int64_t)(real ? kt : 0) * 128;
 #pragma unroll
         for (int q = 0; q < G6_AQ; ++q)
-            __builtin_amdgcn_global_load_lds((g6_gbl_void*)(ab + aoff[q]), (g6_lds_void*)(dst + (wave + G6_NW * q) * 1024),
-                                             16, 0, 0);
+            __builtin_amdgcn_global_load_lds((g6_gbl_void*)(ab + aoff[q]),
+                                             (g6_lds_void*)(real ? dst + (wave + G6_NW * q) * 1024 : dst), 16, 0, 0);
     };
     // B fragments G6_BD K-steps ahead in a ring of G6_BD + 1 register sets: the A DMA of K-tile kt + 3, issued
     // after B(2 kt + 3), then stays in flight until the wait for B(2 kt + 4), two K-tiles later (one vmcnt orders both
@@ -92,33 +98,21 @@ __global__ __launch_bounds__(G6_NT, 2) void gemm6_kernel(const GemmDesc d) {
     constexpr int BD = 3;
     bf16x8_t bq[BD + 1][TN];                     // [K-step % 4][column tile]
     // (the base of column tile j at K-step ks is wave-uniform: an SGPR pair; the lane's part is boff)
+    // (the tile's column-tile bases are wave-uniform SGPR pairs, set by setup; a K-step past the last re-reads K-step
+    // 0 into the free register set, so that every K-step issues the same operations)
 #define G6_LOAD_B(KS_, BUF)                                                                                        \
-    for (int j_ = 0; j_ < TN; ++j_)                                                                                \
-        asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(bq[BUF][j_])                                          \
-                     : "v"(boff), "s"((const char*)d.Wp + ((int64_t)(n0 + wn0 + 16 * j_) * d.Kp + 32 * (KS_)) * 2))
-    // VM operations issued at K-step j (B(j + BD), then at even j A(j / 2 + 3))
-    auto ops_at = [&](int j) { return (j + BD < 2 * KT ? TN : 0) + ((j % 2 == 0 && j / 2 + 3 < KT) ? G6_AQ : 0); };
-    // B of K-step ks (buffer BUF) landed: the operations issued after it may stay in flight
+    do {                                                                                                           \
+        const uint32_t vo_ = boff + (uint32_t)((KS_) < 2 * KT ? (KS_) : 0) * 64;                                   \
+        for (int j_ = 0; j_ < TN; ++j_)                                                                            \
+            asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(bq[BUF][j_]) : "v"(vo_), "s"(bbase[j_]));       \
+    } while (0)
+    // B of K-step ks landed: with the constant issue pattern, 14 younger operations may be in flight from K-step 2
+    // on, 10 at K-steps 0 and 1 (the prologue's three B loads came after its A pieces); simulated over the issue
+    // order for KT = 4, 8, 32, including that A(kt + 1) has landed in every wave before the barrier ending K-tile kt
 #define G6_WAIT_B(KS_, BUF)                                                                                        \
     do {                                                                                                           \
-        const int ks0_ = (KS_) - BD;                                                                               \
-        int n_ = (ks0_ >= 0 && ks0_ % 2 == 0 && ks0_ / 2 + 3 < KT) ? G6_AQ : 0;                                    \
-        for (int j_ = (ks0_ >= 0 ? ks0_ + 1 : 0); j_ <= (KS_); ++j_) n_ += ops_at(j_);                             \
-        if (ks0_ < 0) n_ += (BD - 1 - (KS_)) * TN;   /* prologue: A(0 .. 2), then B(0 .. 2) */                  \
-        n_ = __builtin_amdgcn_readfirstlane(n_);                                                                   \
-        switch (n_ >= 20 ? 20 : n_ - n_ % 2) {                                                                    \
-            case 20: asm volatile("s_waitcnt vmcnt(20)" ::: "memory"); break;                                     \
-            case 18: asm volatile("s_waitcnt vmcnt(18)" ::: "memory"); break;                                     \
-            case 16: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;                                     \
-            case 14: asm volatile("s_waitcnt vmcnt(14)" ::: "memory"); break;                                     \
-            case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;                                     \
-            case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;                                     \
-            case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;                                       \
-            case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;                                       \
-            case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;                                       \
-            case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;                                       \
-            default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;                                      \
-        }                                                                                                          \
+        if ((KS_) < 2) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");                                         \
+        else asm volatile("s_waitcnt vmcnt(14)" ::: "memory");                                                    \
         for (int j_ = 0; j_ < TN; ++j_) asm volatile("" : "+v"(bq[BUF][j_]));                                    \
     } while (0)
 
@@ -127,8 +121,7 @@ __global__ __launch_bounds__(G6_NT, 2) void gemm6_kernel(const GemmDesc d) {
     // also land them (A(0) before K-tile 0, A(1) before the barrier that ends it)
     auto prologue = [&]() {
 #pragma unroll
-        for (int k = 0; k < G6_NS - 1; ++k)
-            if (k < KT) dma_a(k);
+        for (int k = 0; k < G6_NS - 1; ++k) dma_a(k);
         asm volatile("" ::: "memory");
         G6_LOAD_B(0, 0);
         G6_LOAD_B(1, 1);
@@ -146,15 +139,15 @@ __global__ __launch_bounds__(G6_NT, 2) void gemm6_kernel(const GemmDesc d) {
         for (int i = 0; i < TM; ++i)
 #pragma unroll
             for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-        // K-step ks = 2 kt + s: issue B(ks + 3) and (s = 0) A(kt + 3); wait for B(ks) (G6_WAIT_B's count).  At the
+        // K-step ks = 2 kt + s: issue B(ks + 3) and (s = 0) A(kt + 3) (dummies past the end); wait for B(ks).  At the
         // first K-step of K-tile kt - 1 that wait also landed A(kt) (issued before B(2 kt - 5)), in every wave, and
         // the barrier that ends K-tile kt - 1 published it
 #define G6_KSTEP(KS_, BUF)                                                                                         \
         {                                                                                                          \
             const int ks = (KS_), kt = ks / 2, s = ks % 2;                                                         \
-            if (ks + BD < 2 * KT) { G6_LOAD_B(ks + BD, ((BUF) + BD) % (BD + 1)); }                                 \
+            G6_LOAD_B(ks + BD, ((BUF) + BD) % (BD + 1));                                                           \
             asm volatile("" ::: "memory");                                                                         \
-            if (s == 0 && kt + 3 < KT) dma_a(kt + 3);                                                              \
+            if (s == 0) dma_a(kt + 3);                                                                             \
             asm volatile("" ::: "memory");                                                                         \
             G6_WAIT_B(ks, BUF);                                                                                    \
             if (ks == 0) __builtin_amdgcn_s_barrier();    /* A(0) of every wave */                                \
@@ -206,9 +199,11 @@ __global__ __launch_bounds__(G6_NT, 2) void gemm6_kernel(const GemmDesc d) {
             prologue();
         }
 #endif
+        // (the dummy A pieces of the last K-steps land in the sink: they must finish before the workgroup's LDS is
+        // released; the next prologue's B loads write the registers of the dummy B loads after them, in order)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (the epilogue's stores and the prologue's loads)
         if (next >= ntiles) break;
         tile = next;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (the epilogue's stores and the prologue's loads)
         __builtin_amdgcn_s_barrier();
     }
 #undef G6_LOAD_B

@@ -80,12 +80,14 @@ __global__ __launch_bounds__(64 * NW, 2) void rowln_kernel(const GemmDesc d) {
     constexpr int NT = 64 * NW;
     constexpr int TM = BM / 16, TN = RL_N / NW / 16;
     constexpr int STAGE = BM * 128;
-    constexpr int AQ = BM / 8 / NW;              // A DMAs per wave per K-tile
-    static_assert(AQ * 8 * NW == BM && TN * 16 * NW == RL_N, "tile shape");
+    constexpr int AP = BM / 8;                   // 1-KB A pieces (8 rows) per K-tile
+    constexpr int AQ = (AP + NW - 1) / NW;       // A DMAs per wave per K-tile (surplus pieces: zero page -> sink)
+    static_assert(AP * 8 == BM && BM % 16 == 0 && TN * 16 * NW == RL_N, "tile shape");
     using S = RlSched<TN, AQ>;
     __shared__ __attribute__((aligned(1024))) char ring[RL_NS * STAGE];
     __shared__ __attribute__((aligned(16))) float par[RL_PAR];
     __shared__ __attribute__((aligned(16))) float red[2][BM][NW];
+    __shared__ __attribute__((aligned(1024))) char sink[AQ * NW > AP ? 1024 : 16];
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -117,14 +119,16 @@ __global__ __launch_bounds__(64 * NW, 2) void rowln_kernel(const GemmDesc d) {
 #pragma unroll
     for (int q = 0; q < AQ; ++q) {
         const uint32_t m = m0 + 8 * (wave + NW * q) + lrow;
-        arow[q] = m < M ? (const char*)d.A + ((int64_t)m * RL_K + 8 * chunk) * 2 : nullptr;
+        arow[q] = m < M && wave + NW * q < AP ? (const char*)d.A + ((int64_t)m * RL_K + 8 * chunk) * 2 : nullptr;
     }
     auto dma_a = [&](int kt) {
         char* dst = ring + (kt % RL_NS) * STAGE;
 #pragma unroll
         for (int q = 0; q < AQ; ++q) {
             const char* src = arow[q] ? arow[q] + kt * 128 : zero;
-            __builtin_amdgcn_global_load_lds((rl_gbl_void*)src, (rl_lds_void*)(dst + (wave + NW * q) * 1024), 16, 0, 0);
+            char* to = dst + (wave + NW * q) * 1024;
+            if (AQ * NW > AP && wave + NW * q >= AP) to = sink;      // (wave-uniform)
+            __builtin_amdgcn_global_load_lds((rl_gbl_void*)src, (rl_lds_void*)to, 16, 0, 0);
         }
     };
     // B fragments by global_load_dwordx4 in inline asm, waited for by explicit counts: with VGPR-returning loads and
