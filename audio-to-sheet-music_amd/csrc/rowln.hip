@@ -7,14 +7,16 @@
 //
 // The unfused pair (gemm5 out_proj, then layernorm_rows_kernel) reads the f32 rows of X twice: 271 MB more per freq
 // layer than this pass, which needs whole rows in one workgroup (N = 512).  Tile = BM rows x 512 columns, K = 512,
-// NW waves; wave w owns 512 / NW columns of all BM rows (TM x TN accumulator tiles of 16 x 16, 128 registers).
-// One workgroup per CU (8 waves at 2 per SIMD, 240 VGPRs each: the accumulators alone take 128), so a workgroup's
+// NW waves; wave w owns 512 / NW columns of all BM rows (TM x TN accumulator tiles of 16 x 16, 144 registers at
+// BM = 144).  One workgroup per CU (8 waves at 2 per SIMD, 246 VGPRs each), so a workgroup's
 // K-loop (matrix cores, B from L2) and its epilogue (HBM: 10 bytes per output element) alternate.  Measured forms
 // (serialised events for the 10 launches of a forward, one box each): 128 x 512 tiles 2.08 ms; 64 x 512 tiles of 4
 // waves, two workgroups per CU so one's epilogue runs beside the other's K-loop, 2.34 ms (the B fragments, re-read
 // from L2 for every 64 rows, then need ~39 TB/s of L2 bandwidth); out_proj + LayerNorm unfused 2.03 ms.  Whole step
 // neutral in A/B (ATHD_ROWLN=0, 4 alternating pairs: 1822 vs 1821 segments/s); kept for the 10 fewer launches and
-// 2.7 GB less HBM traffic per forward.
+// 2.7 GB less HBM traffic per forward.  144-row tiles (round 5; 18 A pieces per K-tile, 3 per wave, the 6 surplus
+// ones from the zero page into a sink): the freq / time launches take 4 / 2 rounds of tiles instead of 5 / 3, 2.13 ->
+// 1.84 ms, whole step 1837 -> 1855 segments/s (3 alternating runs each, driver protocol).
 //   - A (the attention output, bf16) is shared by all waves: 16-KB K-tiles by LDS-DMA into a 3-deep ring (gemm3's
 //     swizzled image and counted waits).
 //   - B (the weights, 512 KB of bf16: resident in every XCD's L2) goes global -> VGPR as MFMA fragments, one K-step
@@ -324,8 +326,8 @@ __global__ __launch_bounds__(64 * NW, 2) void rowln_kernel(const GemmDesc d) {
 }
 
 #ifndef ATHD_RL_BM
-#define ATHD_RL_BM 128
-#endif
+#define ATHD_RL_BM 144       // (the tile-round count: 921 / 460 row tiles over 256 CUs for M = 132608 / 66176, where
+#endif                       // 128-row tiles need 1036 / 517, i.e. 5 and 3 rounds; 2.13 -> 1.84 ms per forward)
 #ifndef ATHD_RL_NW
 #define ATHD_RL_NW 8
 #endif
