@@ -13,7 +13,9 @@
 // Q_q / c1_q depend only on (Hd, Hs, Hk) (fdec1_gram_q_kernel, double); G_q and the per-channel sums of x_q are a
 // Gram matrix over (w, c): matrix-core work on the Z tile while it is in LDS.  So this pass computes Z tile by tile
 // (MFMA, into LDS, never to HBM), accumulates the 4 classes' 80 x 80 Gram blocks in MFMA accumulators across the
-// tiles of an item, flushes them per item with fp32 atomics, and fdec1_gram_final_kernel forms {sum, sumsq}.  It
+// tiles of an item, flushes them per item into a partial slot of its own (workgroup, item), fdec1_gram_reduce_kernel
+// sums an item's slots in a fixed order (bit-reproducible, round 5: the fp32 atomics of rounds 3-4 made two forwards
+// differ at ~121 dB) and fdec1_gram_final_kernel forms {sum, sumsq}.  It
 // replaces the 8-tap Z GEMM + fdec_lr_stats3_kernel's sweep (VALU-bound); it also stores the 4-tap Z (taps 0, 3, 4, 7)
 // the merge pass reads, from the same LDS tiles.
 //
@@ -50,6 +52,10 @@ constexpr int G_LDS = G_B_BYTES + G_ZT_BYTES + G_ZS_BYTES;   // 128 KB
 constexpr int G_NX = 80;                      // x_q entries
 constexpr int G_NB = G_NX + G_CO;             // Gram row: 80 data columns + 96 per-channel sums
 constexpr int G_ITEM = 4 * G_NX * G_NB;       // floats per item
+constexpr int G_PSLOT = 8 * 10 * 64 * 4;      // floats per partial slot: the 8 waves' 10 Gram blocks as held in registers
+
+// tile range [tb(qi), tb(qi + 1)) of the workgroups with logical index L = NG qi + g (T tiles over Qg ranges)
+ATHD_HD int g_tb(int qi, int T, int Qg) { return (int)((int64_t)T * qi / Qg); }
 
 ATHD_DEV int swz(int row, int chunk) { return row * 256 + ((chunk ^ (row & 15)) << 4); }
 
@@ -118,7 +124,8 @@ __device__ uint64_t g_gr_stamp[1024 * 8 * 8];
 #define GR_MARK(k) do { } while (0)
 #endif
 
-__global__ __launch_bounds__(G_THREADS, 1) void fdec1_gram_kernel(const LowRankDesc d, float* gram) {
+__global__ __launch_bounds__(G_THREADS, 1) void fdec1_gram_kernel(const LowRankDesc d, float* gram, float* part,
+                                                                    int kmax) {
     __shared__ __attribute__((aligned(16))) char smem[G_LDS];
     char* const bl = smem;                                    // weights
     char* const zt = smem + G_B_BYTES;                        // ZT
@@ -185,19 +192,14 @@ __global__ __launch_bounds__(G_THREADS, 1) void fdec1_gram_kernel(const LowRankD
     f32x4_t gacc[G_NBLK];
 #pragma unroll
     for (int b = 0; b < G_NBLK; ++b) gacc[b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    // the item's partial slot of this workgroup (slot n - first item of the range), the accumulators as they are held
+    const int n_first = t_beg / NWB;
     auto flush = [&](int n) {
-        float* const gb = gram + ((int64_t)n * 4 + gq) * G_NX * G_NB;
+        f32x4_t* const pb = reinterpret_cast<f32x4_t*>(part + ((int64_t)L * kmax + (n - n_first)) * G_PSLOT) +
+                            wv * G_NBLK * 64 + lane;
 #pragma unroll
         for (int b = 0; b < G_NBLK; ++b) {
-            {
-                const int ri = blk_r(gh, b), ci = blk_c(gh, b);
-                const int col = ci < 5 ? ci * 16 + (lane & 15) : G_NX + c0 + (lane & 15);
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const int a = ri * 16 + 4 * (lane >> 4) + i;
-                    atomicAdd(gb + a * G_NB + col, gacc[b][i]);
-                }
-            }
+            pb[b * 64] = gacc[b];
             gacc[b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
         }
     };
@@ -336,6 +338,50 @@ __global__ __launch_bounds__(G_THREADS, 1) void fdec1_gram_kernel(const LowRankD
 #endif
 }
 
+// item n's Gram blocks from the partial slots of the workgroups whose tile ranges meet the item, summed in a fixed
+// order (channel group, then range): one thread per accumulator register quadruple (wave, block, lane) of a slot.
+// The 5 x 5 upper block triangle is summed over all channel groups; the one-hot blocks (per-channel sums) belong to
+// one group each.  Every entry fdec1_gram_final_kernel reads is written here.
+__global__ __launch_bounds__(256) void fdec1_gram_reduce_kernel(const float* part, float* gram, int kmax, int T, int Qg,
+                                                                int NWB) {
+    const int n = blockIdx.y;
+    const int p = blockIdx.x * 256 + threadIdx.x;
+    if (p >= 8 * G_NBLK * 64) return;
+    const int wv = p / (G_NBLK * 64), b = (p / 64) % G_NBLK, lane = p % 64;
+    const int gq = wv >> 1, gh = wv & 1, ri = blk_r(gh, b), ci = blk_c(gh, b);
+    auto owner = [&](int t) {                          // the range holding tile t
+        int q = (int)((int64_t)t * Qg / T);
+        while (q + 1 < Qg && g_tb(q + 1, T, Qg) <= t) ++q;
+        while (q > 0 && g_tb(q, T, Qg) > t) --q;
+        return q;
+    };
+    const int q_lo = owner(n * NWB), q_hi = owner(n * NWB + NWB - 1);
+    float* const gb = gram + ((int64_t)n * 4 + gq) * G_NX * G_NB;
+    f32x4_t tot = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    for (int g = 0; g < G_NG; ++g) {
+        f32x4_t sg = f32x4_t{0.f, 0.f, 0.f, 0.f};
+        for (int qi = q_lo; qi <= q_hi; ++qi) {
+            const int tb = g_tb(qi, T, Qg);
+            if (tb >= g_tb(qi + 1, T, Qg)) continue;   // an empty range flushed nothing
+            const int L = qi * G_NG + g, k = n - tb / NWB;
+            const f32x4_t v = *(reinterpret_cast<const f32x4_t*>(part + ((int64_t)L * kmax + k) * G_PSLOT) + p);
+            sg[0] += v[0]; sg[1] += v[1]; sg[2] += v[2]; sg[3] += v[3];
+        }
+        if (ci == 5) {                                 // this group's channel columns
+            const int col = G_NX + g * G_CG + (lane & 15);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) gb[(ri * 16 + 4 * (lane >> 4) + i) * G_NB + col] = sg[i];
+        } else {
+            tot[0] += sg[0]; tot[1] += sg[1]; tot[2] += sg[2]; tot[3] += sg[3];
+        }
+    }
+    if (ci < 5) {
+        const int col = ci * 16 + (lane & 15);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) gb[(ri * 16 + 4 * (lane >> 4) + i) * G_NB + col] = tot[i];
+    }
+}
+
 // {sum, sumsq} of item n from its Gram blocks: one 256-thread block per item
 __global__ __launch_bounds__(256) void fdec1_gram_final_kernel(const float* gram, const double* gq, const float* bias,
                                                                double* stats, int Hd, int W) {
@@ -391,7 +437,6 @@ bool fdec1_gram_supported(const LowRankDesc& d) {
            (int64_t)d.NI * ((d.W + G_WB - 1) / G_WB) < (1LL << 31);
 }
 
-int64_t fdec1_gram_floats(int64_t NI) { return NI * G_ITEM + G_THREADS * 16; }   // + the prologue's scratch slot
 int64_t fdec1_gram_q_doubles() { return 4 * (G_NX * G_NX + G_NX); }
 
 static int g_blocks() {
@@ -403,9 +448,22 @@ static int g_blocks() {
     return cus / G_NG * G_NG;
 }
 
+// partial slots per workgroup: the most items one tile range can meet
+static int g_kmax(int64_t NI, int W) {
+    const int64_t NWB = (W + G_WB - 1) / G_WB, T = NI * NWB, Qg = g_blocks() / G_NG;
+    const int64_t len = (T + Qg - 1) / Qg;
+    return (int)((len + NWB - 1) / NWB + 1);
+}
+
+// the item Gram rows, the prologue's scratch slot, the partial slots
+int64_t fdec1_gram_floats(int64_t NI, int W) {
+    return NI * G_ITEM + G_THREADS * 16 + (int64_t)g_blocks() * g_kmax(NI, W) * G_PSLOT;
+}
+
 int fdec1_gram_launch(const LowRankDesc& d, float* gram, double* gq, hipStream_t s) {
     if (!fdec1_gram_supported(d) || !gram || !gq || !d.z4 || d.z_taps != 4) return -1;
-    HIP_CHECK_RET(hipMemsetAsync(gram, 0, (size_t)fdec1_gram_floats(d.NI) * sizeof(float), s));
+    const int nblk = g_blocks(), kmax = g_kmax(d.NI, d.W);
+    float* const part = gram + (int64_t)d.NI * G_ITEM + G_THREADS * 16;
     {
         KScope ks(s);
         if (ks.on()) ks.begin("fdec1_gram_q_kernel", 0.0, (double)fdec1_gram_q_doubles() * 8.0);
@@ -424,7 +482,15 @@ int fdec1_gram_launch(const LowRankDesc& d, float* gram, double* gq, hipStream_t
             const double fl = 2.0 * rows * G_CI * 8 * G_CO + 2.0 * (double)d.NI * d.W * G_CO * 4 * 20 * 256;
             ks.begin("fdec1_gram_kernel", fl, by);
         }
-        hipLaunchKernelGGL(fdec1_gram_kernel, dim3(g_blocks()), dim3(G_THREADS), 0, s, d, gram);
+        hipLaunchKernelGGL(fdec1_gram_kernel, dim3(nblk), dim3(G_THREADS), 0, s, d, gram, part, kmax);
+        HIP_CHECK_RET(hipGetLastError());
+    }
+    {
+        KScope ks(s);
+        const int NWB = (d.W + G_WB - 1) / G_WB;
+        if (ks.on()) ks.begin("fdec1_gram_reduce_kernel", 0.0, (double)nblk * kmax * G_PSLOT * 4.0 + d.NI * G_ITEM * 4.0);
+        hipLaunchKernelGGL(fdec1_gram_reduce_kernel, dim3((8 * G_NBLK * 64 + 255) / 256, d.NI), dim3(256), 0, s, part,
+                           gram, kmax, d.NI * NWB, nblk / G_NG, NWB);
         HIP_CHECK_RET(hipGetLastError());
     }
     {

@@ -180,7 +180,7 @@ size_t plan(Arena& ar, const Dims& d, Bufs& b, bool actbf) {
     if (d.chunks > 1) b.FO2 = ar.take<float>(NI * Ts * Ts * 2);
     b.ola_part = ar.take<float>(istft_ola_part_floats(NI, (int)Ts));
     b.lrsteps = ar.take<LrStep>(Ts + 1);
-    b.gram = actbf ? ar.take<float>(fdec1_gram_floats(NI)) : nullptr;
+    b.gram = actbf ? ar.take<float>(fdec1_gram_floats(NI, (int)Ts)) : nullptr;
     b.gramq = actbf ? ar.take<double>(fdec1_gram_q_doubles()) : nullptr;
     return ar.off;
 }

@@ -124,9 +124,9 @@ int fdec_lr_steps_launch(LrStep* steps, int Hd, int Hs, int Hk, int H_skip, hipS
 int fdec_lr_stats_launch(const LowRankDesc& d, hipStream_t s);
 int fdec_lr_merge_launch(const LowRankDesc& d, hipStream_t s);
 // fdec1f.hip: the statistics pass as Gram matrices of Z tiles computed in LDS (bf16 mode, Co = 96, Ci = 192, Hs = 32,
-// Hk = 8, Hd > 32); gram: fdec1_gram_floats(NI) floats, gq: fdec1_gram_q_doubles() doubles of workspace
+// Hk = 8, Hd > 32); gram: fdec1_gram_floats(NI, W) floats, gq: fdec1_gram_q_doubles() doubles of workspace
 bool fdec1_gram_supported(const LowRankDesc& d);
-int64_t fdec1_gram_floats(int64_t NI);
+int64_t fdec1_gram_floats(int64_t NI, int W);
 int64_t fdec1_gram_q_doubles();
 int fdec1_gram_launch(const LowRankDesc& d, float* gram, double* gq, hipStream_t s);
 // fenc_row.hip: a whole narrow frequency-encoder level (conv + GELU + DConv + rewrite GLU) per (b, f) row, bf16 mode

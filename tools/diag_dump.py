@@ -21,22 +21,29 @@ def main():
     m = AudioTextHTDemucs(dtype="bf16", text_table={s: t[i] for i, s in enumerate(STEMS)})
     m.load_state_dict(synthetic_state_dict(seed=0))
     m = m.to("cuda").eval()
-    wav = torch.as_tensor(synthetic_batch(2, 264600, seed0=31)).cuda()
+    # DIAG_B / DIAG_SEED / DIAG_RUNS: batch, synthetic seed, forwards compared against the first
+    nb, seed, runs = (int(os.environ.get(k, v)) for k, v in (("DIAG_B", 2), ("DIAG_SEED", 31), ("DIAG_RUNS", 2)))
+    wav = torch.as_tensor(synthetic_batch(nb, 264600, seed0=seed)).cuda()
     outs = []
-    for k in range(2):
+    for k in range(runs):
         d = tempfile.mkdtemp()
         os.environ["ATHD_DUMP"] = d
-        m.forward_prompts(wav, list(STEMS))
+        y = m.forward_prompts(wav, list(STEMS))
         torch.cuda.synchronize()
-        outs.append({n: np.fromfile(os.path.join(d, n), np.uint8) for n in sorted(os.listdir(d)) if n != "index.txt"})
+        o = {n: np.fromfile(os.path.join(d, n), np.uint8) for n in sorted(os.listdir(d)) if n != "index.txt"}
+        o["output"] = y.cpu().numpy().view(np.uint8).ravel()
+        outs.append(o)
     del os.environ["ATHD_DUMP"]
-    for n in outs[0]:
-        a, b = outs[0][n], outs[1][n]
-        print(f"{n}: {int((a != b).sum())} of {a.size} bytes differ", flush=True)
-        if n == "stats.raw" and (a != b).any():
-            da, db = a.view(np.float64), b.view(np.float64)
-            for i in np.nonzero(da != db)[0][:40]:
-                print(f"   stats[{i}]: {da[i]!r} vs {db[i]!r}", flush=True)
+    for k in range(1, runs):
+        print(f"-- run 0 vs run {k}", flush=True)
+        for n in outs[0]:
+            a, b = outs[0][n], outs[k][n]
+            if (a != b).any() or k == 1:
+                print(f"{n}: {int((a != b).sum())} of {a.size} bytes differ", flush=True)
+            if n == "stats.raw" and (a != b).any():
+                da, db = a.view(np.float64), b.view(np.float64)
+                for i in np.nonzero(da != db)[0][:40]:
+                    print(f"   stats[{i}]: {da[i]!r} vs {db[i]!r}", flush=True)
 
 if __name__ == "__main__":
     main()
