@@ -244,21 +244,22 @@ def test_fdec1_gram_large_mean(state_dict, text_table, monkeypatch):
 
 
 def test_bf16_forward_reproducible(models):
-    """Two bf16 forwards of the same inputs (bench shape: 6 s segments x 4 prompts) agree to >= 150 dB.  The level-1
-    frequency decoder's Gram statistics are summed from per-(workgroup, item) partial slots in a fixed order
-    (fdec1f.hip fdec1_gram_reduce_kernel; round 4's fp32 atomics made two forwards differ at ~121 dB).  Not bit-exact:
-    the per-item GroupNorm statistics are fp64 sums whose atomic order changes their last bit, which flips the fp32
-    rounding of a normalised value on rare outputs (~2e-5 of them)."""
+    """Two bf16 forwards of the same inputs (bench shape: 6 s segments x 4 prompts) are bit-identical (round 5):
+    the level-1 frequency decoder's Gram statistics are summed from per-(workgroup, item) partial slots in a fixed
+    order (fdec1f.hip fdec1_gram_reduce_kernel; round 4's fp32 atomics made two forwards differ at ~121 dB), and
+    tdec_tail_kernel pads its accumulator -> LDS stores explicitly (dec_last.hip: the compiler's 10 wait states let
+    a store read a stale register when the frequency branch ran beside it, ~100 outputs per forward)."""
     from athd.synth import synthetic_batch
     wav = torch.as_tensor(synthetic_batch(4, 264600, seed0=57)).cuda()
     prompts = ["drums", "bass", "other", "vocals"]
     m = models["bf16"]
     a = m.forward_prompts(wav, prompts)
-    b = m.forward_prompts(wav, prompts)
-    diff = int((a != b).sum().item())
-    s = sdr_db(a.cpu().numpy(), b.cpu().numpy())
-    _report("bf16_reproducible", {"differing_outputs": diff, "outputs": a.numel(), "sdr_db_run_to_run": s})
-    assert s >= 150.0 and diff <= a.numel() // 10000, (s, diff)
+    diffs = []
+    for _ in range(3):
+        b = m.forward_prompts(wav, prompts)
+        diffs.append(int((a != b).sum().item()))
+    _report("bf16_reproducible", {"differing_outputs": diffs, "outputs": a.numel()})
+    assert diffs == [0, 0, 0], diffs
 
 
 def test_batch_independence(models):
