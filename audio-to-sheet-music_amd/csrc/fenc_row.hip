@@ -101,15 +101,26 @@ namespace {
 constexpr int F0_NT = 18;                 // m-tiles per row
 constexpr int F0_TP = 16 * F0_NT;         // positions per row (T <= 288)
 constexpr int F0_C = 48, F0_H = 6;
-// LDS images (bf16 elements).  xs (the residual stream x, 2 halo rows each side): 160-B rows with the 16-B chunk
-// XOR-swizzled by (row >> 2) & 1; xin (conv input) and hs (DConv hidden) share one buffer of 64-B rows, chunk XOR
-// (row >> 1) & 3.  With these every fragment read (16 rows x 16 B per lane group; the conv3 taps shift rows by 0, +-1, +-2) and
-// every 8-B residual / hidden write is bank-conflict-free (round 3's padded pitches 56 / 40 cost 1.9 extra LDS cycles
-// per LDS instruction, SQ_LDS_BANK_CONFLICT).
-// (pitch 128 B with chunk XOR row & 7 is conflict-free too, but that layout made the compiler allocate 131 VGPRs:
-// two 6-wave workgroups per CU need <= 128)
-constexpr int F0_XIN_P = 32, F0_XS_P = 80, F0_HS_P = 32;
-ATHD_DEV int xs_off(int row, int col) { return row * F0_XS_P + (((col >> 3) ^ ((row >> 2) & 1)) << 3) + (col & 7); }
+// LDS images (bf16 elements).  xs (the residual stream x, 2 halo rows each side): 112-B rows (7 chunks of 16 B: an
+// odd chunk count, so 16 consecutive rows start in 16 distinct chunk slots of the 256-B bank space and every 16-row
+// fragment read - the conv3 taps shift rows by 0, +-1, +-2 - is conflict-free); xin (conv input) and hs (DConv
+// hidden) share one buffer of 64-B rows, chunk XOR (row >> 1) & 3.
+// Round 5: the 112-B rows replace round 4's 160-B rows (chunk XOR (row >> 2) & 1): 65.8 -> 51.7 KB of LDS per
+// workgroup, 2.23 -> 1.68 ms per forward (serialised events), whole step 1861 -> 1898 segments/s (one box); the
+// register target stays 4 waves per SIMD (ATHD_F0_WPE=5 reaches 96 VGPRs with 26 spilled: 1.87 ms).
+// (round 3's padded pitches 56 / 40 cost 1.9 extra LDS cycles per LDS instruction, SQ_LDS_BANK_CONFLICT, with the
+// 40-element hidden rows; pitch 80 with the swizzle is kept as ATHD_F0_XSP=80)
+#ifndef ATHD_F0_XSP
+#define ATHD_F0_XSP 56
+#endif
+#ifndef ATHD_F0_WPE
+#define ATHD_F0_WPE 4       // (waves per SIMD the register allocation targets)
+#endif
+constexpr int F0_XIN_P = 32, F0_XS_P = ATHD_F0_XSP, F0_HS_P = 32;
+ATHD_DEV int xs_off(int row, int col) {
+    if constexpr (F0_XS_P == 80) return row * F0_XS_P + (((col >> 3) ^ ((row >> 2) & 1)) << 3) + (col & 7);
+    else return row * F0_XS_P + col;      // (an odd number of 16-B chunks per row: 16-row fragment reads conflict-free)
+}
 ATHD_DEV int hs_off(int row, int col) { return row * F0_HS_P + (((col >> 3) ^ ((row >> 1) & 3)) << 3) + (col & 7); }
 // (both swizzles repeat every 8 rows, so an m-tile's image is the lane's offset at row l15 (+ halo, + tap shift) plus
 // mt * 16 rows: the per-tile part stays an immediate offset)
@@ -166,7 +177,7 @@ ATHD_DEV int opaque_lane() {
 }  // namespace
 
 
-__global__ __launch_bounds__(FR_NT, 4) void fenc_row0_kernel(const FencRowDesc d) {
+__global__ __launch_bounds__(FR_NT, ATHD_F0_WPE) void fenc_row0_kernel(const FencRowDesc d) {
     constexpr int C = F0_C, H = F0_H, NCT = 3, MTW = 9;
     __shared__ __attribute__((aligned(16))) bf16_t xin[F0_TP * F0_XIN_P];    // conv input, then the hidden tile
     __shared__ __attribute__((aligned(16))) bf16_t xs[(F0_TP + 2 * FR_HALO) * F0_XS_P];
