@@ -116,12 +116,18 @@ constexpr int F0_C = 48, F0_H = 6;
 #ifndef ATHD_F0_WPE
 #define ATHD_F0_WPE 4       // (waves per SIMD the register allocation targets)
 #endif
-constexpr int F0_XIN_P = 32, F0_XS_P = ATHD_F0_XSP, F0_HS_P = 32;
+#ifndef ATHD_F0_HSP
+#define ATHD_F0_HSP 32
+#endif
+constexpr int F0_XIN_P = ATHD_F0_HSP, F0_XS_P = ATHD_F0_XSP, F0_HS_P = ATHD_F0_HSP;
 ATHD_DEV int xs_off(int row, int col) {
     if constexpr (F0_XS_P == 80) return row * F0_XS_P + (((col >> 3) ^ ((row >> 2) & 1)) << 3) + (col & 7);
     else return row * F0_XS_P + col;      // (an odd number of 16-B chunks per row: 16-row fragment reads conflict-free)
 }
-ATHD_DEV int hs_off(int row, int col) { return row * F0_HS_P + (((col >> 3) ^ ((row >> 1) & 3)) << 3) + (col & 7); }
+ATHD_DEV int hs_off(int row, int col) {
+    if constexpr (F0_HS_P == 32) return row * F0_HS_P + (((col >> 3) ^ ((row >> 1) & 3)) << 3) + (col & 7);
+    else return row * F0_HS_P + col;      // (F0_HS_P = 40: 5 chunks per row; 56.4 KB in all: 2.16 ms, measured)
+}
 // (both swizzles repeat every 8 rows, so an m-tile's image is the lane's offset at row l15 (+ halo, + tap shift) plus
 // mt * 16 rows: the per-tile part stays an immediate offset)
 
