@@ -64,6 +64,15 @@ ATHD_DEV void section_barrier() {
     __builtin_amdgcn_sched_barrier(0);
 }
 
+// persistent grid: epilogues without residual or statistics (as gemm4); ATHD_G5_PRES=1 adds the residual-stream
+// epilogue with statistics (F_RES | F_STATS, not F_RGN: that one stages its affine through a ring slot)
+#ifndef ATHD_G5_PRES
+#define ATHD_G5_PRES 0
+#endif
+ATHD_HD constexpr bool g5_persist(unsigned F) {
+    return (F & (F_RES | F_STATS)) == 0 || (ATHD_G5_PRES && (F & F_RGN) == 0 && (F & ~(F_RES | F_STATS)) == 0);
+}
+
 ATHD_DEV int xcd_remap5(int i, int n) {
     const int q = n / 8, r = n % 8, x = i % 8;
     return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i / 8;
@@ -83,7 +92,7 @@ __device__ __attribute__((aligned(64))) uint4 g_zero_page5[4];
 // 8 pieces) instead of the counted-history branch chain; the last two K-steps keep the history.
 template <unsigned F, int PROBE = 0, bool LIN = false>
 __global__ __launch_bounds__(512) void gemm5_kernel(const GemmDesc d) {
-    constexpr bool PERSIST = (F & (F_RES | F_STATS)) == 0;
+    constexpr bool PERSIST = g5_persist(F);
     constexpr int TM = 8, TN = 4;
     constexpr int NW = 8;
     // one LDS array (cdna_hip_programming.md §5 item 4(a)): 8 staging slots | GroupNorm statistics | bias of the
@@ -416,7 +425,7 @@ static void launch5f(const GemmDesc& d, hipStream_t s) {
     const int64_t M = (int64_t)d.nb * d.H_out * d.W;
     const int64_t tiles = ((M + 255) / 256) * ((d.N + 255) / 256);
     int64_t grid = tiles;
-    if constexpr ((F & (F_RES | F_STATS)) == 0) {   // persistent: the resident blocks (one per CU), a multiple of 8
+    if constexpr (g5_persist(F)) {   // persistent: the resident blocks (one per CU), a multiple of 8
         static int per_cu = 0;   // a property of the kernel; the CU count is the current device's
         if (per_cu == 0) {
             (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, gemm5_kernel<F, PROBE, LIN>, 512, 0);
