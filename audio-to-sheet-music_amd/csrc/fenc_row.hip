@@ -107,7 +107,8 @@ constexpr int F0_C = 48, F0_H = 6;
 // hidden) share one buffer of 64-B rows, chunk XOR (row >> 1) & 3.
 // Round 5: the 112-B rows replace round 4's 160-B rows (chunk XOR (row >> 2) & 1): 65.8 -> 51.7 KB of LDS per
 // workgroup, 2.23 -> 1.68 ms per forward (serialised events), whole step 1861 -> 1898 segments/s (one box); the
-// register target stays 4 waves per SIMD (ATHD_F0_WPE=5 reaches 96 VGPRs with 26 spilled: 1.87 ms).
+// register target stays 4 waves per SIMD (ATHD_F0_WPE=5 reaches 96 VGPRs with 26 spilled: 1.87 ms).  The LDS size,
+// not the bank pattern, made the difference (56.4 KB with 80-B hidden rows: 2.16 ms).
 // (round 3's padded pitches 56 / 40 cost 1.9 extra LDS cycles per LDS instruction, SQ_LDS_BANK_CONFLICT, with the
 // 40-element hidden rows; pitch 80 with the swizzle is kept as ATHD_F0_XSP=80)
 #ifndef ATHD_F0_XSP
