@@ -37,6 +37,11 @@ def load_model(checkpoint_path: str, device: str = "cuda", dtype: str = "bf16",
     local Hugging Face cache as the reference does (`:26-28`, `text.load_clap`, `local_files_only=True`), the
     checkpoint's `clap.*` keys are loaded into it (`:34-35`), and the embeddings of the 4 stem prompts are computed
     once and cached (the CLAP tower is frozen: its output depends on the prompt string only)."""
+    if text_table is None and (clap is None) != (tokenizer is None):
+        # the reference builds the two together (`:26-28`); a lone tokenizer must not be silently replaced by the
+        # cached one, nor a lone model be left without one (ADVICE r05)
+        raise ValueError("load_model: pass both clap= and tokenizer=, or neither (then both come from the local "
+                         "Hugging Face cache), or text_table=")
     default_clap = text_table is None and clap is None
     if default_clap:
         clap, tokenizer = load_clap()

@@ -484,6 +484,13 @@ typedef __attribute__((ext_vector_type(4))) unsigned int u32x4_t;   // (arrays o
 typedef __attribute__((address_space(3))) void a32_lds_void;
 typedef __attribute__((address_space(1))) void a32_gbl_void;
 
+// round-6 form of attn32_kernel (DMA addressing from a uniform tile base, row-sum overflow check instead of a per-tile
+// max); 0 builds the round-5 form for A/B libraries
+#ifndef ATHD_ATTN_V6
+#define ATHD_ATTN_V6 1
+#endif
+constexpr float A32_SUMCHK = 1024.0f;               // max lane row sum of a tile before the exact-max rescale
+
 constexpr int A32_KP = 72;                          // K row pitch (bf16)
 constexpr int A32_VP = 64;                          // V row pitch (bf16), swizzled chunks
 
@@ -532,9 +539,11 @@ ATHD_DEV float exp2_poly(float x) {
                 sc[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_, qf[ks], sc[kb], 0, 0, 0);                 \
             }                                                                                                  \
         if (kt0 + KT > d.Nk) {                                                                                 \
+            int lim_ = d.Nk - kt0 - 4 * hh;            /* key index - kt0 - 4 hh vs constants: no per-key adds */ \
+            asm volatile("" : "+v"(lim_));             /* (keeps the compares in this branch, not hoisted) */  \
             _Pragma("unroll") for (int kb = 0; kb < NKB; ++kb)                                                \
                 _Pragma("unroll") for (int i = 0; i < 16; ++i)                                                 \
-                    if (kt0 + 32 * kb + (i & 3) + 8 * (i >> 2) + 4 * hh >= d.Nk) sc[kb][i] = -INFINITY;        \
+                    if (32 * kb + (i & 3) + 8 * (i >> 2) >= lim_) sc[kb][i] = -INFINITY;                       \
         }                                                                                                      \
     } while (0)
 // K tile element index of (key, 16-B chunk).  Register-staged: row pitch 72 (padding).  LDS-DMA staged: pitch 64,
@@ -597,6 +606,37 @@ __global__ __launch_bounds__(256, MINW) void attn32_kernel(const AttnDesc d) {
     }
     // LDS-DMA staging of tile KT0 into slot ST: wave w fills keys 8 (w + 4 j) .. +7 of K and of V, j < KT / 32
     const int dkey = lane >> 3, dph = lane & 7;
+#if ATHD_ATTN_V6
+    // round 6: a tile's sources are a wave-uniform base (the tile's first key row) plus a 32-bit per-lane byte
+    // offset (key row in the tile, clamped to the last key, times the row pitch, plus the swizzled chunk), so each
+    // piece is one v_min + one v_mad_u32_u24 and the load takes the SGPR-base form; the 64-bit per-piece address
+    // arithmetic of the round-2 form (v_mad_i64_i32 + v_lshl_add_u64 per piece) cost ~100 issue cycles per tile.
+    // The swizzles depend on key & 15 only, and KT0 is a multiple of 64, so they are tile-invariant.
+    const uint32_t kldb = (uint32_t)d.k_ld * 2u, vldb = (uint32_t)d.v_ld * 2u;
+    uint32_t kswz[KT / 32], vswz[KT / 32];
+#pragma unroll
+    for (int j = 0; j < KT / 32; ++j) {
+        const int kk = 8 * (wave + 4 * j) + dkey;
+        kswz[j] = 16u * (uint32_t)(dph ^ ((kk >> 1) & 7));
+        vswz[j] = 16u * (uint32_t)a32_vchunk(kk, dph);
+    }
+#define ATHD_A32_DMA(KT0, ST)                                                                                  \
+    {                                                                                                          \
+        const char* kt_ = (const char*)(Kb + (int64_t)(KT0) * d.k_ld);                                         \
+        const char* vt_ = (const char*)(Vb + (int64_t)(KT0) * d.v_ld);                                         \
+        const int last_ = d.Nk - 1 - (KT0);                                                                    \
+        _Pragma("unroll") for (int j = 0; j < KT / 32; ++j) {                                                 \
+            const uint32_t kc_ = (uint32_t)min(8 * (wave + 4 * j) + dkey, last_);                              \
+            uint32_t ko_ = __umul24(kc_, kldb) + kswz[j];                                     \
+            uint32_t vo_ = __umul24(kc_, vldb) + vswz[j];                                     \
+            asm volatile("" : "+v"(ko_), "+v"(vo_));     /* opaque: keeps (uniform base, 32-bit offset) */   \
+            __builtin_amdgcn_global_load_lds((a32_gbl_void*)(kt_ + ko_),                                       \
+                                             (a32_lds_void*)&Ks[ST][8 * (wave + 4 * j) * 64], 16, 0, 0);        \
+            __builtin_amdgcn_global_load_lds((a32_gbl_void*)(vt_ + vo_),                                       \
+                                             (a32_lds_void*)&Vs[ST][8 * (wave + 4 * j) * A32_VP], 16, 0, 0);   \
+        }                                                                                                      \
+    }
+#else
 #define ATHD_A32_DMA(KT0, ST)                                                                                  \
     _Pragma("unroll") for (int j = 0; j < KT / 32; ++j) {                                                     \
         const int kk = 8 * (wave + 4 * j) + dkey;                                                              \
@@ -606,6 +646,7 @@ __global__ __launch_bounds__(256, MINW) void attn32_kernel(const AttnDesc d) {
         __builtin_amdgcn_global_load_lds((a32_gbl_void*)(Vb + (int64_t)ka * d.v_ld + 8 * a32_vchunk(kk, dph)),  \
                                          (a32_lds_void*)&Vs[ST][8 * (wave + 4 * j) * A32_VP], 16, 0, 0);       \
     }
+#endif
 
     // transposed-read addresses (elements): lane 4q'+p of 16-lane group g' -> key row 4h + q' (+8, +16 s2, +32 kb),
     // d columns 32 db + 16 (g' & 1) + 4p
@@ -655,6 +696,64 @@ __global__ __launch_bounds__(256, MINW) void attn32_kernel(const AttnDesc d) {
             A32_PRIO(1);
             ATHD_A32_QK(-mrun);
             A32_PRIO(0);
+#if ATHD_ATTN_V6
+            // ---- online softmax (log2 units), round 6: no per-tile max ----
+            // The running max is set exactly on the first tile.  Later tiles exponentiate against it at once, and the
+            // lane's own row sum (its 32 P values, computed anyway) tells whether any of its P exceeds A32_SUMCHK: only
+            // then (rare, __any) are the scores recomputed, their exact max taken, O and l rescaled and the tile
+            // re-exponentiated - so P <= A32_SUMCHK always (the defer-max bound; bf16 P keeps its relative precision at
+            // any scale).  Saves the 17 v_max3 + swap + compare of every tile (~90 of ~900 issue cycles per tile).
+            auto tile_max = [&]() -> float {                      // max over the tile's scores of the lane's query
+                float mxk[NKB];
+#pragma unroll
+                for (int kb = 0; kb < NKB; ++kb) {
+                    float m = vmax3(sc[kb][0], sc[kb][1], sc[kb][2]);
+#pragma unroll
+                    for (int i = 3; i < 15; i += 2) m = vmax3(m, sc[kb][i], sc[kb][i + 1]);
+                    mxk[kb] = vmax3(m, sc[kb][15], sc[kb][15]);
+                }
+                float mx = mxk[0];
+#pragma unroll
+                for (int kb = 1; kb < NKB; ++kb) mx = vmax3(mx, mxk[kb], mxk[kb]);
+                return half_swap_max(mx);
+            };
+            auto exp_sum = [&]() -> float {                       // P = exp2(S) in place; the lane's row sum
+                athd_f2v ls2[NKB];                                 // one chain per key block
+#pragma unroll
+                for (int kb = 0; kb < NKB; ++kb) {
+                    ls2[kb] = (athd_f2v){0.f, 0.f};
+#pragma unroll
+                    for (int i = 0; i < 16; i += 2) {
+                        sc[kb][i] = __builtin_amdgcn_exp2f(sc[kb][i]);
+                        sc[kb][i + 1] = __builtin_amdgcn_exp2f(sc[kb][i + 1]);
+                        ls2[kb] += (athd_f2v){sc[kb][i], sc[kb][i + 1]};
+                    }
+                }
+#pragma unroll
+                for (int kb = 1; kb < NKB; ++kb) ls2[0] += ls2[kb];
+                return ls2[0].x + ls2[0].y;
+            };
+            if (t == 0) {                                          // first tile: the exact max (O and l are zero)
+                mrun = tile_max();
+                ATHD_A32_QK(-mrun);
+            }
+            float ls = exp_sum();
+            if (__any(!(ls <= A32_SUMCHK))) {                      // some P > A32_SUMCHK (or not finite): rescale
+                ATHD_A32_QK(-mrun);
+                const float dm = fmaxf(tile_max(), 0.f);
+                const float alpha = __builtin_amdgcn_exp2f(-dm);
+                mrun += dm;
+                lrun *= alpha;
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    o0[i] *= alpha;
+                    o1[i] *= alpha;
+                }
+                ATHD_A32_QK(-mrun);
+                ls = exp_sum();
+            }
+            lrun += ls;
+#else
             // ---- online softmax (log2 units) ----
             float mxk[NKB];
 #pragma unroll
@@ -701,6 +800,7 @@ __global__ __launch_bounds__(256, MINW) void attn32_kernel(const AttnDesc d) {
 #pragma unroll
             for (int kb = 1; kb < NKB; ++kb) ls2[0] += ls2[kb];
             lrun += ls2[0].x + ls2[0].y;
+#endif
             // ---- O^T += V^T P^T ----
             A32_PRIO(1);
 #pragma unroll

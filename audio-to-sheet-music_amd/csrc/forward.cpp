@@ -241,11 +241,11 @@ struct Run {
 // the second stream (time branch of the transformer and of the decoder) and its fork / join events, made once
 // ATHD_SERIAL=1: both branches on the caller's stream (profiling runs whose per-kernel times should be the kernel's
 // own; also the behaviour while an athd_profile window is open)
-// round-5 A/B switch: ATHD_ROWLN=0 keeps out_proj and the FFN's LayerNorm as two launches
+// round-5 A/B switch: ATHD_ROWLN=0 keeps out_proj and the FFN's LayerNorm as two launches; read at every forward
+// (tests/test_gpu_parity.py::test_rowln_off_matches_default switches it between calls)
 static bool rowln_enabled() {
-    static int v = -1;
-    if (v < 0) { const char* e = std::getenv("ATHD_ROWLN"); v = (e && e[0] == '0') ? 0 : 1; }
-    return v == 1;
+    const char* e = std::getenv("ATHD_ROWLN");
+    return !(e && e[0] == '0');
 }
 
 bool serial_branches(const Run& r) {

@@ -287,7 +287,9 @@ int gemm5_launch(const GemmDesc& d, hipStream_t s);
 
 bool rowln_supported(const GemmDesc& d);
 int rowln_launch(const GemmDesc& d, hipStream_t s);
+#ifdef ATHD_KBENCH
 int gemm6_launch(const GemmDesc& d, hipStream_t s);
+#endif
 
 int gemm_launch(const GemmDesc& d0, int mode, hipStream_t s) {
     if (d0.Kp % BK != 0 || d0.Kp < d0.K || d0.C_in <= 0 || d0.N <= 0) return -2;
@@ -304,12 +306,14 @@ int gemm_launch(const GemmDesc& d0, int mode, hipStream_t s) {
     // bf16 activations, N a multiple of 256: 256x256 tile, staggered two-group K-loop (gemm5.hip; it replaced round
     // 2's gemm4.hip, which tools/kbench still builds as the A/B baseline: kbench +6..16 % on the transformer shapes,
     // equal at K = 2048).  (Measured on N = 192 / 384: slower than gemm3's 256x192 tiles, which waste no columns.)
-    // dense linear rows without a residual epilogue, B from L2 (gemm6.hip, round-5 experiment: only with ATHD_G6=1;
-    // -2 otherwise or when the shape or epilogue is not its)
+#ifdef ATHD_KBENCH
+    // dense linear rows without a residual epilogue, B from L2 (gemm6.hip, round-5 experiment, measured slower than
+    // gemm5: built into tools/libkbench.so only, with ATHD_G6=1; -2 otherwise or when the shape is not its)
     if (mode == 1) {
         const int rc = gemm6_launch(d, s);
         if (rc != -2) return rc;
     }
+#endif
     if (mode == 1 && gemm5_supported(d) && d.N % 256 == 0) return gemm5_launch(d, s);
     // other N >= 192: 256x192 or 192x192 tile, 8 waves (gemm3.hip)
     // (K >= 384: 192x192 tiles with a 3-stage ring, two K-tiles in flight across each barrier; measured per call

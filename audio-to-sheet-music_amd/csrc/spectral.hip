@@ -117,8 +117,9 @@ ATHD_DEV void exchange(cx<R> (&v)[16], void* lds, Dst dst, int j) {
 // (the f32 parity mode) reads every power from the table; R = float takes them as running products of the two base
 // twiddles the caller loaded once (tw16, tw256): no table loads per frame (30 dependent L2 round trips per frame were
 // most of the iSTFT's wait time, SQ), at <= 15 ulp of twiddle error, below the fp32 FFT's own rounding over 12 stages.
+// (no defaults for tw16 / tw256: a float caller that forgot them would run on zero twiddles)
 template <typename R, typename TW>
-ATHD_DEV void fft4096(cx<R> (&v)[16], void* lds, const TW* __restrict__ tw, int j, cpx tw16 = {}, cpx tw256 = {}) {
+ATHD_DEV void fft4096(cx<R> (&v)[16], void* lds, const TW* __restrict__ tw, int j, cpx tw16, cpx tw256) {
     constexpr bool REC = sizeof(R) == 4;
     dft16(v);                                                       // Ns = 1: no twiddles
     exchange(v, lds, [j](int q) { return 16 * j + q; }, j);

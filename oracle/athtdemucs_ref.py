@@ -161,6 +161,8 @@ class AudioTextHTDemucsRef:
         Fq, T_spec = mag.shape[2], mag.shape[3]
         x_cond, xt_cond = self.text_attn(x_enc, xt_enc, text_emb)
         x_dec = self.freq_decoder(x_cond, saved[::-1], lengths[::-1])
+        if capture is not None:
+            capture["x_fdec"] = x_dec        # FreqDecoder output, before freq_out (`:293`)
         x_dec = F.conv2d(x_dec, *self.freq_out)
         if capture is not None:
             capture["x_fo"] = x_dec

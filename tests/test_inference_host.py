@@ -22,6 +22,18 @@ def test_load_model_reads_checkpoint(tmp_path, state_dict):
     assert m.device == torch.device("cuda", 0) and not m.training
 
 
+def test_load_model_rejects_lone_tokenizer_or_clap(tmp_path):
+    """a caller-given tokenizer without a CLAP model (or the reverse) is an error, not silently replaced
+    by the cached pair (the reference builds the two together, test_inference.py:26-28)."""
+    from athd.inference import load_model
+    path = tmp_path / "best_model.pt"
+    torch.save({"model_state_dict": {}}, path)
+    with pytest.raises(ValueError, match="both clap= and tokenizer="):
+        load_model(str(path), device="cuda", tokenizer=object())
+    with pytest.raises(ValueError, match="both clap= and tokenizer="):
+        load_model(str(path), device="cuda", clap=object())
+
+
 def test_load_state_dict_reports_missing_and_strict():
     from athd.model import AudioTextHTDemucs
     m = AudioTextHTDemucs(dtype="bf16")

@@ -38,6 +38,14 @@ def test_oracle_matches_reference_fixture(oracle_model, text_table, name):
         for k in ("x_enc", "xt_enc", "x_cond", "xt_cond"):
             a, b = cap[k].numpy(), g[k]
             assert np.abs(a - b).max() <= 1e-5 * max(1.0, np.abs(b).max()), k
+    if "x_fdec" in g:
+        # the reference-owned decoders (ATHTDemucs_v2.py:61-139, captured at :293 / :313 by oracle/gen_golden.py):
+        # the 259-row freq decoder and the off-by-one x0.1 skips, pinned at their own stage to 1e-5 * RMS
+        for k, ck in (("x_fdec", "x_fdec"), ("xt_tdec", "xt_dec3")):
+            a, b = cap[ck].numpy(), g[k]
+            assert a.shape == b.shape, (k, a.shape, b.shape)
+            rms = float(np.sqrt(np.mean(b.astype(np.float64) ** 2)))
+            assert np.abs(a - b).max() <= 1e-5 * rms, (k, float(np.abs(a - b).max()), rms)
 
 
 def test_oracle_full_length_stats(oracle_model, text_table):
