@@ -490,6 +490,9 @@ typedef __attribute__((address_space(1))) void a32_gbl_void;
 #define ATHD_ATTN_V6 1
 #endif
 constexpr float A32_SUMCHK = 1024.0f;               // max lane row sum of a tile before the exact-max rescale
+#ifndef ATHD_ATTN_KM
+#define ATHD_ATTN_KM 0        // 1: the running max subtracted by a fifth QK^T k-step (A/B)
+#endif
 
 constexpr int A32_KP = 72;                          // K row pitch (bf16)
 constexpr int A32_VP = 64;                          // V row pitch (bf16), swizzled chunks
@@ -506,7 +509,12 @@ ATHD_DEV float half_swap_sum(float x) {
     return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
-// v_max3_f32 without the canonicalising v_max(x, x) that fmaxf puts on MFMA results (inputs are never NaN here)
+// v_max3_f32 without the canonicalising v_max(x, x) that fmaxf puts on MFMA results (inputs are never NaN here).
+// HAZARD (round 6, tools/hazard/README.md): hipcc inserts no wait states before an inline-asm instruction that reads
+// an MFMA result (or a v_exp / v_rcp result): an asm VALU right after v_mfma_f32_32x32x16_bf16 reads the accumulator
+// registers before the MFMA has written them, where compiler-emitted VALU reads get s_nop 9.  The round-2..5 kernel's
+// per-tile max read the last QK^T MFMA's accumulators this way (a max of partly accumulated scores); the round-6
+// kernel's max (tile_max, first tile and rare rescales only) puts explicit wait states before it.
 ATHD_DEV float vmax3(float a, float b, float c) {
     float r;
     asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
@@ -546,6 +554,32 @@ ATHD_DEV float exp2_poly(float x) {
                     if (32 * kb + (i & 3) + 8 * (i >> 2) >= lim_) sc[kb][i] = -INFINITY;                       \
         }                                                                                                      \
     } while (0)
+// ATHD_ATTN_KM: the running max enters the scores as a fifth k-step of QK^T (K's column 64 is 1, Q's is -mrun, kept
+// bf16-exact), so the accumulators start from the inline constant 0 instead of 16 v_mov of -mrun per tile (the
+// fifth-step MFMA is the same for both key blocks: one extra MFMA per tile)
+#define ATHD_A32_QKM()                                                                                         \
+    do {                                                                                                       \
+        _Pragma("unroll") for (int kb = 0; kb < NKB; ++kb)                                                    \
+            sc[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k5, q5, (f32x16_t){}, 0, 0, 0);                \
+        _Pragma("unroll") for (int ks = 0; ks < 4; ++ks)                                                      \
+            _Pragma("unroll") for (int kb = 0; kb < NKB; ++kb) {                                              \
+                const bf16v8 a_ = *reinterpret_cast<const bf16v8*>(&K_[a32_kidx<DMA>(32 * kb + r, 2 * ks + hh)]); \
+                sc[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_, qf[ks], sc[kb], 0, 0, 0);                 \
+            }                                                                                                  \
+        if (kt0 + KT > d.Nk) {                                                                                 \
+            int lim_ = d.Nk - kt0 - 4 * hh;                                                                    \
+            asm volatile("" : "+v"(lim_));                                                                     \
+            _Pragma("unroll") for (int kb = 0; kb < NKB; ++kb)                                                \
+                _Pragma("unroll") for (int i = 0; i < 16; ++i)                                                 \
+                    if (32 * kb + (i & 3) + 8 * (i >> 2) >= lim_) sc[kb][i] = -INFINITY;                       \
+        }                                                                                                      \
+    } while (0)
+#if ATHD_ATTN_KM
+#define ATHD_A32_QKX() ATHD_A32_QKM()
+#else
+#define ATHD_A32_QKX() ATHD_A32_QK(-mrun)
+#endif
+
 // K tile element index of (key, 16-B chunk).  Register-staged: row pitch 72 (padding).  LDS-DMA staged: pitch 64,
 // chunk XOR-swizzled by (key >> 1) & 7 - the QK^T fragment reads (lanes = 32 consecutive keys, one chunk) then put the
 // 16 lanes of every ds_read_b128 group on 16 distinct 4-bank groups (key & 1 picks the bank half of the 128-B row).
@@ -586,6 +620,10 @@ __global__ __launch_bounds__(256, MINW) void attn32_kernel(const AttnDesc d) {
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks) qf[ks] = *reinterpret_cast<const bf16v8*>(Qp + 16 * ks);
     }
+#if ATHD_ATTN_KM
+    bf16v8 k5 = {}, q5 = {};                 // the fifth k-step: A row (key) k = 0 is 1, B column (query) k = 0 is -mrun
+    if (hh == 0) k5[0] = (__bf16)1.0f;
+#endif
 
     // staging: thread -> keys tid/8 + 32 j, 16-B chunk tid % 8 of the 128-B head row
     const bf16_t* Kb = (const bf16_t*)d.K + b * d.k_bs + d.k_off + h * 64;
@@ -694,7 +732,11 @@ __global__ __launch_bounds__(256, MINW) void attn32_kernel(const AttnDesc d) {
             f32x16_t sc[NKB];
             // (ATHD_A32_QK: key tail -> scores of keys >= Nk are -inf)
             A32_PRIO(1);
+#if ATHD_ATTN_V6
+            ATHD_A32_QKX();
+#else
             ATHD_A32_QK(-mrun);
+#endif
             A32_PRIO(0);
 #if ATHD_ATTN_V6
             // ---- online softmax (log2 units), round 6: no per-tile max ----
@@ -704,6 +746,11 @@ __global__ __launch_bounds__(256, MINW) void attn32_kernel(const AttnDesc d) {
             // re-exponentiated - so P <= A32_SUMCHK always (the defer-max bound; bf16 P keeps its relative precision at
             // any scale).  Saves the 17 v_max3 + swap + compare of every tile (~90 of ~900 issue cycles per tile).
             auto tile_max = [&]() -> float {                      // max over the tile's scores of the lane's query
+                // (the vmax3 asm reads MFMA results and hipcc pads nothing before it (see vmax3): the caller's MFMAs
+                // are fenced off by sched_barrier and 12 explicit wait states; compiler VALU reads get 10)
+                __builtin_amdgcn_sched_barrier(0);
+                asm volatile("s_nop 11" ::: "memory");
+                __builtin_amdgcn_sched_barrier(0);
                 float mxk[NKB];
 #pragma unroll
                 for (int kb = 0; kb < NKB; ++kb) {
@@ -733,23 +780,32 @@ __global__ __launch_bounds__(256, MINW) void attn32_kernel(const AttnDesc d) {
                 for (int kb = 1; kb < NKB; ++kb) ls2[0] += ls2[kb];
                 return ls2[0].x + ls2[0].y;
             };
+#if ATHD_ATTN_KM
+            // (mrun rounded to bf16: the fifth k-step multiplies it exactly; alpha uses the rounded values)
+            auto set_max = [&](float m) {
+                mrun = (float)(__bf16)m;
+                if (hh == 0) q5[0] = (__bf16)(-mrun);
+            };
+#else
+            auto set_max = [&](float m) { mrun = m; };
+#endif
             if (t == 0) {                                          // first tile: the exact max (O and l are zero)
-                mrun = tile_max();
-                ATHD_A32_QK(-mrun);
+                set_max(tile_max());
+                ATHD_A32_QKX();
             }
             float ls = exp_sum();
             if (__any(!(ls <= A32_SUMCHK))) {                      // some P > A32_SUMCHK (or not finite): rescale
-                ATHD_A32_QK(-mrun);
-                const float dm = fmaxf(tile_max(), 0.f);
-                const float alpha = __builtin_amdgcn_exp2f(-dm);
-                mrun += dm;
+                ATHD_A32_QKX();
+                const float m_old = mrun;
+                set_max(mrun + fmaxf(tile_max(), 0.f));
+                const float alpha = __builtin_amdgcn_exp2f(m_old - mrun);
                 lrun *= alpha;
 #pragma unroll
                 for (int i = 0; i < 16; ++i) {
                     o0[i] *= alpha;
                     o1[i] *= alpha;
                 }
-                ATHD_A32_QK(-mrun);
+                ATHD_A32_QKX();
                 ls = exp_sum();
             }
             lrun += ls;
@@ -867,6 +923,8 @@ __global__ __launch_bounds__(256, MINW) void attn32_kernel(const AttnDesc d) {
 #undef ATHD_A32_DMA
 
 #undef ATHD_A32_QK
+#undef ATHD_A32_QKM
+#undef ATHD_A32_QKX
 
 // kernel choice for the bf16 path (tools/kbench builds, -DATHD_KBENCH; the product always takes 0): 0 =
 // attn32_kernel<3, 2, true> (3 waves per SIMD, 64-key tiles, LDS-DMA staging), 1 = attn_bf16_kernel (16x16x32), 2 = attn32_kernel<2, 2>, 3 = attn32_kernel<2, 4> (128-key

@@ -605,14 +605,21 @@ __global__ __launch_bounds__(TL_NT) void tdec_tail_kernel(const DecLastDesc d) {
         for (int s = 0; s < 12; ++s) z[k] = __builtin_amdgcn_mfma_f32_16x16x4f32(wA[s], x[s], z[k], 0, 0, 0);
     }
     __syncthreads();                             // every wave is done reading the phase-1 tile
-    // The last chain's result goes straight from the accumulator registers into an LDS store.  hipcc (ROCm 7.2)
-    // separates the two by 10 wait states, which is short for v_mfma_f32_16x16x4_f32 on gfx950 (40-cycle result
-    // latency): under load (the frequency branch's kernels beside this one on the other stream) the store then read
-    // a stale first accumulator register - channel 0 of ~100 of 8.5 M outputs differed run to run (round 5,
-    // tools/diag_dump.py; never with ATHD_SERIAL=1).  An explicit 48-state pad, pinned between the chains and the stores.
+    // Round 5 put an explicit 48-state pad here: ~100 of 8.5 M outputs (channel 0) differed run to run with the two
+    // branch streams, never with ATHD_SERIAL=1, and the pad made 9 of 9 comparisons identical.  The explanation given
+    // then - that hipcc's padding between the last MFMA of a chain and the LDS store of its result is too short on
+    // gfx950 - does NOT hold: tools/hazard/mfma_ds.hip (profiles/r06_hazard.txt) stores v_mfma_f32_16x16x4_f32 results,
+    // single and at the end of 12-MFMA chains, after exactly N wait states, alone and beside a kernel saturating the
+    // matrix pipes: 0 mismatches in 2.6e8 lane-stores at hipcc's 9 states, stale values below 5.  ATHD_TDEC_PAD=0 builds
+    // without the pad (round 6 A/B of test_bf16_forward_reproducible).
+#ifndef ATHD_TDEC_PAD
+#define ATHD_TDEC_PAD 1
+#endif
+#if ATHD_TDEC_PAD
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
+#endif
 #pragma unroll
     for (int k = 0; k < 4; ++k)
         *reinterpret_cast<float4*>(zb + (64 * k + 16 * wave + p) * TZ_LD + 4 * cg) = make_float4(z[k][0], z[k][1], z[k][2], z[k][3]);

@@ -91,6 +91,7 @@ struct Bufs {
     double* gramq;
     void *S, *Z, *Zs;   // freq level 1 re-associated (fdec_lr.hip): per-tap products of the 32 / 8 source rows
     mutable float* xt2 = nullptr;   // time_out(time decoder) of the last decode chunk: D (fused tail) or G (ragged T)
+    float* skw[2] = {nullptr, nullptr};   // split-K tail scratch of the freq / time stream (gemm5, GemmDesc::sk_ws)
 };
 
 size_t plan(Arena& ar, const Dims& d, Bufs& b, bool actbf) {
@@ -182,6 +183,7 @@ size_t plan(Arena& ar, const Dims& d, Bufs& b, bool actbf) {
     b.lrsteps = ar.take<LrStep>(Ts + 1);
     b.gram = actbf ? ar.take<float>(fdec1_gram_floats(NI, (int)Ts)) : nullptr;
     b.gramq = actbf ? ar.take<double>(fdec1_gram_q_doubles()) : nullptr;
+    for (int i = 0; i < 2; ++i) b.skw[i] = actbf ? ar.take<float>(SK_WS_BYTES / 4) : nullptr;
     return ar.off;
 }
 
@@ -191,6 +193,7 @@ inline void* eoff(void* p, int64_t n, int ea) { return (char*)p + n * ea; }
 struct Run {
     athd_ctx* c;
     hipStream_t s;
+    const Bufs* b = nullptr;
     int mode;
     bool actbf;
     double* st_next;
@@ -232,6 +235,13 @@ struct Run {
         KSite site(w);
         check(gemm_launch(g, mode, s), w);
     }
+    // the split-K tail scratch of the stream this Run currently launches on (freq: caller's stream, time: s_time);
+    // ATHD_SK=0 turns the split off (read at every call: tests/test_gpu_parity.py::test_splitk_tail_matches_unsplit)
+    float* skws() const {
+        const char* e = std::getenv("ATHD_SK");
+        if (e && e[0] == '0') return nullptr;
+        return b ? b->skw[s == c->s_time ? 1 : 0] : nullptr;
+    }
 };
 
 // One encoder level's DConv (2 residual layers) on x viewed as [nb][L][C] (freq: nb = B*F rows along time).
@@ -246,6 +256,13 @@ struct Run {
 static bool rowln_enabled() {
     const char* e = std::getenv("ATHD_ROWLN");
     return !(e && e[0] == '0');
+}
+
+// ATHD_NT=1: linear1's output stored with non-temporal stores; ATHD_NT=2: also the QKV / Q / KV projections'.
+// Default 0 (plain stores): round 6 measured NT on linear1 0.26 ms per step slower (read per forward)
+static int gemm_nt_enabled() {
+    const char* e = std::getenv("ATHD_NT");
+    return e && e[0] >= '0' && e[0] <= '2' ? e[0] - '0' : 0;
 }
 
 bool serial_branches(const Run& r) {
@@ -546,7 +563,7 @@ void encode(Run& r, const Dims& d, const Bufs& b, const float* wav) {
         a.scale = r.actbf ? ATTN_SCALE_PRESCALED : 0.125f;     // bf16: queries prescaled at pack time (attn.h)
         if (!L.cross) {
             GemmDesc g = r.lin(L.qkv, Hq, ab, (int)B, N, 512);
-            g.C = sQKV; g.c_bf16 = ab;
+            g.C = sQKV; g.c_bf16 = ab; g.c_nt = gemm_nt_enabled() >= 2;
             r.gemm(g, "qkv");
             a.Q = sQKV; a.q_bf16 = ab; a.q_bs = N * 1536; a.q_ld = 1536; a.q_off = 0;
             a.K = sQKV; a.k_bf16 = ab; a.k_bs = N * 1536; a.k_ld = 1536; a.k_off = 512;
@@ -555,10 +572,10 @@ void encode(Run& r, const Dims& d, const Bufs& b, const float* wav) {
             char* Qb = (char*)sQKV;
             char* KVb = Qb + (size_t)B * d.Nmax * 512 * (ab ? 2 : 4);
             GemmDesc gq = r.lin(L.q, Hq, ab, (int)B, N, 512);
-            gq.C = Qb; gq.c_bf16 = ab;
+            gq.C = Qb; gq.c_bf16 = ab; gq.c_nt = gemm_nt_enabled() >= 2;
             r.gemm(gq, "q");
             GemmDesc gk = r.lin(L.kv, Hkv, ab, (int)B, Nk, 512);
-            gk.C = KVb; gk.c_bf16 = ab;
+            gk.C = KVb; gk.c_bf16 = ab; gk.c_nt = gemm_nt_enabled() >= 2;
             r.gemm(gk, "kv");
             a.Q = Qb; a.q_bf16 = ab; a.q_bs = N * 512; a.q_ld = 512; a.q_off = 0;
             a.K = KVb; a.k_bf16 = ab; a.k_bs = Nk * 1024; a.k_ld = 1024; a.k_off = 0;
@@ -586,10 +603,12 @@ void encode(Run& r, const Dims& d, const Bufs& b, const float* wav) {
         }
         GemmDesc g1 = r.lin(L.l1, Hq, ab, (int)B, N, 512);
         g1.C = sF1; g1.c_bf16 = ab; g1.act = ACT_GELU;
+        g1.c_nt = gemm_nt_enabled() >= 1;
         r.gemm(g1, "linear1");
         double* st = r.stats(B);
         GemmDesc g2 = r.lin(L.l2, sF1, ab, (int)B, N, 2048);
         g2.C = X; g2.res = X; g2.res_scale = L.g2; g2.stats = st;
+        g2.sk_ws = r.skws();                     // K = 2048: the last partial round of tiles split along K (gemm5)
         r.gemm(g2, "linear2");
         pend->st = st; pend->w = L.now; pend->b = L.nob;
     };
@@ -982,6 +1001,7 @@ int forward_impl(athd_ctx* c, const float* wav, int64_t B, int64_t T, const floa
     if (hipSetDevice(c->device) != hipSuccess) return c->fail(ATHD_EHIP, "hipSetDevice failed");
     Run r;
     r.c = c;
+    r.b = &b;
     r.s = (hipStream_t)stream;
     r.mode = c->mode;
     r.actbf = c->mode == 1;

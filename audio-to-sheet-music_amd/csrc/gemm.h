@@ -108,7 +108,19 @@ struct GemmDesc {
     const float* ln_b = nullptr;
     // with an f32 C and a residual (rowln.hip, N = 512): C keeps the rows, ln_out gets their LayerNorm as bf16
     void* ln_out = nullptr;
+    // split-K tail (gemm5, residual-stream epilogues, dense rows; gemm5.hip): scratch for the f32 partial tiles of
+    // the last, partial round of tiles (SK_WS_BYTES per stream).  Null: no split.  sk_full / sk_S are filled by the
+    // launcher (tiles computed whole, K pieces per tail tile).
+    float* sk_ws = nullptr;
+    int sk_full = 0, sk_S = 1;
+    // non-temporal output stores (the epilogue's paired 16-B bf16 stores): an output that no later kernel re-reads
+    // from L2 (e.g. linear1's F1, 543 MB) does not evict the A row blocks and weights the running tiles share
+    int c_nt = 0;
 };
+
+// per-stream scratch of the split-K tail: at most SK_MAX_PIECES f32 partial tiles of 256 x 256
+constexpr int SK_MAX_PIECES = 320;
+constexpr size_t SK_WS_BYTES = (size_t)SK_MAX_PIECES * 256 * 256 * 4;
 
 // Algorithmic work of one launch (prof.h): 2 M N K flops; bytes = unique activations read once + packed weights +
 // outputs (+ residual read).  mode 1 weights are bf16, mode 0 f32.

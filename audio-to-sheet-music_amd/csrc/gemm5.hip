@@ -28,6 +28,7 @@
 #include "gemm.h"
 #include "gemm_epi.h"
 
+#include <algorithm>
 #include <climits>
 #include <type_traits>
 
@@ -117,13 +118,26 @@ __global__ __launch_bounds__(512) void gemm5_kernel(const GemmDesc d) {
     int tile = blockIdx.x;
     int64_t m0 = 0;
     int n0 = 0;
+    // split-K tail (non-persistent launches, GemmDesc::sk_ws): blocks >= sk_full are K pieces of the last partial
+    // round's tiles; piece q covers K-tiles [kb0, kb0 + nk) of tile sk_full + q / sk_S and leaves its f32 partial tile
+    // in the scratch (gemm5_sk_reduce_kernel adds the pieces in order and runs the epilogue)
+    int kb0 = 0, nk = d.Kp / 64, sk_piece = -1;
     // this lane's slot rows: sr = 8 (wave + 8 q) + lrow, q = 0, 1 (gemm4's piece map)
     uint32_t a_base[2][2];
     int a_h0[2][2];
     uint32_t b_off[2];
     const uint32_t a_ld2 = (uint32_t)d.a_ld * 2u;
     auto setup = [&](int t) {
-        const int id = xcd_remap5(t, ntiles);
+        int id;
+        if (!PERSIST && d.sk_ws && t >= d.sk_full) {
+            const int q = t - d.sk_full, j = q / d.sk_S, p = q - j * d.sk_S, nkt = d.Kp / 64;
+            id = d.sk_full + j;
+            kb0 = p * nkt / d.sk_S;
+            nk = (p + 1) * nkt / d.sk_S - kb0;
+            sk_piece = q;
+        } else {
+            id = xcd_remap5(t, !PERSIST && d.sk_ws ? d.sk_full : ntiles);
+        }
         m0 = (int64_t)(id / ntn) * 256;
         n0 = (id % ntn) * 256;
 #pragma unroll
@@ -150,20 +164,19 @@ __global__ __launch_bounds__(512) void gemm5_kernel(const GemmDesc d) {
             }
     };
     const uint32_t b_h1 = (uint32_t)(32 * d.Kp * 2);     // slot B1 rows are 32 columns further
-    const int nk = d.Kp / 64;
 
     auto issueA = [&](int kt, int h) {
         if (PROBE == 1 && kt > 1) return;
         char* dst = smem + ((kt & 1) * 4 + h) * G5_SLOT;
         if constexpr (LIN) {
-            const char* base = (const char*)d.A + (int64_t)kt * 128;      // wave-uniform
+            const char* base = (const char*)d.A + (int64_t)(kb0 + kt) * 128;      // wave-uniform
 #pragma unroll
             for (int q = 0; q < G5_PIECES; ++q)
                 __builtin_amdgcn_global_load_lds((gbl_void*)(base + a_base[h][q]), (lds_void*)(dst + (wave + NW * q) * 1024),
                                                  16, 0, 0);
             return;
         }
-        const int k = kt * 64 + 8 * chunk;
+        const int k = (kb0 + kt) * 64 + 8 * chunk;
         const bool kok = k < d.K;
         const int tap = k / d.C_in, ci = k - tap * d.C_in;
 #pragma unroll
@@ -177,7 +190,7 @@ __global__ __launch_bounds__(512) void gemm5_kernel(const GemmDesc d) {
     auto issueB = [&](int kt, int h) {
         if (PROBE == 1 && kt > 1) return;
         char* dst = smem + ((kt & 1) * 4 + 2 + h) * G5_SLOT;
-        const char* wb = (const char*)d.Wp + (int64_t)kt * 128 + (h ? b_h1 : 0u);
+        const char* wb = (const char*)d.Wp + (int64_t)(kb0 + kt) * 128 + (h ? b_h1 : 0u);
 #pragma unroll
         for (int q = 0; q < G5_PIECES; ++q)
             __builtin_amdgcn_global_load_lds((gbl_void*)(wb + b_off[q]), (lds_void*)(dst + (wave + NW * q) * 1024), 16, 0, 0);
@@ -238,14 +251,14 @@ __global__ __launch_bounds__(512) void gemm5_kernel(const GemmDesc d) {
     // prologue of a tile: K-tile 0 whole, then what the sections of K-tile -1 would have staged: A0(1), B0(1), B1(1)
     // (both groups) and A1(1) (G1; G0 stages its pieces in section 0); afterwards the pieces of K-tile 1 are the
     // in-flight history
-    const bool two = nk > 1;
+    // (nk is per block: a split-K piece covers a K range of its own)
     auto prologue = [&]() {
         issueA(0, 0);
         issueB(0, 0);
         issueB(0, 1);
         issueA(0, 1);
         hist[0] = hist[1] = hist[2] = hist[3] = 0;
-        if (two) {
+        if (nk > 1) {
             issueA(1, 0);
             issueB(1, 0);
             issueB(1, 1);
@@ -366,6 +379,17 @@ __global__ __launch_bounds__(512) void gemm5_kernel(const GemmDesc d) {
         } else {
             vm_wait_n(0);
         }
+        if (sk_piece >= 0) {                      // split-K piece: the raw partial tile, row-major [256][256] f32
+            float* slab = d.sk_ws + (size_t)sk_piece * 65536;
+            const int fr = lane & 15, fg = lane >> 4;
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+                    *reinterpret_cast<float4*>(slab + (wm0 + 16 * i + fr) * 256 + wn0 + 16 * j + 4 * fg) =
+                        make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+            break;
+        }
         float4 bias4[TN];
         {
             const float* bl = bias_lds + 256 * bsel + wn0 + 4 * (lane >> 4);
@@ -412,6 +436,59 @@ __global__ __launch_bounds__(512) void gemm5_kernel(const GemmDesc d) {
     }
 }
 
+// Split-K tail reduce (GemmDesc::sk_ws): block = 16 rows of one tail tile, thread = 4 columns of 4 rows.  The S f32
+// partial tiles of the tile are added in piece order (deterministic), then the residual-stream epilogue of
+// gemm_epilogue_res: out = res + res_scale * (acc + bias), f32, and the per-batch {sum, sumsq} statistics.
+__global__ __launch_bounds__(256) void gemm5_sk_reduce_kernel(const GemmDesc d) {
+    __shared__ double red[4][4][2];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int j = blockIdx.x >> 4, rb = (blockIdx.x & 15) * 16;
+    const int ntn = (d.N + 255) / 256;
+    const int id = d.sk_full + j;
+    const int64_t m0 = (int64_t)(id / ntn) * 256;
+    const int n0 = (id % ntn) * 256;
+    const uint32_t M = (uint32_t)d.nb * d.H_out * d.W;
+    const int c = 4 * lane, n = n0 + c;
+    const bool colok = n < d.N;
+    const float4 bias = d.bias && colok ? *reinterpret_cast<const float4*>(d.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4 sc = d.res_scale && colok ? *reinterpret_cast<const float4*>(d.res_scale + n)
+                                           : make_float4(1.f, 1.f, 1.f, 1.f);
+    const float* slab = d.sk_ws + (size_t)j * d.sk_S * 65536;
+    const uint32_t g0 = fdiv((uint32_t)(m0 + rb < M ? m0 + rb : M - 1), d.fd_hw);
+    double s1[2] = {0.0, 0.0}, s2[2] = {0.0, 0.0};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int r = rb + w + 4 * k;
+        const uint32_t m = (uint32_t)(m0 + r);
+        if (m >= M || !colok) continue;
+        float4 a = *reinterpret_cast<const float4*>(slab + r * 256 + c);
+        for (int p = 1; p < d.sk_S; ++p) {
+            const float4 b = *reinterpret_cast<const float4*>(slab + (size_t)p * 65536 + r * 256 + c);
+            a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+        }
+        const int64_t off = (int64_t)m * d.ldo + d.col_off + n;
+        const float4 rc = *reinterpret_cast<const float4*>((const float*)d.res + off);
+        const float4 o = make_float4(rc.x + sc.x * (a.x + bias.x), rc.y + sc.y * (a.y + bias.y), rc.z + sc.z * (a.z + bias.z),
+                                     rc.w + sc.w * (a.w + bias.w));
+        *reinterpret_cast<float4*>((float*)d.C + off) = o;
+        const int gi = fdiv(m, d.fd_hw) != g0 ? 1 : 0;     // 16 rows span at most two batches (H_out * W >= 16)
+        s1[gi] += (double)((o.x + o.y) + (o.z + o.w));
+        s2[gi] += (double)((o.x * o.x + o.y * o.y) + (o.z * o.z + o.w * o.w));
+    }
+    if (!d.stats) return;
+#pragma unroll
+    for (int gi = 0; gi < 2; ++gi) {
+        const double t1 = wave_sum_d(s1[gi]), t2 = wave_sum_d(s2[gi]);
+        if (lane == 0) { red[w][gi][0] = t1; red[w][gi][1] = t2; }
+    }
+    __syncthreads();
+    if (tid < 4) {
+        const int gi = tid >> 1, q = tid & 1;
+        const double v = (red[0][gi][q] + red[1][gi][q]) + (red[2][gi][q] + red[3][gi][q]);
+        if (v != 0.0) atomicAdd(&d.stats[2 * (g0 + gi) + q], v);
+    }
+}
+
 bool gemm5_supported(const GemmDesc& d) {
     const int64_t a_elems = (d.a_bs >= 0 ? d.a_bs : (int64_t)d.H_in * d.W * d.a_ld) * d.nb;
     // N % 64 == 0: the packed weights hold roundup(N, 256) rows (ctx.h up_gemm), the epilogue skips columns >= N
@@ -434,13 +511,47 @@ static void launch5f(const GemmDesc& d, hipStream_t s) {
         const int resident = per_cu > 0 ? per_cu * device_cus() / 8 * 8 : -1;
         if (resident >= 8 && resident < tiles) grid = resident;
     }
-    KScope ks(s);
-    if (ks.on()) {
-        double fl, by;
-        gemm_work(d, 1, fl, by);
-        ks.begin(klabel("gemm5_kernel<%u,%d,%s>", F, PROBE, LIN ? "true" : "false"), fl, by);
+    GemmDesc e = with_fastdiv(d);
+    int sk_tail = 0;
+    if constexpr (!g5_persist(F) && LIN && (F == (F_RES | F_STATS) || F == F_RES)) {
+        // split-K tail: a grid of `tiles` one-tile blocks at one block per CU runs ceil(tiles / R) rounds; the last
+        // round's `tail` tiles (e.g. linear2: 1036 = 4 x 256 + 12) leave the other CUs idle for a whole tile time.
+        // Those tiles are cut into S K pieces each (>= 4 K-tiles), computed as extra blocks of the same launch, and
+        // added up by gemm5_sk_reduce_kernel, which also runs their epilogue.
+        static int per_cu = 0;
+        if (per_cu == 0) {
+            (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, gemm5_kernel<F, PROBE, LIN>, 512, 0);
+            if (per_cu <= 0) per_cu = -1;
+        }
+        const int64_t R = per_cu > 0 ? (int64_t)per_cu * device_cus() : 0;
+        const int nkt = d.Kp / 64;
+        const int64_t tail = R > 0 ? tiles % R : 0;
+        if (d.sk_ws && epi_res_fast_ok(d) && tiles > R && tail > 0 && 2 * tail <= R && nkt >= 8) {
+            int S = (int)std::min<int64_t>(R / tail, nkt / 4);
+            S = std::min<int64_t>(S, SK_MAX_PIECES / tail);
+            if (S >= 2) {
+                e.sk_full = (int)(tiles - tail);
+                e.sk_S = S;
+                grid = e.sk_full + tail * S;
+                sk_tail = (int)tail;
+            }
+        }
     }
-    hipLaunchKernelGGL((gemm5_kernel<F, PROBE, LIN>), dim3((unsigned)grid), dim3(512), 0, s, with_fastdiv(d));
+    if (!sk_tail) e.sk_ws = nullptr;
+    {
+        KScope ks(s);
+        if (ks.on()) {
+            double fl, by;
+            gemm_work(d, 1, fl, by);
+            ks.begin(klabel("gemm5_kernel<%u,%d,%s>", F, PROBE, LIN ? "true" : "false"), fl, by);
+        }
+        hipLaunchKernelGGL((gemm5_kernel<F, PROBE, LIN>), dim3((unsigned)grid), dim3(512), 0, s, e);
+    }
+    if (sk_tail) {
+        KScope ks(s);
+        if (ks.on()) ks.begin("gemm5_sk_reduce_kernel", 0.0, (double)sk_tail * 65536 * 4 * (e.sk_S + 2));
+        hipLaunchKernelGGL(gemm5_sk_reduce_kernel, dim3((unsigned)sk_tail * 16), dim3(256), 0, s, e);
+    }
 }
 
 // dense single-tap rows: the LIN fast path of gemm5_kernel applies
@@ -456,6 +567,14 @@ static bool gemm5_lin(const GemmDesc& d) {
 
 int gemm5_launch(const GemmDesc& d, hipStream_t s) {
     const bool lin = ATHD_G5_LIN && gemm5_lin(d);
+    if (d.c_nt && epi_flags(d) == (F_GELU | F_CBF16)) {      // linear1: its output stored non-temporally
+        lin ? launch5f<F_GELU | F_CBF16 | F_NT, 0, true>(d, s) : launch5f<F_GELU | F_CBF16 | F_NT>(d, s);
+        return (int)hipGetLastError();
+    }
+    if (d.c_nt && epi_flags(d) == F_CBF16) {                 // the QKV / Q / KV projections
+        lin ? launch5f<F_CBF16 | F_NT, 0, true>(d, s) : launch5f<F_CBF16 | F_NT>(d, s);
+        return (int)hipGetLastError();
+    }
     switch (epi_flags(d)) {
 #define ATHD_CASE(FL) \
     case (FL): lin ? launch5f<(FL), 0, true>(d, s) : launch5f<(FL)>(d, s); break;

@@ -320,6 +320,17 @@ ATHD_DEV float* ola_part(float* part, int64_t item, int nwg, int k, int side, in
     return part + ((((item * nwg + k) * 2 + side) * 3 + blk) * 4) * 256 * 2;
 }
 
+// Lane -> FFT thread index j of the iSTFT (round 6): lanes l < 32 of wave w take j = 32 w + l + 1 and lane l + 32 takes
+// its Hermitian partner 256 - j, so the mirrored half of the packed spectrum (bins 4096 - kb, computed by the partner
+// of the thread that needs them) crosses between the two halves of one wave by v_permlane32_swap instead of an LDS
+// round trip with two workgroup barriers.  The self-mirrored j = 128 and j = 0 (lanes 31 and 63 of wave 3) use their
+// own values.  Any lane -> j map is valid for the FFT's LDS exchanges; outputs stay coalesced per 32-lane half.
+ATHD_DEV int istft_j(int tid) {
+    const int w = tid >> 6, l = tid & 63;
+    if (l < 32) return 32 * w + l + 1;
+    return tid == 255 ? 0 : 255 - 32 * w - (l - 32);
+}
+
 // FAST (R = float, the bf16 throughput mode): the mask's sigmoid and phase division and the envelope division use
 // v_exp / v_rcp (~1 ulp) instead of the IEEE sequences; the f32 parity mode (R = double) keeps them exact.
 // PF: the next frame's spectrum is prefetched into registers during the current frame's FFT (32 VGPRs)
@@ -347,14 +358,16 @@ __global__ __launch_bounds__(256, MINW) void istft_ola_kernel(const float* __res
         const LinIdx li = lin_index(kb, Tspec, 2048);
         ltab[kb] = make_uint2((uint32_t)li.i0 | ((uint32_t)li.i1 << 16), __float_as_uint(li.l1));
     }
+    const int jl = istft_j((int)threadIdx.x);
+    const bool hi_half = (threadIdx.x & 63) >= 32;
     float env_in[4];                   // interior envelope of this thread's offsets j + 256 o (FAST: reciprocal)
-    ola_env_in(threadIdx.x, win2, env_in);
+    ola_env_in(jl, win2, env_in);
     if constexpr (FAST) {
 #pragma unroll
         for (int o = 0; o < 4; ++o) env_in[o] = __builtin_amdgcn_rcpf(env_in[o]);
     }
     cpx tw16, tw256;                    // (frame-invariant: fft4096's base twiddles, R = float)
-    if constexpr (FAST) fft4096_base(tw, (int)threadIdx.x, tw16, tw256);
+    if constexpr (FAST) fft4096_base(tw, jl, tw16, tw256);
     float acc[4][4][2];
 #pragma unroll
     for (int h = 0; h < 4; ++h)
@@ -370,7 +383,7 @@ __global__ __launch_bounds__(256, MINW) void istft_ola_kernel(const float* __res
     auto load_spec = [&](int t) {
         const float* S = specT + (b * Tspec + t) * 2048LL * 4;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) zs[i] = *reinterpret_cast<const float4*>(S + (int64_t)(threadIdx.x + 256 * i) * 4);
+        for (int i = 0; i < 8; ++i) zs[i] = *reinterpret_cast<const float4*>(S + (int64_t)(jl + 256 * i) * 4);
     };
     auto put = [&](int side, int blk, int j) {             // acc[0] -> a partial slot (coalesced 8-B stores)
         float* pp = ola_part(part, item, nwg, k, side, blk);
@@ -395,9 +408,13 @@ __global__ __launch_bounds__(256, MINW) void istft_ola_kernel(const float* __res
         // the thread index made opaque per frame: the FFT's frame-invariant address arithmetic (twiddle pointers, LDS
         // slots) is recomputed each frame instead of being hoisted out of the loop and spilled
         int j;
-        asm volatile("v_mov_b32 %0, %1" : "=v"(j) : "v"((int)threadIdx.x));
-        // ---- masked, Hermitian-packed spectrum of frame t into LDS  ----
+        asm volatile("v_mov_b32 %0, %1" : "=v"(j) : "v"(jl));
+        // ---- masked, Hermitian-packed spectrum of frame t: the FFT input x[j + 256 r] in registers ----
+        // r < 8: this thread's bins kb = j + 256 r (Z_k); r >= 8: index 4096 - kb' with kb' = (256 - j) + 256 (15 - r),
+        // the partner lane's mirror value (Z_m), by v_permlane32_swap
         const float* F0 = fo + (item * (int64_t)Tspec + t) * Tspec * 2;
+        cx<R> v[16];
+        cpx mir[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             const int kb = j + 256 * i;
@@ -423,25 +440,27 @@ __global__ __launch_bounds__(256, MINW) void istft_ola_kernel(const float* __res
                 X1 = {ms1 * (z.z / d1), ms1 * (z.w / d1)};
             }
             if (kb == 0) { X0.y = 0.f; X1.y = 0.f; }
-            cpx Zk = {X0.x - X1.y, X0.y + X1.x};
-            buf[pidx(kb)] = {Zk.x, -Zk.y};
-            if (kb > 0) {
-                cpx Zm = {X0.x + X1.y, -X0.y + X1.x};
-                buf[pidx(NFFT - kb)] = {Zm.x, -Zm.y};
+            const cpx Zk = {X0.x - X1.y, X0.y + X1.x};
+            v[i] = {(R)Zk.x, (R)-Zk.y};
+            const cpx Zm = {X0.x + X1.y, -X0.y + X1.x};   // (kb = 0: unused)
+            mir[i] = {Zm.x, -Zm.y};
+        }
+        {
+            const bool self128 = j == 128, self0 = j == 0;
+#pragma unroll
+            for (int r = 8; r < 16; ++r) {
+                const cpx mine = mir[15 - r];
+                const auto sx = __builtin_amdgcn_permlane32_swap(__float_as_uint(mine.x), __float_as_uint(mine.x), false, false);
+                const auto sy = __builtin_amdgcn_permlane32_swap(__float_as_uint(mine.y), __float_as_uint(mine.y), false, false);
+                cpx z = {__uint_as_float(hi_half ? sx[0] : sx[1]), __uint_as_float(hi_half ? sy[0] : sy[1])};
+                if (self128) z = mine;                     // its own mirror bins 128 + 256 (15 - r)
+                if (self0) z = r == 8 ? cpx{0.f, 0.f} : mir[16 - r];   // the Nyquist bin 2048 (zero), own bins 256 (16 - r)
+                v[r] = {(R)z.x, (R)z.y};
             }
         }
-        if (j == 0) buf[pidx(2048)] = {0.f, 0.f};
         if constexpr (PF) {
             if (t + 1 < t1) load_spec(t + 1);              // next frame's spectrum, in flight during the FFT
         }
-        __syncthreads();
-        cx<R> v[16];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const cpx z = buf[pidx(j + 256 * r)];
-            v[r] = {(R)z.x, (R)z.y};
-        }
-        __syncthreads();
         fft4096(v, buf, tw, j, tw16, tw256);               // ends synced: buf is free for the next frame
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
@@ -458,7 +477,7 @@ __global__ __launch_bounds__(256, MINW) void istft_ola_kernel(const float* __res
         shift();
     }
     // tail blocks f_last + 1 .. + 3: final if no real frame follows, else partial
-    const int j = threadIdx.x;
+    const int j = jl;
 #pragma unroll
     for (int h = 0; h < 3; ++h) {
         if (t1 >= Tspec) ola_finish<FAST>(t1 + 2 + h, j, acc[0], T, env_in, x2, mean, stdv, o0, o1);
