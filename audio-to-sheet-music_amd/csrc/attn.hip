@@ -922,6 +922,338 @@ __global__ __launch_bounds__(256, MINW) void attn32_kernel(const AttnDesc d) {
 #undef ATHD_A32_STASH
 #undef ATHD_A32_DMA
 
+// ----------------------------------------------------------------------------------------------------------------
+// Ping-pong form (ATHD_ATTN_PP=1): 8 waves in two groups of 4, G0 = waves 0-3 and G1 = waves 4-7
+// (one wave of each per SIMD), 32 queries per wave, 256 per workgroup, 64-key tiles.  A group spends a tile in two
+// sections separated by workgroup barriers:
+//   M(t)  MFMA section: QK^T of tile t into fresh score accumulators (started at -m, as attn32_kernel) and PV of tile
+//         t - 1 with the P packed in the group's previous section - 16 v_mfma_f32_32x32x16_bf16 at s_setprio 1;
+//   V(t)  softmax section: key-tail mask, exp2 + row sums, the A32_SUMCHK check (rare rescale: O and l scaled, the
+//         tile's scores recomputed), P -> bf16, this wave's LDS-DMA pieces of K(t + 3) and V(t + 2), and the K(t + 1)
+//         fragments for the next M.
+// G1 runs one section behind G0, so in every section one wave of each SIMD issues MFMAs while the other runs the
+// softmax: matrix beside VALU by construction (attn32_kernel gets it from the chance alignment of three independent
+// workgroups per CU; MFMA busy 0.44, profiles/pmc_sq_r05.txt).
+// LDS: rings of 4 K slots and 4 V slots (8 KB each; attn32_kernel's swizzles).  K(t) is read in sections 2t - 1 (G0)
+// and 2t (G1), V(t) in 2t + 2 and 2t + 3; V(t) issues K(t + 3) into the slot of K(t - 1) and V(t + 2) into that of
+// V(t - 2), both free by then.  Before every barrier a wave waits (counted vmcnt) for all of its pieces except those
+// of its latest softmax section: every piece has >= 2 sections in flight and a barrier between landing and first read.
+// The fragment reads are inline asm with explicit lgkmcnt waits: the compiler cannot tell the ring slots apart and
+// would put a vmcnt(0) before every LDS read while DMAs are in flight.
+// Same arithmetic in the same order as attn32_kernel<3, 2, true>: the outputs are bit-identical (test_gpu_parity).
+constexpr int PP_KT = 64;                          // keys per tile
+constexpr int PP_SLOT_B = PP_KT * 64 * 2;          // bytes per K or V slot
+constexpr int PP_NS = 4;                           // slots per ring
+typedef __attribute__((ext_vector_type(2))) unsigned int pp_u32x2;
+
+ATHD_DEV void pp_vm_wait(int n) {                  // n wave-uniform, 0..4
+    if (n >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else if (n == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    else if (n == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else if (n == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// PRIO: 1 = s_setprio 1 around each MFMA section (as attn32_kernel); 0 = none; 2 = the static form for G1 only
+// (cdna_hip_programming.md T5; MI355X_MICROARCH.md §Two waves per SIMD item 2: a prio-1 MFMA wave delays the other
+// wave's v_exp by hundreds of cycles per section)
+template <int PRIO>
+__global__ __launch_bounds__(512, 1) void attn_pp_kernel(const AttnDesc d) {
+    constexpr int KT = PP_KT, NKB = 2;
+    __shared__ __attribute__((aligned(1024))) char smem_pp[2 * PP_NS * PP_SLOT_B];    // K ring | V ring (64 KB)
+    const uint32_t lds0 = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)smem_pp;
+    const uint32_t vring = lds0 + PP_NS * PP_SLOT_B;
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int grp = wave >> 2;
+    const int r = lane & 31, hh = lane >> 5;
+    int qblk, h;
+    int64_t b;
+    attn_tile(d, qblk, h, b, 256);
+    const int qw0 = qblk * 256 + wave * 32;
+    const bool active = qw0 < d.Nq;                               // wave-uniform
+    const int q = min(qw0 + r, d.Nq - 1);                          // rows past Nq compute on a copy, never stored
+    bf16v8 qf[4];
+    {
+        const bf16_t* Qp = (const bf16_t*)d.Q + b * d.q_bs + (int64_t)q * d.q_ld + d.q_off + h * 64 + 8 * hh;
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) qf[ks] = *reinterpret_cast<const bf16v8*>(Qp + 16 * ks);
+    }
+    const bf16_t* Kb = (const bf16_t*)d.K + b * d.k_bs + d.k_off + h * 64;
+    const bf16_t* Vb = (const bf16_t*)d.V + b * d.v_bs + d.v_off + h * 64;
+    const int T = (d.Nk + KT - 1) / KT;
+
+    // LDS-DMA: wave w fills keys 8w .. 8w + 7 of every K and V tile (one 1-KB piece each); the lane fetches the logical
+    // 16-B chunk that the slot's swizzle puts at its physical chunk (attn32_kernel's images)
+    const int dkey = lane >> 3, dph = lane & 7, kk8 = 8 * wave + dkey;
+    const uint32_t kswz = 16u * (uint32_t)(dph ^ ((kk8 >> 1) & 7));
+    const uint32_t vswz = 16u * (uint32_t)a32_vchunk(kk8, dph);
+    const uint32_t kldb = (uint32_t)d.k_ld * 2u, vldb = (uint32_t)d.v_ld * 2u;
+    auto dma_k = [&](int t) {
+        const char* base = (const char*)(Kb + (int64_t)t * KT * d.k_ld);
+        uint32_t off = __umul24((uint32_t)min(kk8, d.Nk - 1 - t * KT), kldb) + kswz;
+        asm volatile("" : "+v"(off));
+        __builtin_amdgcn_global_load_lds((a32_gbl_void*)(base + off),
+                                         (a32_lds_void*)(smem_pp + (t & (PP_NS - 1)) * PP_SLOT_B + wave * 1024), 16, 0, 0);
+    };
+    auto dma_v = [&](int t) {
+        const char* base = (const char*)(Vb + (int64_t)t * KT * d.v_ld);
+        uint32_t off = __umul24((uint32_t)min(kk8, d.Nk - 1 - t * KT), vldb) + vswz;
+        asm volatile("" : "+v"(off));
+        __builtin_amdgcn_global_load_lds((a32_gbl_void*)(base + off),
+                                         (a32_lds_void*)(smem_pp + (PP_NS + (t & (PP_NS - 1))) * PP_SLOT_B + wave * 1024),
+                                         16, 0, 0);
+    };
+
+    // K fragment (key 32 kb + r, 16-B chunk 2 ks + hh) byte offsets in a slot: 128 r + 16 ((2 ks + hh) ^ ((r >> 1) & 7))
+    // + 4096 kb (the kb part is the immediate)
+    uint32_t koff[4];
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) koff[ks] = 128u * r + 16u * (uint32_t)((2 * ks + hh) ^ ((r >> 1) & 7));
+    // V transposed-read byte offsets (attn32_kernel's voff), + 2048 kk + 1024 for the upper 8 keys as immediates
+    const int g16 = lane >> 4, i16 = lane & 15, qr = i16 >> 2, pc = i16 & 3;
+    const int vrow = 4 * hh + qr;
+    uint32_t voffb[2];
+#pragma unroll
+    for (int db = 0; db < 2; ++db) {
+        const int col = 32 * db + 16 * (g16 & 1) + 4 * pc;
+        voffb[db] = 2u * (uint32_t)(vrow * A32_VP + 8 * a32_vchunk(vrow, col >> 3) + (col & 7));
+    }
+
+    bf16v8 kf[4][NKB];                          // K fragments of the tile the next QK^T uses
+    auto read_k = [&](int t) {
+        const uint32_t sb = lds0 + (uint32_t)(t & (PP_NS - 1)) * PP_SLOT_B;
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+            const uint32_t a = sb + koff[ks];
+            asm volatile("ds_read_b128 %0, %1" : "=v"(kf[ks][0]) : "v"(a));
+            asm volatile("ds_read_b128 %0, %1 offset:4096" : "=v"(kf[ks][1]) : "v"(a));
+        }
+    };
+    auto pin_k = [&]() {                         // after an lgkmcnt(0): the fragments are used no earlier
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) asm volatile("" : "+v"(kf[ks][0]), "+v"(kf[ks][1]));
+    };
+
+    f32x16_t o0, o1, sc[NKB];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) { o0[i] = 0.f; o1[i] = 0.f; }
+    float mrun = 0.f, lrun = 0.f;
+    bf16v8 pb[4];                               // P of the group's last softmax section, bf16, per PV k-step
+
+    auto qk = [&](float init) {
+#pragma unroll
+        for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) sc[kb][i] = init;
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+            for (int kb = 0; kb < NKB; ++kb) sc[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[ks][kb], qf[ks], sc[kb], 0, 0, 0);
+    };
+    auto mask_tail = [&](int kt0) {             // keys >= Nk -> -inf (last tile only)
+        if (kt0 + KT > d.Nk) {
+            int lim = d.Nk - kt0 - 4 * hh;
+            asm volatile("" : "+v"(lim));
+#pragma unroll
+            for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+                for (int i = 0; i < 16; ++i)
+                    if (32 * kb + (i & 3) + 8 * (i >> 2) >= lim) sc[kb][i] = -INFINITY;
+        }
+    };
+    auto tile_max = [&]() -> float {            // (explicit pad before the vmax3 asm: see vmax3)
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_nop 11" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        float mxk[NKB];
+#pragma unroll
+        for (int kb = 0; kb < NKB; ++kb) {
+            float m = vmax3(sc[kb][0], sc[kb][1], sc[kb][2]);
+#pragma unroll
+            for (int i = 3; i < 15; i += 2) m = vmax3(m, sc[kb][i], sc[kb][i + 1]);
+            mxk[kb] = vmax3(m, sc[kb][15], sc[kb][15]);
+        }
+        return half_swap_max(vmax3(mxk[0], mxk[1], mxk[1]));
+    };
+    auto exp_sum = [&]() -> float {
+        athd_f2v ls2[NKB];
+#pragma unroll
+        for (int kb = 0; kb < NKB; ++kb) {
+            ls2[kb] = (athd_f2v){0.f, 0.f};
+#pragma unroll
+            for (int i = 0; i < 16; i += 2) {
+                sc[kb][i] = __builtin_amdgcn_exp2f(sc[kb][i]);
+                sc[kb][i + 1] = __builtin_amdgcn_exp2f(sc[kb][i + 1]);
+                ls2[kb] += (athd_f2v){sc[kb][i], sc[kb][i + 1]};
+            }
+        }
+        ls2[0] += ls2[1];
+        return ls2[0].x + ls2[0].y;
+    };
+
+    // ---- prologue: K(0), K(1), V(0), K(2), V(1) (those that exist) ----
+    dma_k(0);
+    if (T > 1) dma_k(1);
+    dma_v(0);
+    if (T > 2) dma_k(2);
+    if (T > 1) dma_v(1);
+    const int npro = 2 + (T > 1 ? 2 : 0) + (T > 2 ? 1 : 0);
+    pp_vm_wait(npro - 1);                       // K(0) landed ...
+    __builtin_amdgcn_s_barrier();               // ... in every wave's pieces
+    __builtin_amdgcn_sched_barrier(0);
+    if (active) read_k(0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    pin_k();
+    int nlast = (T > 2 ? 1 : 0) + (T > 1 ? 1 : 0);   // pieces of the latest issuing section (the prologue's K(2), V(1))
+
+    // one section boundary: this wave's LDS reads retired, its pieces older than its latest softmax section landed
+    // (the first boundary after B0: K(1), which G0's V(0) reads), then the workgroup barrier
+    int nbar = 0;
+    auto boundary = [&]() {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        pin_k();
+        if (nbar++ == 0) pp_vm_wait(T > 1 ? npro - 2 : npro - 1);
+        else pp_vm_wait(nlast);
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    if (grp == 1) boundary();                   // the stagger: G1 runs one section behind G0
+    if constexpr (PRIO == 2) {
+        if (grp == 1) __builtin_amdgcn_s_setprio(1);
+    }
+    for (int t = 0; t <= T; ++t) {
+        // ---- M(t): QK^T of tile t, PV of tile t - 1 ----
+        if (active) {
+            pp_u32x2 vlo[4][2], vhi[4][2];
+            if (t >= 1) {
+                const uint32_t sb = vring + (uint32_t)((t - 1) & (PP_NS - 1)) * PP_SLOT_B;
+#pragma unroll
+                for (int db = 0; db < 2; ++db) {
+                    const uint32_t a = sb + voffb[db];
+                    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(vlo[0][db]) : "v"(a));
+                    asm volatile("ds_read_b64_tr_b16 %0, %1 offset:1024" : "=v"(vhi[0][db]) : "v"(a));
+                    asm volatile("ds_read_b64_tr_b16 %0, %1 offset:2048" : "=v"(vlo[1][db]) : "v"(a));
+                    asm volatile("ds_read_b64_tr_b16 %0, %1 offset:3072" : "=v"(vhi[1][db]) : "v"(a));
+                    asm volatile("ds_read_b64_tr_b16 %0, %1 offset:4096" : "=v"(vlo[2][db]) : "v"(a));
+                    asm volatile("ds_read_b64_tr_b16 %0, %1 offset:5120" : "=v"(vhi[2][db]) : "v"(a));
+                    asm volatile("ds_read_b64_tr_b16 %0, %1 offset:6144" : "=v"(vlo[3][db]) : "v"(a));
+                    asm volatile("ds_read_b64_tr_b16 %0, %1 offset:7168" : "=v"(vhi[3][db]) : "v"(a));
+                }
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (PRIO == 1) A32_PRIO(1);
+            if (t < T) qk(-mrun);
+            if (t >= 1) {
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+                    for (int db = 0; db < 2; ++db) asm volatile("" : "+v"(vlo[kk][db]), "+v"(vhi[kk][db]));
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk) {
+                    const pp_u32x2 l0 = vlo[kk][0], h0 = vhi[kk][0], l1 = vlo[kk][1], h1 = vhi[kk][1];
+                    const bf16v8 a0 = __builtin_bit_cast(bf16v8, (u32x4_t){l0.x, l0.y, h0.x, h0.y});
+                    const bf16v8 a1 = __builtin_bit_cast(bf16v8, (u32x4_t){l1.x, l1.y, h1.x, h1.y});
+                    o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, pb[kk], o0, 0, 0, 0);
+                    o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, pb[kk], o1, 0, 0, 0);
+                }
+            }
+            if constexpr (PRIO == 1) A32_PRIO(0);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        boundary();
+        if (t == T) break;
+        // ---- V(t): DMA, the next K fragments (their latency under the softmax), softmax of tile t ----
+        const int kt0 = t * KT;
+        nlast = 0;
+        if (t + 3 < T) { dma_k(t + 3); ++nlast; }
+        if (t + 2 < T) { dma_v(t + 2); ++nlast; }
+        if (active) {
+            if (t + 1 < T) read_k(t + 1);
+            // the recomputations of this tile's scores (first tile; rare rescale) re-read K(t) (its slot is rewritten
+            // only by V(t + 1)'s DMA) and then K(t + 1) again
+            auto with_kt = [&](auto&& fn) {
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                pin_k();
+                read_k(t);
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                pin_k();
+                fn();
+                if (t + 1 < T) read_k(t + 1);
+            };
+            mask_tail(kt0);
+            if (t == 0) {                                      // first tile: the exact max (O and l are zero)
+                with_kt([&]() {
+                    mrun = tile_max();
+                    qk(-mrun);
+                    mask_tail(kt0);
+                });
+            }
+            float ls = exp_sum();
+            if (__any(!(ls <= A32_SUMCHK))) {                  // some P > A32_SUMCHK (or not finite): rescale
+                with_kt([&]() {
+                    qk(-mrun);
+                    mask_tail(kt0);
+                    const float m_old = mrun;
+                    mrun = mrun + fmaxf(tile_max(), 0.f);
+                    const float alpha = __builtin_amdgcn_exp2f(m_old - mrun);
+                    lrun *= alpha;
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) {
+                        o0[i] *= alpha;
+                        o1[i] *= alpha;
+                    }
+                    qk(-mrun);
+                    mask_tail(kt0);
+                    ls = exp_sum();
+                });
+            }
+            lrun += ls;
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) {
+                const f32x16_t& sp = sc[kk >> 1];
+                const int j0 = 8 * (kk & 1);
+                const uint32_t w[4] = {pack2bf(sp[j0 + 0], sp[j0 + 1]), pack2bf(sp[j0 + 2], sp[j0 + 3]),
+                                       pack2bf(sp[j0 + 4], sp[j0 + 5]), pack2bf(sp[j0 + 6], sp[j0 + 7])};
+                pb[kk] = __builtin_bit_cast(bf16v8, w);
+            }
+        }
+        boundary();
+    }
+    if (grp == 0) boundary();                   // equal barrier counts
+
+    // ---- normalise; stage the wave's 32 x 64 output tile in LDS (the ring is free); store whole 128-B rows ----
+    const float l = half_swap_sum(lrun);
+    const float inv = 1.f / l;
+    bf16_t* stage = reinterpret_cast<bf16_t*>(smem_pp) + wave * 32 * A32_KP;    // 8 x 32 x 72 x 2 B = 36 KB
+    if (active) {
+#pragma unroll
+        for (int db = 0; db < 2; ++db) {
+            const f32x16_t& oo = db ? o1 : o0;
+#pragma unroll
+            for (int g4 = 0; g4 < 4; ++g4) {
+                const int dcol = 32 * db + 8 * g4 + 4 * hh;
+                *reinterpret_cast<uint2*>(&stage[r * A32_KP + dcol]) =
+                    make_uint2(pack2bf(oo[4 * g4] * inv, oo[4 * g4 + 1] * inv),
+                               pack2bf(oo[4 * g4 + 2] * inv, oo[4 * g4 + 3] * inv));
+            }
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);                         // lgkmcnt(0): the wave's own LDS writes landed
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int it = 0; it < 4; ++it) {
+            const int id = it * 64 + lane, row = id >> 3, ch = id & 7;
+            const int qq = qw0 + row;
+            if (qq < d.Nq) {
+                const uint4 v = *reinterpret_cast<const uint4*>(&stage[row * A32_KP + 8 * ch]);
+                *reinterpret_cast<uint4*>((bf16_t*)d.O + b * d.o_bs + (int64_t)qq * d.o_ld + h * 64 + 8 * ch) = v;
+            }
+        }
+    }
+}
+
 #undef ATHD_A32_QK
 #undef ATHD_A32_QKM
 #undef ATHD_A32_QKX
@@ -949,9 +1281,28 @@ static bool attn32_ok(const AttnDesc& d, int mode) {
            d.Nq > 0 && d.Nk > 0;
 }
 
+// ATHD_ATTN_PP=1/2/3: the bf16 path on attn_pp_kernel<1/0/2> (A/B; read at every launch)
+static int attn_pp_mode() {
+    const char* e = std::getenv("ATHD_ATTN_PP");
+    return e && e[0] >= '1' && e[0] <= '3' ? e[0] - '0' : 0;
+}
+
 int attn_launch(const AttnDesc& d, int mode, hipStream_t s) {
     if (d.heads * 64 > d.o_ld && d.o_ld != 0) return -2;
     const bool a32 = attn32_ok(d, mode);
+    const int ppm = attn_pp_mode();
+    if (a32 && attn_variant() == 0 && ppm) {
+        dim3 grid((unsigned)((d.Nq + 255) / 256) * (unsigned)d.heads * (unsigned)d.nb);
+        KScope ks(s);
+        if (ks.on()) {
+            const double nh = (double)d.nb * d.heads;
+            ks.begin("attn_pp_kernel", 4.0 * nh * d.Nq * d.Nk * 64, nh * 64 * 2.0 * (2.0 * d.Nq + 2.0 * d.Nk));
+        }
+        if (ppm == 1) hipLaunchKernelGGL(attn_pp_kernel<1>, grid, dim3(512), 0, s, d);
+        else if (ppm == 2) hipLaunchKernelGGL(attn_pp_kernel<0>, grid, dim3(512), 0, s, d);
+        else hipLaunchKernelGGL(attn_pp_kernel<2>, grid, dim3(512), 0, s, d);
+        return (int)hipGetLastError();
+    }
     const int qblock = 128;
     dim3 grid((unsigned)((d.Nq + qblock - 1) / qblock) * (unsigned)d.heads * (unsigned)d.nb);   // attn_tile decodes it
     KScope ks(s);

@@ -547,6 +547,9 @@ __global__ __launch_bounds__(TL_NT) void tdec_tail_kernel(const DecLastDesc d) {
     const int bxi = g % nbx;
     const int64_t item = seg * d.P + pr;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+#if ATHD_TDEC_PAD == 3
+    asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");   // A/B: the same delay at the kernel start
+#endif
     float mean, rstd;
     gn_params(d.stats, item, d.gn_count, mean, rstd);
     int r0;
@@ -608,17 +611,26 @@ __global__ __launch_bounds__(TL_NT) void tdec_tail_kernel(const DecLastDesc d) {
     // Round 5 put an explicit 48-state pad here: ~100 of 8.5 M outputs (channel 0) differed run to run with the two
     // branch streams, never with ATHD_SERIAL=1, and the pad made 9 of 9 comparisons identical.  The explanation given
     // then - that hipcc's padding between the last MFMA of a chain and the LDS store of its result is too short on
-    // gfx950 - does NOT hold: tools/hazard/mfma_ds.hip (profiles/r06_hazard.txt) stores v_mfma_f32_16x16x4_f32 results,
-    // single and at the end of 12-MFMA chains, after exactly N wait states, alone and beside a kernel saturating the
-    // matrix pipes: 0 mismatches in 2.6e8 lane-stores at hipcc's 9 states, stale values below 5.  ATHD_TDEC_PAD=0 builds
-    // without the pad (round 6 A/B of test_bf16_forward_reproducible).
+    // gfx950 - does NOT hold.  Round 6 (tools/hazard/README.md, profiles/r06_hazard.txt):
+    //   - probes: v_mfma_f32_16x16x4_f32 results stored after exactly N wait states, single and at the end of 12-MFMA
+    //     chains, alone and beside a matrix-saturating kernel: 0 stale in 2.6e8 lane-stores from 5 states on (hipcc
+    //     emits 9-10); the reverse order (LDS store, then an MFMA overwriting its data registers 1 state later): 0;
+    //   - builds (tools/diag_det4.py, 3 forwards each): no pad (ATHD_TDEC_PAD=0) 110 / 30 / 203 outputs differ; the pad's
+    //     sched_barrier fence alone, the same instruction order as the pad build without its wait states (2): 158 / 141;
+    //     the same 48 states at the kernel START instead (3): 0 / 0 / 0 / 0; no pad with ATHD_SERIAL=1: 0 / 0.
+    // So the wait states matter only as a delay of the workgroup relative to the kernels of the other branch stream,
+    // not as a hazard pad between MFMA and store: a timing-dependent interaction with the concurrent frequency-branch
+    // kernels (the differing outputs are confined to the first-scheduled segment and to channel 0).  Its root cause is
+    // not established; the pad is kept as the measured mitigation, guarded by test_bf16_forward_reproducible.
 #ifndef ATHD_TDEC_PAD
 #define ATHD_TDEC_PAD 1
 #endif
-#if ATHD_TDEC_PAD
+#if ATHD_TDEC_PAD == 1
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
+#elif ATHD_TDEC_PAD == 2 || ATHD_TDEC_PAD == 3
+    __builtin_amdgcn_sched_barrier(0);               // A/B: the pad's scheduling fence without its wait states
 #endif
 #pragma unroll
     for (int k = 0; k < 4; ++k)

@@ -531,6 +531,45 @@ def test_sharp_attention_encoder(state_dict, text_table):
         assert v >= (F32_STAGE_DB if key.startswith("f32") else SHARP_BF16_SDR_DB), res
 
 
+def test_attn_pingpong_bit_identical(models, state_dict, text_table):
+    """attn_pp_kernel (ATHD_ATTN_PP=1: two wave groups per SIMD alternating MFMA and softmax sections, attn.hip) does
+    attn32_kernel's arithmetic in the same order, so the bf16 forward is bit-identical with either kernel: on the
+    bench shape (6 s segments x 4 prompts: full and tail key tiles) and with sharpened attentions on a short input
+    (Nq / Nk below one 256-query block; the defer-max rescale branch taken)."""
+    from athd.model import AudioTextHTDemucs
+    from athd.synth import synthetic_batch
+    from athd.weights import STEMS
+
+    def both(fn):
+        outs = []
+        for pp in ("0", os.environ.get("ATHD_PP_TEST_MODE", "1")):
+            os.environ["ATHD_ATTN_PP"] = pp
+            try:
+                outs.append(fn())
+            finally:
+                del os.environ["ATHD_ATTN_PP"]
+        return outs
+
+    wav = torch.as_tensor(synthetic_batch(4, 264600, seed0=57)).cuda()
+    m = models["bf16"]
+    a, b = both(lambda: m.forward_prompts(wav, ["drums", "bass", "other", "vocals"]).cpu())
+    n_full = int((a != b).sum().item())
+    sd = dict(state_dict)
+    for k in sd:
+        if "crosstransformer" in k and k.endswith("in_proj_weight"):
+            w = np.array(sd[k], dtype=np.float32, copy=True)
+            w[:1024] *= SHARP_SCALE
+            sd[k] = w
+    ms = AudioTextHTDemucs(dtype="bf16", text_table={s: text_table[i] for i, s in enumerate(STEMS)})
+    ms.load_state_dict(sd)
+    ms = ms.to("cuda").eval()
+    wav2 = torch.as_tensor(synthetic_batch(2, 30000, seed0=11)).cuda()
+    c, e = both(lambda: ms(wav2, ["bass", "other"]).cpu())
+    n_sharp = int((c != e).sum().item())
+    _report("attn_pingpong", {"differing_full": n_full, "differing_sharp": n_sharp, "outputs": a.numel() + c.numel()})
+    assert n_full == 0 and n_sharp == 0, (n_full, n_sharp)
+
+
 @pytest.mark.parametrize("dt", ["f32", "bf16"])
 def test_graph_replay_matches_eager(models, dt):
     """capture_prompts: one forward_prompts captured into a HIP graph (both branch streams, event fork/joins,
