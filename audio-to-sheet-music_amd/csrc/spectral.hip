@@ -306,6 +306,22 @@ ATHD_DEV void ola_finish(int B, int j, const float (&y)[4][2], int T, const floa
     }
 }
 
+// ola_finish with the block's time-branch samples already loaded (xq[o] = x2[n], zero outside [0, T))
+template <bool FAST>
+ATHD_DEV void ola_finish_x(int B, int j, const float (&y)[4][2], int T, const float (&env_in)[4], const float2 (&xq)[4],
+                           float mean, float stdv, float* __restrict__ o0, float* __restrict__ o1) {
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+        const int n = B * HOP + j + 256 * o - 3584;
+        if (n >= 0 && n < T) {
+            const float r0 = FAST ? y[o][0] * env_in[o] : y[o][0] / env_in[o];
+            const float r1 = FAST ? y[o][1] * env_in[o] : y[o][1] / env_in[o];
+            o0[n] = r0 + (xq[o].x * stdv + mean);
+            o1[n] = r1 + (xq[o].y * stdv + mean);
+        }
+    }
+}
+
 // interior envelope at offsets j + 256 o of a hop block: frames B-3 .. B in ascending order
 ATHD_DEV void ola_env_in(int j, const float* __restrict__ win2, float (&e)[4]) {
 #pragma unroll
@@ -413,6 +429,17 @@ __global__ __launch_bounds__(256, MINW) void istft_ola_kernel(const float* __res
         // r < 8: this thread's bins kb = j + 256 r (Z_k); r >= 8: index 4096 - kb' with kb' = (256 - j) + 256 (15 - r),
         // the partner lane's mirror value (Z_m), by v_permlane32_swap
         const float* F0 = fo + (item * (int64_t)Tspec + t) * Tspec * 2;
+        // the time-branch samples of the block this frame completes (f = t + 2), loaded now and added after the FFT
+        // (round 6: their HBM latency was exposed at the end of every frame)
+        // (FAST only: the f32 parity mode's double FFT has no registers to spare)
+        float2 xq[4];
+        if constexpr (FAST) {
+#pragma unroll
+            for (int o = 0; o < 4; ++o) {
+                const int n = (t + 2) * HOP + j + 256 * o - 3584;
+                xq[o] = (n >= 0 && n < T) ? *reinterpret_cast<const float2*>(x2 + (int64_t)n * 2) : make_float2(0.f, 0.f);
+            }
+        }
         cx<R> v[16];
         cpx mir[8];
 #pragma unroll
@@ -473,6 +500,7 @@ __global__ __launch_bounds__(256, MINW) void istft_ola_kernel(const float* __res
         // block f = t + 2 has all of this workgroup's frames
         const int f = t + 2;
         if (t - t0 < 3 && k > 0) put(0, t - t0, j);        // head block: also takes workgroup k-1's last frames
+        else if constexpr (FAST) ola_finish_x<FAST>(f, j, acc[0], T, env_in, xq, mean, stdv, o0, o1);
         else ola_finish<FAST>(f, j, acc[0], T, env_in, x2, mean, stdv, o0, o1);
         shift();
     }

@@ -297,6 +297,8 @@ def main():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip the SDR, f32 and section measurements")
+    ap.add_argument("--decode-items", type=int, default=0,
+                    help="(segment, prompt) items per decode chunk (default: the whole batch, B x 4, in one chunk)")
     ap.add_argument("--dump-kernels", default=None, help="write the warmup step's per-kernel profile (JSON)")
     ap.add_argument("--kernel", default=None, help="roofline kernel (default: largest summed time in warmup)")
     ap.add_argument("--pipelines", type=int, default=1,
@@ -328,7 +330,8 @@ def main():
     B = args.batch
     tt = {s: table[i] for i, s in enumerate(STEMS)}
     # the whole per-GPU batch in one decode chunk (B x 4 items): fewer, larger decoder launches (≈49 GB: athd_workspace_bytes, reported as workspace_gb)
-    model = AudioTextHTDemucs(dtype=args.dtype, text_table=tt, decode_items=B * len(STEMS))
+    dec_items = args.decode_items or B * len(STEMS)
+    model = AudioTextHTDemucs(dtype=args.dtype, text_table=tt, decode_items=dec_items)
     model.load_state_dict(sd)
     model = model.to(dev).eval()
     # B distinct synthetic segments per rank, resident in HBM before timing (weak scaling: each rank owns its block)
@@ -360,7 +363,7 @@ def main():
     pipes = []
     if world == 1 and graphs and args.pipelines > 1:
         for k in range(1, args.pipelines):
-            mk = AudioTextHTDemucs(dtype=args.dtype, text_table=tt, decode_items=B * len(STEMS))
+            mk = AudioTextHTDemucs(dtype=args.dtype, text_table=tt, decode_items=dec_items)
             mk.load_state_dict(sd)
             mk = mk.to(dev).eval()
             wk = torch.as_tensor(synthetic_batch(B, SEG, seed0=1000 + B * (world + k))).to(dev)
@@ -484,7 +487,7 @@ def main():
                    "gather_timed": world > 1,
                    "launch": (f"hipGraph replay of one athd_forward_prompts per step ({len(graphs)} graph(s) per rank)"
                               if graphs else "eager"),
-                   "pipelines": len(pipes) + 1},
+                   "pipelines": len(pipes) + 1, "decode_items": dec_items},
         "stems_per_s": round(4 * value, 3),
         "roofline": roofline,
         "step_essential_tflops": round(step_tf, 2),
