@@ -258,13 +258,6 @@ static bool rowln_enabled() {
     return !(e && e[0] == '0');
 }
 
-// ATHD_NT=1: linear1's output stored with non-temporal stores; ATHD_NT=2: also the QKV / Q / KV projections'.
-// Default 0 (plain stores): round 6 measured NT on linear1 0.26 ms per step slower (read per forward)
-static int gemm_nt_enabled() {
-    const char* e = std::getenv("ATHD_NT");
-    return e && e[0] >= '0' && e[0] <= '2' ? e[0] - '0' : 0;
-}
-
 bool serial_branches(const Run& r) {
     static int env = -1;
     if (env < 0) {
@@ -563,7 +556,7 @@ void encode(Run& r, const Dims& d, const Bufs& b, const float* wav) {
         a.scale = r.actbf ? ATTN_SCALE_PRESCALED : 0.125f;     // bf16: queries prescaled at pack time (attn.h)
         if (!L.cross) {
             GemmDesc g = r.lin(L.qkv, Hq, ab, (int)B, N, 512);
-            g.C = sQKV; g.c_bf16 = ab; g.c_nt = gemm_nt_enabled() >= 2;
+            g.C = sQKV; g.c_bf16 = ab;
             r.gemm(g, "qkv");
             a.Q = sQKV; a.q_bf16 = ab; a.q_bs = N * 1536; a.q_ld = 1536; a.q_off = 0;
             a.K = sQKV; a.k_bf16 = ab; a.k_bs = N * 1536; a.k_ld = 1536; a.k_off = 512;
@@ -572,10 +565,10 @@ void encode(Run& r, const Dims& d, const Bufs& b, const float* wav) {
             char* Qb = (char*)sQKV;
             char* KVb = Qb + (size_t)B * d.Nmax * 512 * (ab ? 2 : 4);
             GemmDesc gq = r.lin(L.q, Hq, ab, (int)B, N, 512);
-            gq.C = Qb; gq.c_bf16 = ab; gq.c_nt = gemm_nt_enabled() >= 2;
+            gq.C = Qb; gq.c_bf16 = ab;
             r.gemm(gq, "q");
             GemmDesc gk = r.lin(L.kv, Hkv, ab, (int)B, Nk, 512);
-            gk.C = KVb; gk.c_bf16 = ab; gk.c_nt = gemm_nt_enabled() >= 2;
+            gk.C = KVb; gk.c_bf16 = ab;
             r.gemm(gk, "kv");
             a.Q = Qb; a.q_bf16 = ab; a.q_bs = N * 512; a.q_ld = 512; a.q_off = 0;
             a.K = KVb; a.k_bf16 = ab; a.k_bs = Nk * 1024; a.k_ld = 1024; a.k_off = 0;
@@ -603,7 +596,6 @@ void encode(Run& r, const Dims& d, const Bufs& b, const float* wav) {
         }
         GemmDesc g1 = r.lin(L.l1, Hq, ab, (int)B, N, 512);
         g1.C = sF1; g1.c_bf16 = ab; g1.act = ACT_GELU;
-        g1.c_nt = gemm_nt_enabled() >= 1;
         r.gemm(g1, "linear1");
         double* st = r.stats(B);
         GemmDesc g2 = r.lin(L.l2, sF1, ab, (int)B, N, 2048);

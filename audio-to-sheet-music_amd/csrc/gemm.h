@@ -113,9 +113,6 @@ struct GemmDesc {
     // launcher (tiles computed whole, K pieces per tail tile).
     float* sk_ws = nullptr;
     int sk_full = 0, sk_S = 1;
-    // non-temporal output stores (the epilogue's paired 16-B bf16 stores): an output that no later kernel re-reads
-    // from L2 (e.g. linear1's F1, 543 MB) does not evict the A row blocks and weights the running tiles share
-    int c_nt = 0;
 };
 
 // per-stream scratch of the split-K tail: at most SK_MAX_PIECES f32 partial tiles of 256 x 256

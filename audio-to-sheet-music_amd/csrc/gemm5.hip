@@ -567,14 +567,6 @@ static bool gemm5_lin(const GemmDesc& d) {
 
 int gemm5_launch(const GemmDesc& d, hipStream_t s) {
     const bool lin = ATHD_G5_LIN && gemm5_lin(d);
-    if (d.c_nt && epi_flags(d) == (F_GELU | F_CBF16)) {      // linear1: its output stored non-temporally
-        lin ? launch5f<F_GELU | F_CBF16 | F_NT, 0, true>(d, s) : launch5f<F_GELU | F_CBF16 | F_NT>(d, s);
-        return (int)hipGetLastError();
-    }
-    if (d.c_nt && epi_flags(d) == F_CBF16) {                 // the QKV / Q / KV projections
-        lin ? launch5f<F_CBF16 | F_NT, 0, true>(d, s) : launch5f<F_CBF16 | F_NT>(d, s);
-        return (int)hipGetLastError();
-    }
     switch (epi_flags(d)) {
 #define ATHD_CASE(FL) \
     case (FL): lin ? launch5f<(FL), 0, true>(d, s) : launch5f<(FL)>(d, s); break;

@@ -20,7 +20,6 @@ constexpr int EPI_MAXG = 32;   // GroupNorm groups tracked per block in LDS
 enum EpiFlag : unsigned {
     F_GELU = 1u, F_GLU = 2u, F_RES = 4u, F_STATS = 8u, F_GN = 16u, F_ROWADD = 32u, F_SPLIT = 64u, F_CBF16 = 128u,
     F_NOSTORE = 256u, F_PB = 512u, F_LN = 1024u, F_RGN = 2048u,
-    F_NT = 4096u,      // non-temporal paired bf16 stores (GemmDesc::c_nt; gemm5's dispatch only, not in epi_flags)
     F_ALL = 0xFFFFu
 };
 
@@ -275,11 +274,7 @@ ATHD_DEV void gemm_epilogue(const GemmDesc& d, const f32x4_t (&acc)[TM][TN], int
                                     const auto rx = __builtin_amdgcn_permlane16_swap(pk_even.x, pk.x, false, false);
                                     const auto ry = __builtin_amdgcn_permlane16_swap(pk_even.y, pk.y, false, false);
                                     const int col = n0 + wn0 + 16 * (j - 1) + 16 * (fg & 1) + 8 * (fg >> 1);
-                                    typedef __attribute__((ext_vector_type(4))) unsigned int u32v4;
-                                    u32v4* cp = reinterpret_cast<u32v4*>((bf16_t*)d.C + ob + col);
-                                    const u32v4 cv = {rx[0], ry[0], rx[1], ry[1]};
-                                    if constexpr (!GEN && (F & F_NT) != 0) __builtin_nontemporal_store(cv, cp);
-                                    else *cp = cv;
+                                    *reinterpret_cast<uint4*>((bf16_t*)d.C + ob + col) = make_uint4(rx[0], ry[0], rx[1], ry[1]);
                                 }
                             } else if (f_cbf) {
                                 *reinterpret_cast<uint2*>((bf16_t*)d.C + off) = make_uint2(pack2bf(o[0], o[1]), pack2bf(o[2], o[3]));
