@@ -436,44 +436,45 @@ __global__ __launch_bounds__(512) void gemm5_kernel(const GemmDesc d) {
     }
 }
 
-// Split-K tail reduce (GemmDesc::sk_ws): block = 16 rows of one tail tile, thread = 4 columns of 4 rows.  The S f32
-// partial tiles of the tile are added in piece order (deterministic), then the residual-stream epilogue of
-// gemm_epilogue_res: out = res + res_scale * (acc + bias), f32, and the per-batch {sum, sumsq} statistics.
+// Split-K tail reduce (GemmDesc::sk_ws): block = 4 rows of one tail tile (one per wave), lane = 4 columns.  The S f32
+// partial tiles of the tile are loaded together (all S pieces in flight) and added in piece order (deterministic),
+// then the residual-stream epilogue of gemm_epilogue_res: out = res + res_scale * (acc + bias), f32, and the per-batch
+// {sum, sumsq} statistics.  (Round 6: 16 rows per block with the pieces loaded row after row took 18 us per launch.)
+constexpr int SK_MAX_S = 16;
 __global__ __launch_bounds__(256) void gemm5_sk_reduce_kernel(const GemmDesc d) {
     __shared__ double red[4][4][2];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int j = blockIdx.x >> 4, rb = (blockIdx.x & 15) * 16;
+    const int j = blockIdx.x >> 6, r = (blockIdx.x & 63) * 4 + w;
     const int ntn = (d.N + 255) / 256;
     const int id = d.sk_full + j;
     const int64_t m0 = (int64_t)(id / ntn) * 256;
     const int n0 = (id % ntn) * 256;
     const uint32_t M = (uint32_t)d.nb * d.H_out * d.W;
     const int c = 4 * lane, n = n0 + c;
-    const bool colok = n < d.N;
-    const float4 bias = d.bias && colok ? *reinterpret_cast<const float4*>(d.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
-    const float4 sc = d.res_scale && colok ? *reinterpret_cast<const float4*>(d.res_scale + n)
-                                           : make_float4(1.f, 1.f, 1.f, 1.f);
+    const uint32_t m = (uint32_t)(m0 + r);
     const float* slab = d.sk_ws + (size_t)j * d.sk_S * 65536;
-    const uint32_t g0 = fdiv((uint32_t)(m0 + rb < M ? m0 + rb : M - 1), d.fd_hw);
+    const uint32_t mb = (uint32_t)(m0 + (blockIdx.x & 63) * 4);
+    const uint32_t g0 = fdiv(mb < M ? mb : M - 1, d.fd_hw);
     double s1[2] = {0.0, 0.0}, s2[2] = {0.0, 0.0};
+    if (m < M && n < d.N) {
+        float4 part[SK_MAX_S];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const int r = rb + w + 4 * k;
-        const uint32_t m = (uint32_t)(m0 + r);
-        if (m >= M || !colok) continue;
-        float4 a = *reinterpret_cast<const float4*>(slab + r * 256 + c);
-        for (int p = 1; p < d.sk_S; ++p) {
-            const float4 b = *reinterpret_cast<const float4*>(slab + (size_t)p * 65536 + r * 256 + c);
-            a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
-        }
+        for (int p = 0; p < SK_MAX_S; ++p)
+            if (p < d.sk_S) part[p] = *reinterpret_cast<const float4*>(slab + (size_t)p * 65536 + r * 256 + c);
         const int64_t off = (int64_t)m * d.ldo + d.col_off + n;
         const float4 rc = *reinterpret_cast<const float4*>((const float*)d.res + off);
+        const float4 bias = d.bias ? *reinterpret_cast<const float4*>(d.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+        const float4 sc = d.res_scale ? *reinterpret_cast<const float4*>(d.res_scale + n) : make_float4(1.f, 1.f, 1.f, 1.f);
+        float4 a = part[0];
+#pragma unroll
+        for (int p = 1; p < SK_MAX_S; ++p)
+            if (p < d.sk_S) { a.x += part[p].x; a.y += part[p].y; a.z += part[p].z; a.w += part[p].w; }
         const float4 o = make_float4(rc.x + sc.x * (a.x + bias.x), rc.y + sc.y * (a.y + bias.y), rc.z + sc.z * (a.z + bias.z),
                                      rc.w + sc.w * (a.w + bias.w));
         *reinterpret_cast<float4*>((float*)d.C + off) = o;
-        const int gi = fdiv(m, d.fd_hw) != g0 ? 1 : 0;     // 16 rows span at most two batches (H_out * W >= 16)
-        s1[gi] += (double)((o.x + o.y) + (o.z + o.w));
-        s2[gi] += (double)((o.x * o.x + o.y * o.y) + (o.z * o.z + o.w * o.w));
+        const int gi = fdiv(m, d.fd_hw) != g0 ? 1 : 0;     // 4 rows span at most two batches (H_out * W >= 4)
+        s1[gi] = (double)((o.x + o.y) + (o.z + o.w));
+        s2[gi] = (double)((o.x * o.x + o.y * o.y) + (o.z * o.z + o.w * o.w));
     }
     if (!d.stats) return;
 #pragma unroll
@@ -527,7 +528,7 @@ static void launch5f(const GemmDesc& d, hipStream_t s) {
         const int nkt = d.Kp / 64;
         const int64_t tail = R > 0 ? tiles % R : 0;
         if (d.sk_ws && epi_res_fast_ok(d) && tiles > R && tail > 0 && 2 * tail <= R && nkt >= 8) {
-            int S = (int)std::min<int64_t>(R / tail, nkt / 4);
+            int S = (int)std::min<int64_t>(std::min<int64_t>(R / tail, nkt / 4), SK_MAX_S);
             S = std::min<int64_t>(S, SK_MAX_PIECES / tail);
             if (S >= 2) {
                 e.sk_full = (int)(tiles - tail);
@@ -550,7 +551,7 @@ static void launch5f(const GemmDesc& d, hipStream_t s) {
     if (sk_tail) {
         KScope ks(s);
         if (ks.on()) ks.begin("gemm5_sk_reduce_kernel", 0.0, (double)sk_tail * 65536 * 4 * (e.sk_S + 2));
-        hipLaunchKernelGGL(gemm5_sk_reduce_kernel, dim3((unsigned)sk_tail * 16), dim3(256), 0, s, e);
+        hipLaunchKernelGGL(gemm5_sk_reduce_kernel, dim3((unsigned)sk_tail * 64), dim3(256), 0, s, e);
     }
 }
 
