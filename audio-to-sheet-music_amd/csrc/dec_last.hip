@@ -340,7 +340,10 @@ template <> struct Slice12<false> {
 // XCD i % 8) and share those rows through its L2.  The chunk's FO values (16 w x FT_DC rows x 2) are staged in LDS
 // and stored as FT_DC * 8 contiguous bytes per w ([item][w][row][2], the iSTFT's frame-major order) instead of one
 // 8-B store per lane and row.
-constexpr int FT_DC = 32;
+#ifndef ATHD_FT_DC
+#define ATHD_FT_DC 32
+#endif
+constexpr int FT_DC = ATHD_FT_DC;   // rows per wave chunk (A/B builds: -DATHD_FT_DC)
 
 template <bool BF>
 __global__ __launch_bounds__(256) void fdec_tail_kernel(const DecLastDesc d, int nreg) {
