@@ -30,7 +30,15 @@ namespace athd {
 
 namespace {
 
-constexpr int FR_NW = 6;             // waves per workgroup
+// waves per workgroup of fenc_row0_kernel.  8 (round 6): 4 channel-tile slots x 2 m-groups, the
+// fourth slot's waves idle in the (channel tile, m-tile) phases and share the per-m-tile phases, so every working wave
+// keeps the 6-wave form's 9 units while two 8-wave workgroups fit a CU (the 6-wave shape averaged 1.73,
+// profiles/r05_occupancy.txt; 6-wave workgroups at 128 VGPRs reach only 1.5 per CU in r05_residency.txt).
+#ifndef ATHD_F0_NW
+#define ATHD_F0_NW 8
+#endif
+constexpr int FR_NW = ATHD_F0_NW;
+static_assert(FR_NW == 6 || FR_NW == 8, "fenc_row0 wave count");
 constexpr int FR_NT = 64 * FR_NW;
 constexpr int FR_HALO = 2;           // max DConv dilation
 
@@ -156,8 +164,14 @@ ATHD_DEV void block_sum2_dpp(float& s1, float& s2, float* red) {
         red[FR_NW + w] = s2;
     }
     __syncthreads();
-    s1 = ((red[0] + red[1]) + (red[2] + red[3])) + (red[4] + red[5]);
-    s2 = ((red[FR_NW + 0] + red[FR_NW + 1]) + (red[FR_NW + 2] + red[FR_NW + 3])) + (red[FR_NW + 4] + red[FR_NW + 5]);
+    if constexpr (FR_NW == 8) {
+        s1 = ((red[0] + red[1]) + (red[2] + red[3])) + ((red[4] + red[5]) + (red[6] + red[7]));
+        s2 = ((red[FR_NW + 0] + red[FR_NW + 1]) + (red[FR_NW + 2] + red[FR_NW + 3])) +
+             ((red[FR_NW + 4] + red[FR_NW + 5]) + (red[FR_NW + 6] + red[FR_NW + 7]));
+    } else {
+        s1 = ((red[0] + red[1]) + (red[2] + red[3])) + (red[4] + red[5]);
+        s2 = ((red[FR_NW + 0] + red[FR_NW + 1]) + (red[FR_NW + 2] + red[FR_NW + 3])) + (red[FR_NW + 4] + red[FR_NW + 5]);
+    }
 }
 
 ATHD_DEV float4 ld4f(const float* p) { return *reinterpret_cast<const float4*>(p); }
@@ -202,17 +216,23 @@ __global__ __launch_bounds__(FR_NT, ATHD_F0_WPE) void fenc_row0_kernel(const Fen
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int l15 = lane & 15, l4 = lane >> 4;
-    const int ct = wave % NCT, mg = wave / NCT;
-    const int cb = ct * 16 + 4 * l4;             // first of this lane's 4 x channels
-    const int pa = 32 * ct + 4 * l4;             // packed GLU column of this lane's 'a' values (gate: pa + 16)
+    // channel-tile slot and m-group of the wave (FR_NW = 8: slot 3 holds no channel tile - those waves skip the
+    // (channel tile, m-tile) phases; ctl = the tile their addresses use, never read through)
+    constexpr int NCS = FR_NW == 8 ? 4 : NCT;
+    const int ct = wave % NCS, mg = wave / NCS;
+    const bool cwork = ct < NCT;                 // wave-uniform
+    const int ctl = cwork ? ct : NCT - 1;
+    const int cb = ctl * 16 + 4 * l4;            // first of this lane's 4 x channels
+    const int pa = 32 * ctl + 4 * l4;            // packed GLU column of this lane's 'a' values (gate: pa + 16)
 
-    // ---- input gather: chunk c = tid + 384 i -> position c / 4, taps 2 (c % 4), +1 (8 floats = 2 x 16 B)
-    float4 u[3][2];
+    // ---- input gather: chunk c = tid + FR_NT i (< 4 F0_TP) -> position c / 4, taps 2 (c % 4), +1 (8 floats = 2 x 16 B)
+    constexpr int NGC = (4 * F0_TP + FR_NT - 1) / FR_NT;
+    float4 u[NGC][2];
 #pragma unroll
-    for (int i = 0; i < 3; ++i) {
+    for (int i = 0; i < NGC; ++i) {
         const int c = tid + FR_NT * i, m = c >> 2, q = c & 3;
         const int fi = 4 * f - 2 + 2 * q;
-        if (m < T && fi >= 0 && fi + 1 < d.Fin) {
+        if (c < 4 * F0_TP && m < T && fi >= 0 && fi + 1 < d.Fin) {
             const float* p = (const float*)d.in + (((int64_t)b * T + m) * d.Fin + fi) * 4;
             u[i][0] = ld4f(p);
             u[i][1] = ld4f(p + 4);
@@ -220,7 +240,7 @@ __global__ __launch_bounds__(FR_NT, ATHD_F0_WPE) void fenc_row0_kernel(const Fen
             u[i][0] = u[i][1] = make_float4(0.f, 0.f, 0.f, 0.f);
         }
     }
-    const bf16x8_t wf = ldfrag(d.wc + (int64_t)(ct * 16 + l15) * d.wc_ld + 8 * l4);
+    const bf16x8_t wf = ldfrag(d.wc + (int64_t)(ctl * 16 + l15) * d.wc_ld + 8 * l4);
     const float4 bc = ld4f(d.bc + cb);
     const float sub = d.a_norm[2 * b], rdv = 1.0f / d.a_norm[2 * b + 1];
     if (tid < 100) gsh[tid / 50][tid % 50] = d.gram[tid / 50][tid % 50];
@@ -231,8 +251,9 @@ __global__ __launch_bounds__(FR_NT, ATHD_F0_WPE) void fenc_row0_kernel(const Fen
         *reinterpret_cast<uint4*>(&xs[row * F0_XS_P + hc * 8]) = make_uint4(0u, 0u, 0u, 0u);
     }
 #pragma unroll
-    for (int i = 0; i < 3; ++i) {
+    for (int i = 0; i < NGC; ++i) {
         const int c = tid + FR_NT * i, m = c >> 2, q = c & 3;
+        if (c >= 4 * F0_TP) break;
         const bool ok = m < T && 4 * f - 2 + 2 * q >= 0 && 4 * f - 2 + 2 * q + 1 < d.Fin;
         const float4 a = u[i][0], e = u[i][1];
         uint4 v = make_uint4(pack2bf((a.x - sub) * rdv, (a.y - sub) * rdv), pack2bf((a.z - sub) * rdv, (a.w - sub) * rdv),
@@ -245,6 +266,9 @@ __global__ __launch_bounds__(FR_NT, ATHD_F0_WPE) void fenc_row0_kernel(const Fen
 
     // ---- conv (8,1)/(4,1)/(2,0): one K-step of 32 + bias + GELU; residual stream xr in registers
     f32x4_t xr[MTW];
+#pragma unroll
+    for (int i = 0; i < MTW; ++i) xr[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    if (cwork) {
 #pragma unroll
     for (int i = 0; i < MTW; ++i) {
         const int mt = mg + 2 * i;
@@ -267,6 +291,7 @@ __global__ __launch_bounds__(FR_NT, ATHD_F0_WPE) void fenc_row0_kernel(const Fen
             st4bf(&xs[xs_off(FR_HALO + l15, cb) + mt * 16 * F0_XS_P], xr[i][0], xr[i][1], xr[i][2], xr[i][3]);
         }
     }
+    }   // cwork
     __syncthreads();
     FR_STAMP(2);
     // the conv input is dead: zero the hidden tile's K padding columns 16..31
@@ -292,6 +317,7 @@ __global__ __launch_bounds__(FR_NT, ATHD_F0_WPE) void fenc_row0_kernel(const Fen
 #pragma unroll
             for (int i = 0; i < 3; ++i) {
                 const int mt = wave + FR_NW * i;
+                if (mt >= F0_NT) break;                  // (wave-uniform; FR_NW = 8: waves 2..7 have 2 m-tiles)
                 bf16x8_t xf = ldfrag(&xs[xs_off(FR_HALO + l15 + (kok ? (tap - 1) * dil : 0), kok ? c0 : 0) + mt * 16 * F0_XS_P]);
                 if (!kok) xf = bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
                 ha[i] = mfma(w3f, xf, ha[i]);
@@ -332,6 +358,7 @@ __global__ __launch_bounds__(FR_NT, ATHD_F0_WPE) void fenc_row0_kernel(const Fen
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
             const int mt = wave + FR_NW * i;
+            if (mt >= F0_NT) break;
             FR_SCHED();
             float g[4];
 #pragma unroll
@@ -366,8 +393,8 @@ __global__ __launch_bounds__(FR_NT, ATHD_F0_WPE) void fenc_row0_kernel(const Fen
             }
         }
         // the apply pass's 1x1 weights and GroupNorm affine (issued before the reduction's barrier)
-        const bf16x8_t wa = ldfrag(d.w1[dd] + (int64_t)(32 * ct + l15) * d.w1_ld + 8 * l4);
-        const bf16x8_t wg = ldfrag(d.w1[dd] + (int64_t)(32 * ct + 16 + l15) * d.w1_ld + 8 * l4);
+        const bf16x8_t wa = ldfrag(d.w1[dd] + (int64_t)(32 * ctl + l15) * d.w1_ld + 8 * l4);
+        const bf16x8_t wg = ldfrag(d.w1[dd] + (int64_t)(32 * ctl + 16 + l15) * d.w1_ld + 8 * l4);
         const float4 ba = ld4f(d.b1[dd] + pa), bg = ld4f(d.b1[dd] + pa + 16);
         const float bav[4] = {ba.x, ba.y, ba.z, ba.w}, bgv[4] = {bg.x, bg.y, bg.z, bg.w};
         const float4 gwa = ld4f(d.g2w[dd] + pa), gba = ld4f(d.g2b[dd] + pa);
@@ -393,6 +420,7 @@ __global__ __launch_bounds__(FR_NT, ATHD_F0_WPE) void fenc_row0_kernel(const Fen
         }
         // pass 2: GroupNorm -> GLU -> LayerScale -> residual
         const int l15c = opaque_lane() & 15;
+        if (cwork) {
 #pragma unroll
         for (int i = 0; i < MTW; ++i) {
             const int mt = mg + 2 * i;
@@ -413,12 +441,13 @@ __global__ __launch_bounds__(FR_NT, ATHD_F0_WPE) void fenc_row0_kernel(const Fen
             }
             st4bf(&xs[xs_off(FR_HALO + l15c, cb) + mt * 16 * F0_XS_P], xr[i][0], xr[i][1], xr[i][2], xr[i][3]);
         }
+        }   // cwork
         __syncthreads();
         FR_STAMP(6 + 4 * dd);
     }
 
     // ---- rewrite 1x1 (C -> 2C) + GLU + freq embedding
-    {
+    if (cwork) {
         const float* br = launder(d.br);
         const uint16_t* wr = launder(d.wr);
         const float4 ba = ld4f(br + pa), bg = ld4f(br + pa + 16);
@@ -427,8 +456,8 @@ __global__ __launch_bounds__(FR_NT, ATHD_F0_WPE) void fenc_row0_kernel(const Fen
         bf16x8_t wa[2], wg[2];
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
-            wa[ks] = ldfrag(wr + (int64_t)(32 * ct + l15) * d.wr_ld + ks * 32 + 8 * l4);
-            wg[ks] = ldfrag(wr + (int64_t)(32 * ct + 16 + l15) * d.wr_ld + ks * 32 + 8 * l4);
+            wa[ks] = ldfrag(wr + (int64_t)(32 * ctl + l15) * d.wr_ld + ks * 32 + 8 * l4);
+            wg[ks] = ldfrag(wr + (int64_t)(32 * ctl + 16 + l15) * d.wr_ld + ks * 32 + 8 * l4);
         }
         const float bav[4] = {ba.x, ba.y, ba.z, ba.w};
         const float bgv[4] = {bg.x * -1.4426950408889634f, bg.y * -1.4426950408889634f, bg.z * -1.4426950408889634f,

@@ -36,4 +36,7 @@ if __name__ == "__main__":
         p = f"/tmp/same_env_{k}.npy"
         subprocess.check_call([sys.executable, __file__, "run", p], env=env)
         outs.append(np.load(p))
-    print(sys.argv[1], "vs", sys.argv[2], ":", int((outs[0] != outs[1]).sum()), "differing of", outs[0].size)
+    a, b = outs[0].astype(np.float64), outs[1].astype(np.float64)
+    sdr = 10 * np.log10(np.sum(a ** 2) / max(np.sum((a - b) ** 2), 1e-300))
+    print(sys.argv[1], "vs", sys.argv[2], ":", int((outs[0] != outs[1]).sum()), "differing of", outs[0].size,
+          f"SDR {sdr:.1f} dB")
