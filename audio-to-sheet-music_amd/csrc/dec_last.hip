@@ -616,8 +616,9 @@ __global__ __launch_bounds__(TL_NT) void tdec_tail_kernel(const DecLastDesc d) {
     // then - that hipcc's padding between the last MFMA of a chain and the LDS store of its result is too short on
     // gfx950 - does NOT hold.  Round 6 (tools/hazard/README.md, profiles/r06_hazard.txt):
     //   - probes: v_mfma_f32_16x16x4_f32 results stored after exactly N wait states, single and at the end of 12-MFMA
-    //     chains, alone and beside a matrix-saturating kernel: 0 stale in 2.6e8 lane-stores from 5 states on (hipcc
-    //     emits 9-10); the reverse order (LDS store, then an MFMA overwriting its data registers 1 state later): 0;
+    //     chains, alone and beside a matrix-saturating kernel: stale at 0 and 4 states, 0 stale in 2.6e8 lane-stores
+    //     at 9, 10 and 16 (hipcc emits 9-10); the reverse order (LDS store, then an MFMA overwriting its data registers
+    //     1 state later): 0;
     //   - builds (tools/diag_det4.py, 3 forwards each): no pad (ATHD_TDEC_PAD=0) 110 / 30 / 203 outputs differ; the pad's
     //     sched_barrier fence alone, the same instruction order as the pad build without its wait states (2): 158 / 141;
     //     the same 48 states at the kernel START instead (3): 0 / 0 / 0 / 0; no pad with ATHD_SERIAL=1: 0 / 0.
