@@ -371,8 +371,13 @@ bool dconv(Run& r, const EncW& e, void* x, int64_t nb, int64_t L, float* hbuf, u
     return fused;
 }
 
-// the fused narrow freq level (fenc_row.hip) applies: bf16 mode, C in {48, 96}, T <= 272, padded conv3 packed
-bool br_fused(const EncW& e, int Ts) { return e.dc.c3p[0].w && e.dc.c3p[1].w && fenc_row_supported(e.cin, e.cout, Ts); }
+// the fused narrow freq level (fenc_row.hip) applies: bf16 mode, C in {48, 96}, T <= 272, padded conv3 packed;
+// ATHD_FENC_ROW=0 takes the unfused implicit-GEMM + DConv path instead (parity A/B; read at every forward)
+bool br_fused(const EncW& e, int Ts) {
+    const char* v = std::getenv("ATHD_FENC_ROW");
+    if (v && *v == '0') return false;
+    return e.dc.c3p[0].w && e.dc.c3p[1].w && fenc_row_supported(e.cin, e.cout, Ts);
+}
 
 void encode(Run& r, const Dims& d, const Bufs& b, const float* wav) {
     athd_ctx* c = r.c;

@@ -445,6 +445,49 @@ def test_intermediates_f32(models, oracle_model, text_table, T):
     assert not bad, bad
 
 
+def _bf16_dump(path, shape):
+    raw = np.fromfile(path, dtype=np.uint16)
+    return (raw.astype(np.uint32) << 16).view(np.float32).reshape(shape)
+
+
+@pytest.mark.parametrize("T,B", [(44100, 2), (264600, 1)])
+def test_encoder_levels_bf16_stage(models, oracle_model, text_table, monkeypatch, T, B):
+    """The bf16 encoder levels (ATHD_DUMP's raw saved{i} / saved_t{i}) against the fp32 oracle's captures, and the
+    fused narrow frequency levels (fenc_row.hip: fenc_row0_kernel as 8-wave workgroups, fenc_row1_kernel) against the
+    unfused implicit-GEMM + DConv path (ATHD_FENC_ROW=0) at the same inputs.  Tspec = 44 and 259 (the bench rows)."""
+    from athd.synth import synthetic_batch
+    wav = torch.as_tensor(synthetic_batch(B, T, seed0=23))
+    te = torch.as_tensor(text_table[:B])
+    cap = {}
+    oracle_model.forward(wav, te, capture=cap)
+    prompts = ["drums", "bass"][:B]
+    dumps = {}
+    for fused in ("1", "0"):
+        monkeypatch.setenv("ATHD_FENC_ROW", fused)
+        with tempfile.TemporaryDirectory() as tmp:
+            monkeypatch.setenv("ATHD_DUMP", tmp)
+            models["bf16"](wav.cuda(), prompts)
+            torch.cuda.synchronize()
+            monkeypatch.delenv("ATHD_DUMP")
+            d = {}
+            for i in range(4):
+                ref = cap["saved"][i].permute(0, 2, 3, 1).numpy()        # [B][F][Ts][C]
+                d[f"saved{i}"] = _bf16_dump(os.path.join(tmp, f"saved{i}.bf16"), ref.shape)
+                reft = cap["saved_t"][i].permute(0, 2, 1).numpy()       # [B][L][C]
+                d[f"saved_t{i}"] = _bf16_dump(os.path.join(tmp, f"saved_t{i}.bf16"), reft.shape)
+            dumps[fused] = d
+    res = {}
+    for i in range(4):
+        res[f"saved{i}"] = sdr_db(cap["saved"][i].permute(0, 2, 3, 1).numpy(), dumps["1"][f"saved{i}"])
+        res[f"saved_t{i}"] = sdr_db(cap["saved_t"][i].permute(0, 2, 1).numpy(), dumps["1"][f"saved_t{i}"])
+    for i in (0, 1):
+        res[f"saved{i}_fused_vs_unfused"] = sdr_db(dumps["0"][f"saved{i}"], dumps["1"][f"saved{i}"])
+    _report(f"encoder_levels_bf16_T{T}", res)
+    # (measured round 6: 44.5-51.5 dB vs the oracle, fused vs unfused 46.3-51.6 dB: two bf16 roundings apart)
+    bad = {k: v for k, v in res.items() if v < (42.0 if "unfused" in k else BF16_SDR_DB)}
+    assert not bad, (bad, res)
+
+
 def test_reference_decoders_stage_f32(models, state_dict):
     """The reference-owned decoders pinned at their own stage on REFERENCE-made data.
 
