@@ -287,6 +287,8 @@ int gemm5_launch(const GemmDesc& d, hipStream_t s);
 
 bool rowln_supported(const GemmDesc& d);
 int rowln_launch(const GemmDesc& d, hipStream_t s);
+bool rowln_text_enabled();
+int rowln_text_launch(const GemmDesc& d, hipStream_t s);
 #ifdef ATHD_KBENCH
 int gemm6_launch(const GemmDesc& d, hipStream_t s);
 #endif
@@ -297,7 +299,15 @@ int gemm_launch(const GemmDesc& d0, int mode, hipStream_t s) {
     if (d.act == ACT_GLU && (d.N % 32 != 0)) return -2;
     // residual projection + the next LayerNorm (rowln.hip), bf16 mode only
     if (d.ln_out) return mode == 1 && rowln_supported(d) ? rowln_launch(d, s) : -2;
-    if (d.ln_w) return mode == 1 ? gemm3_ln_launch(d, s) : -2;      // row-LayerNorm epilogue: gemm3 only
+    // row-LayerNorm epilogue (the text mlp2): rowln.hip's text form, else gemm3
+    if (d.ln_w) {
+        if (mode != 1) return -2;
+        if (rowln_text_enabled()) {
+            const int rc = rowln_text_launch(d, s);
+            if (rc != -2) return rc;
+        }
+        return gemm3_ln_launch(d, s);
+    }
     // the GroupNorm folded into the A load (a_gn_*, the transformer's last pending GroupNorm): gemm2 only; refuse
     // rather than silently skip it on another kernel
     if (d.a_gn_stats) return mode == 1 && gemm2_supported(d) ? gemm2_launch(d, s) : -2;

@@ -34,11 +34,9 @@ namespace athd {
 
 namespace {
 
-constexpr int RL_N = 512, RL_K = 512;
-constexpr int RL_KT = RL_K / 64;                 // K-tiles (A ring granularity)
-constexpr int RL_KS = RL_K / 32;                 // K-steps (MFMA K, B double-buffer granularity)
+constexpr int RL_N = 512, RL_K = 512;           // the out_proj shape
+constexpr int RT_N = 384, RT_K = 384;           // the text cross-attention's mlp2 shape (TEXT)
 constexpr int RL_NS = 3;                         // A ring depth
-constexpr int RL_PAR = 6 * RL_N;                 // bias, scale, gn_w, gn_b, ln_w, ln_b
 typedef __attribute__((address_space(3))) void rl_lds_void;
 typedef __attribute__((address_space(1))) void rl_gbl_void;
 __device__ __attribute__((aligned(64))) uint4 g_zero_rl[4];
@@ -51,9 +49,10 @@ ATHD_DEV void rl_wait_vm() {
 // The VM issue schedule of the K-loop, for the counted waits (every count is the number of VM operations issued AFTER
 // the one waited for).  Prologue: B(0) (TN loads), A(0), A(1) (AQ DMAs each).  K-step ks: B(ks + 1), then at even ks
 // A(ks / 2 + 2).
-template <int TN, int AQ>
+template <int KS, int TN, int AQ>
 struct RlSched {
-    static constexpr int step(int ks) { return (ks + 1 < RL_KS ? TN : 0) + ((ks % 2 == 0 && ks / 2 + 2 < RL_KT) ? AQ : 0); }
+    static constexpr int KT = KS / 2;
+    static constexpr int step(int ks) { return (ks + 1 < KS ? TN : 0) + ((ks % 2 == 0 && ks / 2 + 2 < KT) ? AQ : 0); }
     static constexpr int through(int ks) {       // issued by the end of step ks's issue block
         int n = TN + 2 * AQ;
         for (int k = 0; k <= ks; ++k) n += step(k);
@@ -76,16 +75,27 @@ struct RlSched {
 #ifndef ATHD_RL_RD
 #define ATHD_RL_RD 2
 #endif
+#ifndef ATHD_RL_PROBE
+#define ATHD_RL_PROBE 0      // ablations for A/B builds only (outputs garbage): 1 = K-loop only (no epilogue), 2 = no MFMAs
+#endif
 
-template <int BM, int NW>
+// TEXT: the text cross-attention's mlp2 + norm_out (ATHTDemucs_v2.py:47-49; gemm3_epilogue_ln's epilogue, N = K = 384):
+// v = res[item / res_div][row] + (acc + bias + pbias[item]), LayerNorm over the row, bf16 to C; nothing else stored.
+// Per-column parameter slots in LDS: 0 bias, 1 / 2 res_scale / res_gn_w (out_proj) or the pbias rows of the tile's
+// two items (TEXT), 3 res_gn_b, 4 / 5 ln_w / ln_b.
+template <int BM, int NW, int N, int K, bool TEXT>
 __global__ __launch_bounds__(64 * NW, 2) void rowln_kernel(const GemmDesc d) {
     constexpr int NT = 64 * NW;
+    constexpr int RL_N = N, RL_K = K;
+    constexpr int RL_KT = K / 64, RL_KS = K / 32;
+    constexpr int RL_PAR = 6 * N;
     constexpr int TM = BM / 16, TN = RL_N / NW / 16;
     constexpr int STAGE = BM * 128;
     constexpr int AP = BM / 8;                   // 1-KB A pieces (8 rows) per K-tile
     constexpr int AQ = (AP + NW - 1) / NW;       // A DMAs per wave per K-tile (surplus pieces: zero page -> sink)
-    static_assert(AP * 8 == BM && BM % 16 == 0 && TN * 16 * NW == RL_N, "tile shape");
-    using S = RlSched<TN, AQ>;
+    static_assert(AP * 8 == BM && BM % 16 == 0 && TN * 16 * NW == RL_N && K % 64 == 0, "tile shape");
+    static_assert(RL_KS == 16 || RL_KS == 12, "K-steps below");
+    using S = RlSched<RL_KS, TN, AQ>;
     __shared__ __attribute__((aligned(1024))) char ring[RL_NS * STAGE];
     __shared__ __attribute__((aligned(16))) float par[RL_PAR];
     __shared__ __attribute__((aligned(16))) float red[2][BM][NW];
@@ -95,6 +105,7 @@ __global__ __launch_bounds__(64 * NW, 2) void rowln_kernel(const GemmDesc d) {
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int l15 = lane & 15, l4 = lane >> 4;
     const uint32_t M = (uint32_t)d.nb * d.H_out;
+    const uint32_t rpb = (uint32_t)d.H_out;      // rows per batch (item)
     const int ntm = (int)((M + BM - 1) / BM);
     // XCD-aware: workgroup i runs on XCD i % 8; each XCD takes a contiguous range of row tiles
     int tile;
@@ -103,15 +114,26 @@ __global__ __launch_bounds__(64 * NW, 2) void rowln_kernel(const GemmDesc d) {
         tile = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (int)blockIdx.x / 8;
     }
     if (tile >= ntm) return;
-    const uint32_t m0 = (uint32_t)tile * BM;
+    // (TEXT, measured: per-item tiles with the res_div prompts of a segment's rows adjacent, so that one XCD's L2
+    // serves the shared residual rows: the kernel 0.49 -> 0.47 ms, the whole step 1.9 % slower, 3 alternating pairs)
+    const uint32_t m0 = (uint32_t)tile * BM, Mend = M;      // the tile's rows [m0, Mend)
     const int n0 = TN * 16 * wave;               // this wave's columns
 
     // ---- per-column parameters -> LDS (published by the K-loop's first barrier) ----
+    const uint32_t b0 = m0 / rpb;
+    const uint32_t b1 = (b0 + 1) * rpb < M ? b0 + 1 : b0;   // the tile's second batch (H_out >= BM: at most two)
     for (int i = tid; i < RL_PAR; i += NT) {
         const int k = i / RL_N, n = i % RL_N;
-        const float* src = k == 0 ? d.bias : k == 1 ? d.res_scale : k == 2 ? d.res_gn_w : k == 3 ? d.res_gn_b
-                                                                     : k == 4 ? d.ln_w : d.ln_b;
-        par[i] = src ? src[n] : (k == 1 ? 1.f : 0.f);
+        if constexpr (TEXT) {
+            const float* src = k == 0 ? d.bias : k == 1 ? (d.pbias ? d.pbias + (int64_t)b0 * RL_N : nullptr)
+                             : k == 2 ? (d.pbias ? d.pbias + (int64_t)b1 * RL_N : nullptr) : k == 3 ? nullptr
+                             : k == 4 ? d.ln_w : d.ln_b;
+            par[i] = src ? src[n] : 0.f;
+        } else {
+            const float* src = k == 0 ? d.bias : k == 1 ? d.res_scale : k == 2 ? d.res_gn_w : k == 3 ? d.res_gn_b
+                                                                         : k == 4 ? d.ln_w : d.ln_b;
+            par[i] = src ? src[n] : (k == 1 ? 1.f : 0.f);
+        }
     }
 
     // ---- operand streams ----
@@ -121,7 +143,7 @@ __global__ __launch_bounds__(64 * NW, 2) void rowln_kernel(const GemmDesc d) {
 #pragma unroll
     for (int q = 0; q < AQ; ++q) {
         const uint32_t m = m0 + 8 * (wave + NW * q) + lrow;
-        arow[q] = m < M && wave + NW * q < AP ? (const char*)d.A + ((int64_t)m * RL_K + 8 * chunk) * 2 : nullptr;
+        arow[q] = m < Mend && wave + NW * q < AP ? (const char*)d.A + ((int64_t)m * RL_K + 8 * chunk) * 2 : nullptr;
     }
     auto dma_a = [&](int kt) {
         char* dst = ring + (kt % RL_NS) * STAGE;
@@ -180,26 +202,36 @@ __global__ __launch_bounds__(64 * NW, 2) void rowln_kernel(const GemmDesc d) {
         for (int i = 0; i < TM; ++i) asm volatile("" : "+v"(af[i]));                                              \
         for (int i = 0; i < TM; ++i)                                                                               \
             for (int j = 0; j < TN; ++j)                                                                           \
+                if constexpr (ATHD_RL_PROBE != 2)                                                                  \
                 acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[(ks) & 1][j], af[i], acc[i][j], 0, 0, 0);   \
         if constexpr (s == 1 && kt + 1 < RL_KT) {                                                                  \
             rl_wait_vm<S::wait_a(ks)>();         /* A(kt + 1) landed (this wave's pieces) ...                  */  \
             __builtin_amdgcn_s_barrier();        /* ... and every wave's; slot kt % 3 is free for A(kt + 3)     */  \
         }                                                                                                          \
     }
-    static_assert(RL_KS == 16, "16 K-steps below");
     RL_KSTEP(0) RL_KSTEP(1) RL_KSTEP(2) RL_KSTEP(3) RL_KSTEP(4) RL_KSTEP(5) RL_KSTEP(6) RL_KSTEP(7)
-    RL_KSTEP(8) RL_KSTEP(9) RL_KSTEP(10) RL_KSTEP(11) RL_KSTEP(12) RL_KSTEP(13) RL_KSTEP(14) RL_KSTEP(15)
+    RL_KSTEP(8) RL_KSTEP(9) RL_KSTEP(10) RL_KSTEP(11)
+    if constexpr (RL_KS == 16) {
+        RL_KSTEP(12) RL_KSTEP(13) RL_KSTEP(14) RL_KSTEP(15)
+    }
 #undef RL_KSTEP
 #undef load_b
     rl_wait_vm<0>();                             // (nothing the compiler does not know of stays in flight)
+    if constexpr (ATHD_RL_PROBE == 1) {          // keep the accumulators live, store nothing
+        float t = 0.f;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) t += acc[i][j][0] + acc[i][j][3];
+        if (t == 1234.5f) ((float*)d.res)[m0] = t;
+        return;
+    }
 
     // ---- epilogue 1: X = res' + scale * (acc + bias), stored; acc keeps X ----
     // the pending GroupNorm's (mean, rstd) of the tile's first batch and the next (a tile spans at most two batches:
     // H_out >= BM rows per batch, rowln_supported)
-    const uint32_t rpb = (uint32_t)d.H_out;
-    const uint32_t b0 = m0 / rpb;
     float gm0 = 0.f, gr0 = 1.f, gm1 = 0.f, gr1 = 1.f;
-    const bool rgn = d.res_gn_stats != nullptr;
+    const bool rgn = !TEXT && d.res_gn_stats != nullptr;
     if (rgn) {
         const uint32_t blast = (M - 1) / rpb;
         gn_params(d.res_gn_stats, b0, d.res_gn_count, gm0, gr0);
@@ -212,11 +244,18 @@ __global__ __launch_bounds__(64 * NW, 2) void rowln_kernel(const GemmDesc d) {
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
         const uint32_t m = m0 + 16 * i + l15;
-        rb[i] = (int64_t)(m < M ? m : M - 1) * RL_N + cl;
+        const uint32_t mm = m < Mend ? m : Mend - 1;
+        if constexpr (TEXT) {                    // the segment's residual row, shared by its res_div prompts
+            const uint32_t b = mm / rpb;
+            rb[i] = (d.res_div > 1 ? (int64_t)(b / (uint32_t)d.res_div) * d.res_bs : (int64_t)b * rpb * RL_N) +
+                    (int64_t)(mm - b * rpb) * RL_N + cl;
+        } else {
+            rb[i] = (int64_t)mm * RL_N + cl;
+        }
     }
-    // residual pieces of 4 fragment columns (16 rows x 64 columns of the wave), RD pieces in flight ahead of the one
-    // being used: a whole row tile ahead (TN float4s per lane twice) spilled accumulators
-    constexpr int PC = 4, NPC = TN / PC, NP = TM * NPC, RD = ATHD_RL_RD;
+    // residual pieces of 4 (3) fragment columns (16 rows x 64 (48) columns of the wave), RD pieces in flight ahead of
+    // the one being used: a whole row tile ahead (TN float4s per lane twice) spilled accumulators
+    constexpr int PC = TN % 4 == 0 ? 4 : TN % 3 == 0 ? 3 : 1, NPC = TN / PC, NP = TM * NPC, RD = ATHD_RL_RD;
     static_assert(TN % PC == 0, "residual pieces");
     float4 rr[RD + 1][PC];
     auto load_piece = [&](int p, float4 (&dst)[PC]) {
@@ -242,8 +281,17 @@ __global__ __launch_bounds__(64 * NW, 2) void rowln_kernel(const GemmDesc d) {
             const int j = j0 + jj;
             const int c = cl + 16 * j;
             const float4 bi = *reinterpret_cast<const float4*>(&par[c]);
-            const float4 sc = *reinterpret_cast<const float4*>(&par[RL_N + c]);
             float4 r = rr[p % (RD + 1)][jj];
+            if constexpr (TEXT) {                // v = res + (acc + bias + pbias), gemm3_epilogue_ln's order
+                const float4 pb = *reinterpret_cast<const float4*>(&par[(second ? 2 : 1) * RL_N + c]);
+                acc[i][j][0] = r.x + (acc[i][j][0] + bi.x + pb.x);
+                acc[i][j][1] = r.y + (acc[i][j][1] + bi.y + pb.y);
+                acc[i][j][2] = r.z + (acc[i][j][2] + bi.z + pb.z);
+                acc[i][j][3] = r.w + (acc[i][j][3] + bi.w + pb.w);
+                sum += (acc[i][j][0] + acc[i][j][1]) + (acc[i][j][2] + acc[i][j][3]);
+                continue;
+            }
+            const float4 sc = *reinterpret_cast<const float4*>(&par[RL_N + c]);
             if (rgn) {
                 const float4 gw = *reinterpret_cast<const float4*>(&par[2 * RL_N + c]);
                 const float4 gb = *reinterpret_cast<const float4*>(&par[3 * RL_N + c]);
@@ -256,7 +304,7 @@ __global__ __launch_bounds__(64 * NW, 2) void rowln_kernel(const GemmDesc d) {
             acc[i][j][1] = r.y + sc.y * (acc[i][j][1] + bi.y);
             acc[i][j][2] = r.z + sc.z * (acc[i][j][2] + bi.z);
             acc[i][j][3] = r.w + sc.w * (acc[i][j][3] + bi.w);
-            if (m < M)
+            if (m < Mend)
                 *reinterpret_cast<float4*>(X + rb[i] + 16 * j) =
                     make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
             sum += (acc[i][j][0] + acc[i][j][1]) + (acc[i][j][2] + acc[i][j][3]);
@@ -305,12 +353,12 @@ __global__ __launch_bounds__(64 * NW, 2) void rowln_kernel(const GemmDesc d) {
         for (int i = 0; i < TM; ++i) red[1][16 * i + l15][wave] = rs[i];
     }
     __syncthreads();
-    bf16_t* Hout = (bf16_t*)d.ln_out;
+    bf16_t* Hout = (bf16_t*)(TEXT ? d.C : d.ln_out);
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
         const float rstd = 1.f / sqrtf(row_total(1, 16 * i + l15) * (1.f / RL_N) + 1e-5f);
         const uint32_t m = m0 + 16 * i + l15;
-        if (m >= M) continue;
+        if (m >= Mend) continue;
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
             const int c = cl + 16 * j;
@@ -354,7 +402,40 @@ int rowln_launch(const GemmDesc& d, hipStream_t s) {
         ks.begin("rowln_kernel", 2.0 * M * RL_N * RL_K,
                  (double)M * RL_K * 2 + (double)RL_N * RL_K * 2 + (double)M * RL_N * (4 + 4 + 2));
     }
-    hipLaunchKernelGGL((rowln_kernel<RL_BM, RL_NW>), dim3((unsigned)ntm), dim3(64 * RL_NW), 0, s, d);
+    hipLaunchKernelGGL((rowln_kernel<RL_BM, RL_NW, RL_N, RL_K, false>), dim3((unsigned)ntm), dim3(64 * RL_NW), 0, s, d);
+    return (int)hipGetLastError();
+}
+
+// The text cross-attention's mlp2 + norm_out (gemm_launch's F_LN route; round 6): the gemm3 form (128 x 384 tiles,
+// A and B through a 2-stage LDS ring of 64-KB K-tiles) ran at 2 TB/s, 26 % of its HBM floor - each 128-row tile
+// streamed all 288 KB of weights through LDS one K-tile ahead.  Here the weights go L2 -> VGPR per wave (48 columns
+// each, one K-step ahead) and only A is staged, 3 deep.  ATHD_RLT=0 keeps the gemm3 form (A/B, tested).
+bool rowln_text_enabled() {                     // (read at every launch: the tests switch it between forwards)
+    const char* e = getenv("ATHD_RLT");
+    return !(e && e[0] == '0');
+}
+
+bool rowln_text_supported(const GemmDesc& d) {
+    return d.ln_w && d.ln_b && !d.ln_out && d.a_bf16 && d.N == RT_N && d.K == RT_K && d.Kp >= RT_K && d.Kp % 8 == 0 &&
+           d.C_in == RT_K && d.a_ld == RT_K && d.ntaps == 1 && d.W == 1 && d.H_in == d.H_out && d.res && !d.res_bf16 &&
+           d.c_bf16 && d.store && d.ldo == RT_N && d.col_off == 0 && d.act == ACT_NONE && !d.stats && !d.gn_stats &&
+           !d.res_scale && !d.res_gn_stats && !d.row_add && !d.col_split && d.o_stride == 1 && d.o_off == 0 &&
+           d.H_out_total == d.H_out && d.c_bs < 0 && d.pfold <= 1 && d.H_out >= RL_BM && d.res_div >= 1 &&
+           (d.res_div == 1 || d.res_bs >= (int64_t)d.H_out * RT_N) && !d.a_norm && !d.a_gn_stats && d.a_bs < 0 &&
+           d.a_hs < 0;
+}
+
+int rowln_text_launch(const GemmDesc& d, hipStream_t s) {
+    if (!rowln_text_supported(d)) return -2;
+    const int64_t M = (int64_t)d.nb * d.H_out;
+    const int ntm = (int)((M + RL_BM - 1) / RL_BM);
+    KScope ks(s);
+    if (ks.on()) {
+        double fl, by;
+        gemm_work(d, 1, fl, by);
+        ks.begin("rowln_kernel<text>", fl, by);
+    }
+    hipLaunchKernelGGL((rowln_kernel<RL_BM, RL_NW, RT_N, RT_K, true>), dim3((unsigned)ntm), dim3(64 * RL_NW), 0, s, d);
     return (int)hipGetLastError();
 }
 
