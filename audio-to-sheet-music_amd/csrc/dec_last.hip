@@ -345,8 +345,11 @@ template <> struct Slice12<false> {
 #endif
 constexpr int FT_DC = ATHD_FT_DC;   // rows per wave chunk (A/B builds: -DATHD_FT_DC)
 
+#ifndef ATHD_FT_LB
+#define ATHD_FT_LB 4         // the bf16 form at 4 waves per SIMD (A/B: 0 = the compiler's choice, 130 VGPRs, 3 waves)
+#endif
 template <bool BF>
-__global__ __launch_bounds__(256) void fdec_tail_kernel(const DecLastDesc d, int nreg) {
+__global__ __launch_bounds__(256, BF && ATHD_FT_LB > 0 ? ATHD_FT_LB : 1) void fdec_tail_kernel(const DecLastDesc d, int nreg) {
     __shared__ __attribute__((aligned(16))) float2 ost[4][16][FT_DC + 1];
     // 1-D block index -> (segment region g, prompt): XCD x runs regions g = x, x + 8, ... with the P prompts of each
     // back to back
