@@ -353,10 +353,7 @@ __global__ __launch_bounds__(256) void fdec_lr_stats3_kernel(const LowRankDesc d
 // v3 merge pass (bf16 mode, strict upsampling Hd > Hs, Hk, H_skip): the one-new-row updates and next-row prefetches
 // of fdec_lr_stats3_kernel for the Z / Zs rows (taps 0, 3, 4, 7) and the skip2 rows, and the first / last steps
 // peeled so that the step loop carries no per-step conditions besides the row changes.
-#ifndef ATHD_LR3_LB
-#define ATHD_LR3_LB 0        // A/B: > 0 = waves per SIMD (__launch_bounds__), 0 = the compiler's choice
-#endif
-__global__ __launch_bounds__(256, ATHD_LR3_LB > 0 ? ATHD_LR3_LB : 1) void fdec_lr_merge3_kernel(const LowRankDesc d) {
+__global__ __launch_bounds__(256) void fdec_lr_merge3_kernel(const LowRankDesc d) {
     const LrThread th = lr_thread(d);
     if (!th.active) return;
     constexpr int NT = 4;

@@ -821,11 +821,8 @@ __global__ __launch_bounds__(256) void dec_merge_kernel(const MergeDesc d) {
 // at once), the skip rows once per segment.  Same arithmetic as dec_merge_kernel, value for value.
 constexpr int DM_RUN = 16;
 
-#ifndef ATHD_MW1_LB
-#define ATHD_MW1_LB 0        // A/B: > 0 = the bf16 form's waves per SIMD (__launch_bounds__), 0 = the compiler's choice
-#endif
 template <int P, int PP, bool FAST>
-__global__ __launch_bounds__(256, FAST && ATHD_MW1_LB > 0 ? ATHD_MW1_LB : 1) void dec_merge_w1_kernel(const MergeDesc d) {
+__global__ __launch_bounds__(256) void dec_merge_w1_kernel(const MergeDesc d) {
     const int64_t seg = blockIdx.y;
     const int cv = d.C / 8;
     const int t = blockIdx.x * 256 + threadIdx.x;
