@@ -490,6 +490,13 @@ typedef __attribute__((address_space(1))) void a32_gbl_void;
 #define ATHD_ATTN_V6 1
 #endif
 constexpr float A32_SUMCHK = 1024.0f;               // max lane row sum of a tile before the exact-max rescale
+// First tile (round 6, late): the exact max is taken over the scores already in registers and subtracted from them in
+// place (32 v_sub) instead of running QK^T again from -m (8 MFMAs + 32 v_mov + the K re-read): attention 3.50 ->
+// 3.45 ms per forward, whole step +0.5-0.7 % (3 alternating pairs); outputs 57 dB from the recomputed form (bf16 P
+// rounding of last-bit score differences).  0 builds the recomputing form for A/B.
+#ifndef ATHD_ATTN_T0SUB
+#define ATHD_ATTN_T0SUB 1
+#endif
 #ifndef ATHD_ATTN_KM
 #define ATHD_ATTN_KM 0        // 1: the running max subtracted by a fifth QK^T k-step (A/B)
 #endif
@@ -791,7 +798,15 @@ __global__ __launch_bounds__(256, MINW) void attn32_kernel(const AttnDesc d) {
 #endif
             if (t == 0) {                                          // first tile: the exact max (O and l are zero)
                 set_max(tile_max());
+#if ATHD_ATTN_T0SUB && !ATHD_ATTN_KM
+                // the scores already in registers, shifted by the max (instead of QK^T again from -m)
+#pragma unroll
+                for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) sc[kb][i] -= mrun;
+#else
                 ATHD_A32_QKX();
+#endif
             }
             float ls = exp_sum();
             if (__any(!(ls <= A32_SUMCHK))) {                      // some P > A32_SUMCHK (or not finite): rescale
@@ -1185,11 +1200,19 @@ __global__ __launch_bounds__(512, 1) void attn_pp_kernel(const AttnDesc d) {
             };
             mask_tail(kt0);
             if (t == 0) {                                      // first tile: the exact max (O and l are zero)
+#if ATHD_ATTN_T0SUB
+                mrun = tile_max();                             // (attn32_kernel's form: the scores shifted in place)
+#pragma unroll
+                for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) sc[kb][i] -= mrun;
+#else
                 with_kt([&]() {
                     mrun = tile_max();
                     qk(-mrun);
                     mask_tail(kt0);
                 });
+#endif
             }
             float ls = exp_sum();
             if (__any(!(ls <= A32_SUMCHK))) {                  // some P > A32_SUMCHK (or not finite): rescale
